@@ -1,0 +1,112 @@
+"""ctypes binding of the C oracle (oracle/build/liboracle.so) -- TEST INFRASTRUCTURE ONLY.
+
+Loaded only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the
+checker / CPU baseline.  Never by the product package.  Parity unpinned by the reference
+(LICENSE-only snapshot); pinned against the Python spec's golden fixtures in tests/golden.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+CURVE_IDS = {"bls12_381": 0, "bn254": 1}
+FP_BYTES = {"bls12_381": 48, "bn254": 32}
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        c = ctypes
+        L.kzgo_batch_verify.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p,
+                                        c.c_size_t, c.c_char_p, c.c_char_p, c.c_char_p,
+                                        c.POINTER(c.c_int), c.c_char_p, c.c_char_p]
+        L.kzgo_msm_g1.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_size_t, c.c_char_p]
+        L.kzgo_g1_mul_gen.argtypes = [c.c_int, c.c_char_p, c.c_size_t, c.c_char_p]
+        L.kzgo_pairing.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p]
+        L.kzgo_g2_mul.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p]
+        L.kzgo_randomizer_bytes.argtypes = [c.c_char_p, c.c_uint64, c.c_char_p]
+        L.kzgo_sha256.argtypes = [c.c_char_p, c.c_char_p, c.c_size_t]
+        L.kzgo_set_threads.argtypes = [c.c_int]
+        L.kzgo_get_threads.restype = c.c_int
+        _lib = L
+    return _lib
+
+
+class OracleError(RuntimeError):
+    def __init__(self, code):
+        super().__init__("oracle error %d" % code)
+        self.code = code
+
+
+def _check(rc):
+    if rc != 0:
+        raise OracleError(rc)
+
+
+def set_threads(n: int):
+    lib().kzgo_set_threads(int(n))
+
+
+def threads() -> int:
+    return lib().kzgo_get_threads()
+
+
+def batch_verify(curve, commitments: bytes, zs: bytes, ys: bytes, proofs: bytes, n: int,
+                 g2: bytes, tau_g2: bytes, seed: bytes, want_ab=False):
+    g1b = 2 * FP_BYTES[curve]
+    ok = ctypes.c_int(-1)
+    a = ctypes.create_string_buffer(g1b)
+    b = ctypes.create_string_buffer(g1b)
+    _check(lib().kzgo_batch_verify(CURVE_IDS[curve], commitments, zs, ys, proofs, n, g2, tau_g2,
+                                   seed, ctypes.byref(ok), a, b))
+    if want_ab:
+        return bool(ok.value), a.raw, b.raw
+    return bool(ok.value)
+
+
+def msm_g1(curve, points: bytes, scalars: bytes, n: int) -> bytes:
+    out = ctypes.create_string_buffer(2 * FP_BYTES[curve])
+    _check(lib().kzgo_msm_g1(CURVE_IDS[curve], points, scalars, n, out))
+    return out.raw
+
+
+def g1_mul_gen(curve, scalars: bytes, n: int) -> bytes:
+    out = ctypes.create_string_buffer(max(1, n * 2 * FP_BYTES[curve]))
+    _check(lib().kzgo_g1_mul_gen(CURVE_IDS[curve], scalars, n, out))
+    return out.raw[: n * 2 * FP_BYTES[curve]]
+
+
+def pairing(curve, g1: bytes, g2: bytes) -> bytes:
+    out = ctypes.create_string_buffer(12 * FP_BYTES[curve])
+    _check(lib().kzgo_pairing(CURVE_IDS[curve], g1, g2, out))
+    return out.raw
+
+
+def g2_mul(curve, q: bytes, k: int) -> bytes:
+    out = ctypes.create_string_buffer(4 * FP_BYTES[curve])
+    _check(lib().kzgo_g2_mul(CURVE_IDS[curve], q, int(k).to_bytes(32, "big"), out))
+    return out.raw
+
+
+def randomizer(seed: bytes, i: int) -> int:
+    out = ctypes.create_string_buffer(32)
+    lib().kzgo_randomizer_bytes(seed, i, out)
+    return int.from_bytes(out.raw, "big")
+
+
+def sha256(msg: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().kzgo_sha256(out, msg, len(msg))
+    return out.raw
