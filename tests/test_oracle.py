@@ -1,0 +1,120 @@
+"""C oracle vs the golden fixtures produced by the independent Python spec (CPU only).
+
+Pins the oracle before it is trusted as the checker for the HIP path (task rule 3).
+Parity against the reference itself is unpinned: the reference holds no code or vectors.
+"""
+import hashlib
+import random
+
+import pytest
+
+from oracle import oracle as O
+from oracle.pyspec import curves as pc
+from oracle.pyspec import kzg as pk
+
+CURVES = ["bls12_381", "bn254"]
+SIZES = {"bls12_381": [4, 16, 256], "bn254": [4, 16, 64]}
+
+
+def h(x):
+    return bytes.fromhex(x)
+
+
+def test_sha256_and_randomizers():
+    for m in [b"", b"abc", bytes(range(55)), bytes(range(56)), bytes(range(64)), bytes(200)]:
+        assert O.sha256(m) == hashlib.sha256(m).digest()
+    seed = bytes(range(32))
+    for i in [0, 1, 2, 1 << 20, (1 << 63) + 5]:
+        assert O.randomizer(seed, i) == pk.randomizer(seed, i)
+        assert 0 < O.randomizer(seed, i) < 1 << 127
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_pairing_kat(curve, golden):
+    g = golden("%s_pairing.json" % curve)
+    assert O.pairing(curve, h(g["g1"]), h(g["g2"])).hex() == g["e_g1_g2"]
+    assert O.pairing(curve, h(g["aP"]), h(g["bQ"])).hex() == g["e_aP_bQ"]
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_msm_golden(curve, golden):
+    g = golden("%s_msm.json" % curve)
+    for case in g["cases"]:
+        got = O.msm_g1(curve, h(case["points"]), h(case["scalars"]), case["n"])
+        assert got.hex() == case["expected"], case["name"]
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_batch_golden(curve, golden):
+    for n in SIZES[curve]:
+        g = golden("%s_batch_n%d.json" % (curve, n))
+        for key in ["valid", "neg_flip_y", "neg_swap_proofs"]:
+            src = g if key == "valid" else g[key]
+            exp = g[key]
+            ok, A, B = O.batch_verify(curve, h(src["commitments"]), h(src["zs"]), h(src["ys"]),
+                                      h(src["proofs"]), n, h(g["g2"]), h(g["tau_g2"]), h(g["seed"]),
+                                      want_ab=True)
+            assert ok == exp["ok"], (n, key)
+            assert A.hex() == exp["A"], (n, key)
+            assert B.hex() == exp["B"], (n, key)
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_genuine_kzg(curve, golden):
+    g = golden("%s_genuine_kzg.json" % curve)
+    ok = O.batch_verify(curve, h(g["commitments"]), h(g["zs"]), h(g["ys"]), h(g["proofs"]), g["n"],
+                        h(g["g2"]), h(g["tau_g2"]), h(g["seed"]))
+    assert ok is True
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_empty_batch_and_errors(curve, golden):
+    g = golden("%s_batch_n4.json" % curve)
+    assert O.batch_verify(curve, b"", b"", b"", b"", 0, h(g["g2"]), h(g["tau_g2"]), h(g["seed"]))
+    C = pc.CURVES[curve]
+    # non-canonical scalar -> error code, not ok=0
+    zs = bytearray(h(g["zs"]))
+    zs[0:32] = (C.r).to_bytes(32, "big")
+    with pytest.raises(O.OracleError) as e:
+        O.batch_verify(curve, h(g["commitments"]), bytes(zs), h(g["ys"]), h(g["proofs"]), 4,
+                       h(g["g2"]), h(g["tau_g2"]), h(g["seed"]))
+    assert e.value.code == -4
+    # off-curve commitment
+    cm = bytearray(h(g["commitments"]))
+    cm[2 * C.fp_bytes - 1] ^= 1
+    with pytest.raises(O.OracleError) as e:
+        O.batch_verify(curve, bytes(cm), h(g["zs"]), h(g["ys"]), h(g["proofs"]), 4,
+                       h(g["g2"]), h(g["tau_g2"]), h(g["seed"]))
+    assert e.value.code == -3
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_msm_discrete_log_identity(curve):
+    """MSM(k_i G, s_i) == (sum k_i s_i) G: size-independent known-answer identity."""
+    C = pc.CURVES[curve]
+    rng = random.Random(11)
+    n = 3000
+    ks = [rng.randrange(C.r) for _ in range(n)]
+    ss = [rng.randrange(C.r) for _ in range(n)]
+    pts = O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(k) for k in ks), n)
+    got = O.msm_g1(curve, pts, b"".join(pk.fr_to_bytes(s) for s in ss), n)
+    tot = sum(k * s for k, s in zip(ks, ss)) % C.r
+    assert got == O.g1_mul_gen(curve, pk.fr_to_bytes(tot), 1)
+
+
+def test_sharded_msm_equals_unsharded():
+    """The multi-GPU decomposition (split the point range, add partials) on the oracle."""
+    curve = "bls12_381"
+    C = pc.CURVES[curve]
+    rng = random.Random(3)
+    n = 700
+    ks = [rng.randrange(C.r) for _ in range(n)]
+    ss = [rng.randrange(C.r) for _ in range(n)]
+    pts = O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(k) for k in ks), n)
+    scs = b"".join(pk.fr_to_bytes(s) for s in ss)
+    full = pk.g1_from_bytes(O.msm_g1(curve, pts, scs, n), C)
+    acc = None
+    for lo, hi in [(0, 100), (100, 350), (350, 351), (351, 700)]:
+        part = O.msm_g1(curve, pts[lo * 96:hi * 96], scs[lo * 32:hi * 32], hi - lo)
+        acc = pc.g1_add(acc, pk.g1_from_bytes(part, C), C)
+    assert acc == full
