@@ -1,0 +1,260 @@
+// Montgomery prime-field arithmetic for gfx950 (CDNA4), 32-bit limbs in VGPRs.
+//
+// Hot-path layer L1 of SURVEY.md section 1 ("Fp<Params> Montgomery mul/sqr/add ... in
+// registers", BASELINE.json:5).  Reference: none -- /root/reference holds only LICENSE
+// (LICENSE:1-201); the semantics are fixed by oracle/pyspec and checked against the C oracle.
+//
+// Design notes (MI355X):
+//  * Limbs are 32-bit so every limb product is one v_mad_u64_u32 (32x32+64 -> 64); measured
+//    ~27 T mad/s chip-wide on MI355X (scratch/ubench.hip), i.e. the multiply pipe, not HBM,
+//    bounds every kernel built on this (SURVEY.md section 7 "the real roofline is not HBM").
+//  * Multiplication is CIOS with the "no-carry" shortcut: every modulus used here has its
+//    top limb < 0x7ffffffe (BLS12-381 p/r, BN254 p/r), so the t[N]/t[N+1] words of textbook
+//    CIOS are never needed and the loop keeps N+0 words live.
+//  * Carry chains use __builtin_addc/__builtin_subc -> v_add_co_u32 / v_addc_co_u32.
+//  * Everything is fully unrolled with compile-time limb indices so the limbs stay in VGPRs
+//    (runtime-indexed arrays would go to scratch: cdna_hip_programming.md 5.4 rule 20).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#define KZ_DEV __device__ __forceinline__
+
+namespace kzgmi {
+
+template <class P>
+struct Fp {
+  static constexpr int N = P::N;
+  uint32_t v[N];
+
+  KZ_DEV static Fp zero() { Fp r; _Pragma("unroll") for (int i = 0; i < N; ++i) r.v[i] = 0; return r; }
+  KZ_DEV static Fp one() { Fp r; _Pragma("unroll") for (int i = 0; i < N; ++i) r.v[i] = P::ONE[i]; return r; }
+  KZ_DEV static Fp from_const(const uint32_t (&c)[N]) { Fp r; _Pragma("unroll") for (int i = 0; i < N; ++i) r.v[i] = c[i]; return r; }
+  KZ_DEV bool is_zero() const {
+    uint32_t x = 0;
+    _Pragma("unroll") for (int i = 0; i < N; ++i) x |= v[i];
+    return x == 0;
+  }
+  KZ_DEV bool operator==(const Fp& o) const {
+    uint32_t x = 0;
+    _Pragma("unroll") for (int i = 0; i < N; ++i) x |= v[i] ^ o.v[i];
+    return x == 0;
+  }
+  KZ_DEV bool operator!=(const Fp& o) const { return !(*this == o); }
+};
+
+// ---------------------------------------------------------------------------- add/sub
+template <class P>
+KZ_DEV Fp<P> fp_add(const Fp<P>& a, const Fp<P>& b) {
+  constexpr int N = P::N;
+  Fp<P> s, d;
+  uint32_t c = 0;
+  _Pragma("unroll") for (int i = 0; i < N; ++i) s.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+  uint32_t bw = 0;
+  _Pragma("unroll") for (int i = 0; i < N; ++i) d.v[i] = __builtin_subc(s.v[i], P::MOD[i], bw, &bw);
+  // a + b < 2p < 2^(32N): no carry out of s; s >= p iff no borrow
+  _Pragma("unroll") for (int i = 0; i < N; ++i) s.v[i] = bw ? s.v[i] : d.v[i];
+  return s;
+}
+
+template <class P>
+KZ_DEV Fp<P> fp_sub(const Fp<P>& a, const Fp<P>& b) {
+  constexpr int N = P::N;
+  Fp<P> d, e;
+  uint32_t bw = 0;
+  _Pragma("unroll") for (int i = 0; i < N; ++i) d.v[i] = __builtin_subc(a.v[i], b.v[i], bw, &bw);
+  uint32_t c = 0;
+  _Pragma("unroll") for (int i = 0; i < N; ++i) e.v[i] = __builtin_addc(d.v[i], P::MOD[i], c, &c);
+  _Pragma("unroll") for (int i = 0; i < N; ++i) d.v[i] = bw ? e.v[i] : d.v[i];
+  return d;
+}
+
+template <class P>
+KZ_DEV Fp<P> fp_dbl(const Fp<P>& a) { return fp_add(a, a); }
+
+template <class P>
+KZ_DEV Fp<P> fp_neg(const Fp<P>& a) {
+  constexpr int N = P::N;
+  Fp<P> d;
+  uint32_t bw = 0;
+  _Pragma("unroll") for (int i = 0; i < N; ++i) d.v[i] = __builtin_subc(P::MOD[i], a.v[i], bw, &bw);
+  bool z = a.is_zero();
+  _Pragma("unroll") for (int i = 0; i < N; ++i) d.v[i] = z ? 0u : d.v[i];
+  return d;
+}
+
+// conditional negation (branch-free): neg ? -a : a
+template <class P>
+KZ_DEV Fp<P> fp_cneg(const Fp<P>& a, bool neg) {
+  Fp<P> n = fp_neg(a);
+  Fp<P> r;
+  _Pragma("unroll") for (int i = 0; i < P::N; ++i) r.v[i] = neg ? n.v[i] : a.v[i];
+  return r;
+}
+
+template <class P>
+KZ_DEV Fp<P> fp_select(bool c, const Fp<P>& a, const Fp<P>& b) {
+  Fp<P> r;
+  _Pragma("unroll") for (int i = 0; i < P::N; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+
+// ---------------------------------------------------------------------------- mul (CIOS)
+// t = a*b*R^-1 mod p.  Per outer i:
+//   (A, t[0]) = t[0] + a[0]*b[i];  m = t[0]*INV;  C = hi(t[0] + m*p[0])
+//   for j>0: (A, t[j]) = t[j] + a[j]*b[i] + A;  (C, t[j-1]) = t[j] + m*p[j] + C
+//   t[N-1] = C + A
+template <class P>
+KZ_DEV Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
+  constexpr int N = P::N;
+  uint32_t t[N];
+  _Pragma("unroll") for (int i = 0; i < N; ++i) t[i] = 0;
+  _Pragma("unroll") for (int i = 0; i < N; ++i) {
+    const uint32_t bi = b.v[i];
+    uint64_t x = (uint64_t)a.v[0] * bi + t[0];
+    uint32_t A = (uint32_t)(x >> 32);
+    uint32_t t0 = (uint32_t)x;
+    uint32_t m = t0 * P::INV;
+    uint64_t y = (uint64_t)m * P::MOD[0] + t0;
+    uint32_t C = (uint32_t)(y >> 32);
+    _Pragma("unroll") for (int j = 1; j < N; ++j) {
+      x = (uint64_t)a.v[j] * bi + t[j] + A;
+      A = (uint32_t)(x >> 32);
+      y = (uint64_t)m * P::MOD[j] + (uint32_t)x + C;
+      C = (uint32_t)(y >> 32);
+      t[j - 1] = (uint32_t)y;
+    }
+    t[N - 1] = C + A;
+  }
+  // result < 2p: one conditional subtraction
+  Fp<P> r, d;
+  uint32_t bw = 0;
+  _Pragma("unroll") for (int i = 0; i < N; ++i) d.v[i] = __builtin_subc(t[i], P::MOD[i], bw, &bw);
+  _Pragma("unroll") for (int i = 0; i < N; ++i) r.v[i] = bw ? t[i] : d.v[i];
+  return r;
+}
+
+template <class P>
+KZ_DEV Fp<P> fp_sqr(const Fp<P>& a) { return fp_mul(a, a); }
+
+// small constant multiples by addition chains
+template <class P>
+KZ_DEV Fp<P> fp_mul3(const Fp<P>& a) { return fp_add(fp_add(a, a), a); }
+template <class P>
+KZ_DEV Fp<P> fp_mul4(const Fp<P>& a) { Fp<P> t = fp_add(a, a); return fp_add(t, t); }
+template <class P>
+KZ_DEV Fp<P> fp_mul8(const Fp<P>& a) { return fp_dbl(fp_mul4(a)); }
+
+// ---------------------------------------------------------------------------- conversions
+template <class P>
+KZ_DEV Fp<P> fp_to_mont(const Fp<P>& raw) { return fp_mul(raw, Fp<P>::from_const(P::R2)); }
+
+template <class P>
+KZ_DEV Fp<P> fp_from_mont(const Fp<P>& a) {
+  Fp<P> one = Fp<P>::zero();
+  one.v[0] = 1;
+  return fp_mul(a, one);
+}
+
+// raw (standard-form) value < modulus ?
+template <class P>
+KZ_DEV bool fp_raw_lt_mod(const Fp<P>& raw) {
+  uint32_t bw = 0;
+  _Pragma("unroll") for (int i = 0; i < P::N; ++i) (void)__builtin_subc(raw.v[i], P::MOD[i], bw, &bw);
+  return bw != 0;
+}
+
+// ---------------------------------------------------------------------------- pow / inverse
+template <class P, int NW>
+KZ_DEV Fp<P> fp_pow_words(const Fp<P>& a, const uint32_t (&e)[NW]) {
+  Fp<P> acc = Fp<P>::one();
+  for (int w = NW - 1; w >= 0; --w) {
+    uint32_t ew = e[w];
+    for (int b = 31; b >= 0; --b) {
+      acc = fp_sqr(acc);
+      if ((ew >> b) & 1) acc = fp_mul(acc, a);
+    }
+  }
+  return acc;
+}
+
+// Fermat inverse (used where a throughput-oriented, branch-uniform inverse is wanted).
+template <class P>
+KZ_DEV Fp<P> fp_inv_fermat(const Fp<P>& a) { return fp_pow_words(a, P::PM2); }
+
+// Binary extended Euclid on Montgomery values (latency-oriented: single-lane tails such as
+// MSM-result normalisation).  Returns a^-1 in Montgomery form; 0 -> 0.
+// Invariants: u*x == a_raw*R^? ...; implemented as the classic "u, v, x1, x2" binary
+// inversion on raw integers, then fixed up by two Montgomery multiplications.
+template <class P>
+KZ_DEV void big_rshift1(uint32_t (&x)[P::N]) {
+  _Pragma("unroll") for (int i = 0; i < P::N - 1; ++i) x[i] = (x[i] >> 1) | (x[i + 1] << 31);
+  x[P::N - 1] >>= 1;
+}
+template <class P>
+KZ_DEV bool big_is_one(const uint32_t (&x)[P::N]) {
+  uint32_t acc = x[0] ^ 1u;
+  _Pragma("unroll") for (int i = 1; i < P::N; ++i) acc |= x[i];
+  return acc == 0;
+}
+template <class P>
+KZ_DEV bool big_geq(const uint32_t (&a)[P::N], const uint32_t (&b)[P::N]) {
+  uint32_t bw = 0;
+  _Pragma("unroll") for (int i = 0; i < P::N; ++i) (void)__builtin_subc(a[i], b[i], bw, &bw);
+  return bw == 0;
+}
+template <class P>
+KZ_DEV void big_sub(uint32_t (&a)[P::N], const uint32_t (&b)[P::N]) {
+  uint32_t bw = 0;
+  _Pragma("unroll") for (int i = 0; i < P::N; ++i) a[i] = __builtin_subc(a[i], b[i], bw, &bw);
+}
+// x = x/2 mod p (x < p)
+template <class P>
+KZ_DEV void half_mod(uint32_t (&x)[P::N]) {
+  if (x[0] & 1) {
+    uint32_t c = 0;
+    _Pragma("unroll") for (int i = 0; i < P::N; ++i) x[i] = __builtin_addc(x[i], P::MOD[i], c, &c);
+    // x + p < 2^(32N) since p < 2^(32N-1)
+  }
+  big_rshift1<P>(x);
+}
+// x = x - y mod p (both < p)
+template <class P>
+KZ_DEV void sub_mod(uint32_t (&x)[P::N], const uint32_t (&y)[P::N]) {
+  uint32_t bw = 0;
+  _Pragma("unroll") for (int i = 0; i < P::N; ++i) x[i] = __builtin_subc(x[i], y[i], bw, &bw);
+  if (bw) {
+    uint32_t c = 0;
+    _Pragma("unroll") for (int i = 0; i < P::N; ++i) x[i] = __builtin_addc(x[i], P::MOD[i], c, &c);
+  }
+}
+
+template <class P>
+KZ_DEV Fp<P> fp_inv(const Fp<P>& a) {
+  constexpr int N = P::N;
+  if (a.is_zero()) return a;
+  // a is a*R (Montgomery).  Binary EEA computes (aR)^-1 mod p on raw integers; then
+  // (aR)^-1 * R^3 (two mont-muls by R2... ) gives a^-1 R.
+  uint32_t u[N], v[N], x1[N], x2[N];
+  _Pragma("unroll") for (int i = 0; i < N; ++i) { u[i] = a.v[i]; v[i] = P::MOD[i]; x1[i] = 0; x2[i] = 0; }
+  x1[0] = 1;
+  // invariant: x1*a == u, x2*a == v (mod p)
+  while (!big_is_one<P>(u) && !big_is_one<P>(v)) {
+    while ((u[0] & 1) == 0) { big_rshift1<P>(u); half_mod<P>(x1); }
+    while ((v[0] & 1) == 0) { big_rshift1<P>(v); half_mod<P>(x2); }
+    if (big_geq<P>(u, v)) { big_sub<P>(u, v); sub_mod<P>(x1, x2); }
+    else { big_sub<P>(v, u); sub_mod<P>(x2, x1); }
+  }
+  Fp<P> r;
+  if (big_is_one<P>(u)) { _Pragma("unroll") for (int i = 0; i < N; ++i) r.v[i] = x1[i]; }
+  else { _Pragma("unroll") for (int i = 0; i < N; ++i) r.v[i] = x2[i]; }
+  // r = (aR)^-1 (raw).  Want a^-1 R = r * R^2:  mont(r, R2) = r R^2 R^-1 = rR; twice -> rR^2.
+  Fp<P> r2 = Fp<P>::from_const(P::R2);
+  return fp_mul(fp_mul(r, r2), r2);
+}
+
+// ---------------------------------------------------------------------------- bytes
+// 32-bit big-endian word -> host order
+KZ_DEV uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+}  // namespace kzgmi

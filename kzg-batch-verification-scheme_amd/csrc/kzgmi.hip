@@ -1,0 +1,735 @@
+// kzgmi host orchestration + C-ABI (layers L3/L4 of SURVEY.md section 1).
+//
+// One translation unit: instantiates every kernel for BLS12-381 and BN254 and implements
+// include/kzgmi.h.  Device memory lives in per-slot workspaces owned by the context and is
+// grown on demand (never inside a timed steady state).  Every compute path is HIP-only:
+// without a device the calls fail with KZGMI_ERR_DEVICE (no CPU fallback).
+// Reference: none (LICENSE only); boundary contract = SURVEY.md 8b, BASELINE.json:5.
+#include "kernels.hpp"
+#include "kzgmi.h"
+
+#include <sys/random.h>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace kzgmi;
+
+namespace {
+
+thread_local std::string g_err = "";
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                              \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) return fail(KZGMI_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define CHK(x)                  \
+  do {                          \
+    int r_ = (x);               \
+    if (r_ != 0) return r_;     \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (bytes <= cap) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, bytes) != hipSuccess) return fail(KZGMI_ERR_OOM, "hipMalloc failed (" + std::to_string(bytes) + " bytes)");
+    cap = bytes;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+const char* const kPhaseNames = "convert,scalars,sort,accumulate,reduce,combine,pairing";
+constexpr int kNumPhases = 7;
+enum Phase { PH_CONVERT = 0, PH_SCALARS, PH_SORT, PH_ACCUM, PH_REDUCE, PH_COMBINE, PH_PAIRING };
+
+struct Slot {
+  hipStream_t stream = nullptr;
+  DevBuf pts, inf, scal_r, scal_s, scal_t, tpart, cnt, off, cursor, blk, total, sval, skey;
+  DevBuf buckets, pfirst, plast, R, U, scratch, winsum, res, flags, stage, outb;
+  int* host_flags = nullptr;  // pinned: [ok, err]
+  hipEvent_t ev[kNumPhases + 1] = {};
+  bool ev_used[kNumPhases + 1] = {};
+  bool pending = false;
+  int curve = 0;
+};
+
+}  // namespace
+
+struct kzgmi_ctx {
+  int device = 0;
+  std::vector<Slot> slots;
+  bool profiling = false;
+  double phase_ms[kNumPhases] = {};
+  DevBuf table[2], table_base[2];
+  bool table_ready[2] = {false, false};
+  DevBuf lines_tmp, tmp;
+};
+
+struct kzgmi_srs {
+  int curve = 0;
+  kzgmi_ctx* ctx = nullptr;
+  DevBuf lines, q, q_inf;
+};
+
+namespace {
+
+int set_dev(kzgmi_ctx* c) {
+  HIPCHK(hipSetDevice(c->device));
+  return 0;
+}
+
+inline unsigned grid(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+void mark(kzgmi_ctx* c, Slot& s, int idx) {
+  if (!c->profiling) return;
+  if (!s.ev[idx]) (void)hipEventCreate(&s.ev[idx]);
+  (void)hipEventRecord(s.ev[idx], s.stream);
+  s.ev_used[idx] = true;
+}
+
+void collect_phases(kzgmi_ctx* c, Slot& s) {
+  if (!c->profiling) return;
+  // phase k spans from the latest earlier recorded mark to mark k+1
+  for (int k = 0; k < kNumPhases; ++k) {
+    c->phase_ms[k] = 0;
+    if (!s.ev_used[k + 1]) continue;
+    int j = k;
+    while (j >= 0 && !s.ev_used[j]) --j;
+    if (j < 0) continue;
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, s.ev[j], s.ev[k + 1]) == hipSuccess) c->phase_ms[k] = ms;
+  }
+  for (int k = 0; k <= kNumPhases; ++k) s.ev_used[k] = false;
+}
+
+Seed make_seed(const uint8_t* seed32, uint8_t (&buf)[32]) {
+  if (seed32) {
+    memcpy(buf, seed32, 32);
+  } else {
+    size_t got = 0;
+    while (got < 32) {
+      ssize_t r = getrandom(buf + got, 32 - got, 0);
+      if (r > 0) got += (size_t)r;
+    }
+  }
+  Seed s;
+  for (int k = 0; k < 8; ++k)
+    s.w[k] = (uint32_t)buf[4 * k] << 24 | (uint32_t)buf[4 * k + 1] << 16 | (uint32_t)buf[4 * k + 2] << 8 | buf[4 * k + 3];
+  return s;
+}
+
+int map_device_err(uint32_t e) {
+  switch (e) {
+    case DERR_NONE: return 0;
+    case DERR_ENCODING: return fail(KZGMI_ERR_ENCODING, "invalid point encoding");
+    case DERR_NOT_ON_CURVE: return fail(KZGMI_ERR_NOT_ON_CURVE, "point not on curve");
+    case DERR_SCALAR: return fail(KZGMI_ERR_SCALAR, "non-canonical scalar (>= r)");
+    default: return fail(KZGMI_ERR_DEVICE, "unknown device error");
+  }
+}
+
+// ------------------------------------------------------------------------------ MSM core
+template <class Cv>
+int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl, uint32_t nsets, size_t emax, const MsmWindows& mw) {
+  using XY = Xyzz<Cv>;
+  const uint32_t NB = nsets * NBUCKETS;
+  const size_t nchunks = (emax + ACC_CHUNK - 1) / ACC_CHUNK + 1;
+  CHK(s.cnt.ensure((size_t)NB * 4));
+  CHK(s.off.ensure((size_t)NB * 4));
+  CHK(s.cursor.ensure((size_t)NB * 4));
+  CHK(s.blk.ensure(1024 * 4));
+  CHK(s.total.ensure(16));
+  CHK(s.sval.ensure(emax * 4));
+  CHK(s.skey.ensure(emax * 4));
+  CHK(s.buckets.ensure((size_t)NB * sizeof(XY)));
+  CHK(s.pfirst.ensure(nchunks * sizeof(XY)));
+  CHK(s.plast.ensure(nchunks * sizeof(XY)));
+  CHK(s.R.ensure((size_t)NB / SEG * sizeof(XY)));
+  CHK(s.U.ensure((size_t)NB / SEG * sizeof(XY)));
+  CHK(s.scratch.ensure((size_t)nsets * 288 * sizeof(XY)));
+  CHK(s.winsum.ensure((size_t)nsets * sizeof(XY)));
+  CHK(s.res.ensure(2 * sizeof(XY)));
+  hipStream_t st = s.stream;
+  HIPCHK(hipMemsetAsync(s.cnt.p, 0, (size_t)NB * 4, st));
+  if (tl.total) {
+    k_digits<false><<<grid(tl.total, 256), 256, 0, st>>>(tl, s.inf.template as<uint8_t>(), s.cnt.template as<uint32_t>(), nullptr, nullptr);
+  }
+  const uint32_t nscan = NB / (SCAN_BLOCK * SCAN_ITEMS);
+  k_scan_blocks<<<nscan, SCAN_BLOCK, 0, st>>>(s.cnt.template as<uint32_t>(), NB, s.off.template as<uint32_t>(), s.blk.template as<uint32_t>());
+  k_scan_totals<<<1, 1024, 0, st>>>(s.blk.template as<uint32_t>(), nscan, s.total.template as<uint32_t>());
+  k_scan_add<<<grid(NB, 256), 256, 0, st>>>(s.off.template as<uint32_t>(), NB, s.blk.template as<uint32_t>(), s.cursor.template as<uint32_t>());
+  if (tl.total) {
+    k_digits<true><<<grid(tl.total, 256), 256, 0, st>>>(tl, s.inf.template as<uint8_t>(), s.cursor.template as<uint32_t>(),
+                                                        s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>());
+  }
+  mark(c, s, PH_SORT + 1);
+  k_accumulate<Cv><<<grid(nchunks, 256), 256, 0, st>>>(s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
+                                                      s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.pts.template as<Affine<Cv>>(),
+                                                      s.buckets.template as<XY>(), s.pfirst.template as<XY>(), s.plast.template as<XY>());
+  k_fixup<Cv><<<grid(nchunks, 256), 256, 0, st>>>(s.total.template as<uint32_t>(), s.skey.template as<uint32_t>(), s.off.template as<uint32_t>(),
+                                                 s.cnt.template as<uint32_t>(), s.pfirst.template as<XY>(), s.plast.template as<XY>(), s.buckets.template as<XY>());
+  mark(c, s, PH_ACCUM + 1);
+  k_reduce_segments<Cv><<<grid(NB / SEG, 256), 256, 0, st>>>(NB / SEG, s.cnt.template as<uint32_t>(), s.buckets.template as<XY>(),
+                                                            s.R.template as<XY>(), s.U.template as<XY>());
+  k_reduce_finish<Cv><<<nsets, 256, 0, st>>>(s.R.template as<XY>(), s.U.template as<XY>(), s.scratch.template as<XY>(), s.winsum.template as<XY>());
+  mark(c, s, PH_REDUCE + 1);
+  k_window_combine<Cv><<<1, 64, 0, st>>>(mw, s.winsum.template as<XY>(), s.res.template as<XY>());
+  mark(c, s, PH_COMBINE + 1);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------------------ batch
+template <class Cv>
+int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, const void* dz, const void* dy,
+                  const void* dpi, size_t n, const Seed& seed, uint64_t offset, void* d_partial_out) {
+  using XY = Xyzz<Cv>;
+  using FrF = Fp<typename Cv::FrP>;
+  const size_t npts = 2 * n + 1;
+  const uint32_t nblk = grid(n, PREP_BLOCK);
+  CHK(s.pts.ensure(npts * sizeof(Affine<Cv>)));
+  CHK(s.inf.ensure(npts));
+  CHK(s.scal_r.ensure(n * 16));
+  CHK(s.scal_s.ensure(n * 32));
+  CHK(s.scal_t.ensure(32));
+  CHK(s.tpart.ensure((size_t)nblk * sizeof(FrF)));
+  CHK(s.flags.ensure(16));
+  hipStream_t st = s.stream;
+  mark(c, s, 0);
+  HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
+  uint32_t* err = s.flags.template as<uint32_t>() + 1;
+  Affine<Cv>* pts = s.pts.template as<Affine<Cv>>();
+  uint8_t* inf = s.inf.template as<uint8_t>();
+  k_convert_points<Cv><<<grid(n, 256), 256, 0, st>>>((const uint8_t*)dpi, (uint32_t)n, pts, inf, err);
+  k_convert_points<Cv><<<grid(n, 256), 256, 0, st>>>((const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err);
+  k_set_generator<Cv><<<1, 1, 0, st>>>(pts + 2 * n, inf + 2 * n);
+  mark(c, s, PH_CONVERT + 1);
+  k_scalar_prep<Cv><<<nblk, PREP_BLOCK, 0, st>>>(seed, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n,
+                                                 s.scal_r.template as<uint32_t>(), s.scal_s.template as<uint32_t>(), s.tpart.template as<FrF>(), err);
+  k_tsum<Cv><<<1, 256, 0, st>>>(s.tpart.template as<FrF>(), nblk, s.scal_t.template as<uint32_t>());
+  mark(c, s, PH_SCALARS + 1);
+  TermList tl{};
+  const uint32_t nn = (uint32_t)n;
+  tl.c[0] = {nn, 0, 4, 8, 0, 4, s.scal_r.template as<uint32_t>()};           // MSM#0: r_i pi_i
+  tl.c[1] = {nn, nn, 4, 8, 8, 4, s.scal_r.template as<uint32_t>()};          // MSM#1: r_i C_i
+  tl.c[2] = {nn, 0, 8, 16, 8, 8, s.scal_s.template as<uint32_t>()};          //        s_i pi_i
+  tl.c[3] = {1, 2 * nn, 8, 16, 8, 0, s.scal_t.template as<uint32_t>()};      //        -t G1
+  tl.nclass = 4;
+  tl.total = 3 * nn + 1;
+  MsmWindows mw{2, {0, 8}, {8, 16}};
+  CHK(run_msm_core<Cv>(c, s, tl, 24, (size_t)32 * n + 16, mw));
+  if (d_partial_out) {
+    HIPCHK(hipMemcpyAsync(d_partial_out, s.res.p, 2 * sizeof(XY), hipMemcpyDeviceToDevice, st));
+  } else {
+    k_pairing_check<Cv><<<1, 64, 0, st>>>(s.res.template as<XY>(), srs->lines.template as<Line<Cv>>(), srs->q_inf.template as<uint8_t>(),
+                                          s.flags.template as<int>());
+    mark(c, s, PH_PAIRING + 1);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
+  s.pending = true;
+  s.curve = Cv::ID;
+  return 0;
+}
+
+int finish_slot(kzgmi_ctx* c, Slot& s, int* ok_out) {
+  HIPCHK(hipStreamSynchronize(s.stream));
+  s.pending = false;
+  collect_phases(c, s);
+  int e = map_device_err((uint32_t)s.host_flags[1]);
+  if (e) return e;
+  if (ok_out) *ok_out = s.host_flags[0];
+  return 0;
+}
+
+template <class F>
+int dispatch(int curve, F&& f) {
+  if (curve == 0) return f(Bls12_381{});
+  if (curve == 1) return f(Bn254{});
+  return fail(KZGMI_ERR_ARG, "unknown curve");
+}
+
+size_t g1_bytes(int curve) { return curve == 0 ? 96 : 64; }
+size_t g2_bytes(int curve) { return curve == 0 ? 192 : 128; }
+
+int check_ctx(kzgmi_ctx* c, int slot = 0) {
+  if (!c) return fail(KZGMI_ERR_ARG, "null context");
+  if (slot < 0 || slot >= (int)c->slots.size()) return fail(KZGMI_ERR_ARG, "bad slot");
+  return set_dev(c);
+}
+
+template <class Cv>
+int ensure_table(kzgmi_ctx* c, hipStream_t st) {
+  if (c->table_ready[Cv::ID]) return 0;
+  CHK(c->table_base[Cv::ID].ensure(32 * sizeof(Xyzz<Cv>)));
+  CHK(c->table[Cv::ID].ensure(32 * 256 * sizeof(Affine<Cv>)));
+  k_gen_table_base<Cv><<<1, 64, 0, st>>>(c->table_base[Cv::ID].template as<Xyzz<Cv>>());
+  k_gen_table<Cv><<<32, 256, 0, st>>>(c->table_base[Cv::ID].template as<Xyzz<Cv>>(), c->table[Cv::ID].template as<Affine<Cv>>());
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));
+  c->table_ready[Cv::ID] = true;
+  return 0;
+}
+
+}  // namespace
+
+// ================================================================================ C ABI
+extern "C" {
+
+const char* kzgmi_version(void) { return "kzgmi 0.1 (gfx950, HIP)"; }
+const char* kzgmi_last_error(void) { return g_err.c_str(); }
+const char* kzgmi_phase_names(void) { return kPhaseNames; }
+
+int kzgmi_ctx_create(kzgmi_ctx** out, int device_id, int pipeline_slots) {
+  if (!out || device_id < 0 || pipeline_slots < 1 || pipeline_slots > 16) return fail(KZGMI_ERR_ARG, "bad ctx args");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device_id)
+    return fail(KZGMI_ERR_DEVICE, "no HIP device " + std::to_string(device_id) + " (found " + std::to_string(ndev) + ")");
+  HIPCHK(hipSetDevice(device_id));
+  kzgmi_ctx* c = new kzgmi_ctx();
+  c->device = device_id;
+  c->slots.resize(pipeline_slots);
+  for (auto& s : c->slots) {
+    if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void**)&s.host_flags, 16, hipHostMallocDefault) != hipSuccess) {
+      kzgmi_ctx_destroy(c);
+      return fail(KZGMI_ERR_DEVICE, "stream/pinned allocation failed");
+    }
+  }
+  *out = c;
+  return 0;
+}
+
+void kzgmi_ctx_destroy(kzgmi_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  for (auto& s : c->slots) {
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    DevBuf* bufs[] = {&s.pts, &s.inf, &s.scal_r, &s.scal_s, &s.scal_t, &s.tpart, &s.cnt, &s.off, &s.cursor, &s.blk,
+                      &s.total, &s.sval, &s.skey, &s.buckets, &s.pfirst, &s.plast, &s.R, &s.U, &s.scratch,
+                      &s.winsum, &s.res, &s.flags, &s.stage, &s.outb};
+    for (DevBuf* b : bufs) b->release();
+    for (auto& e : s.ev)
+      if (e) (void)hipEventDestroy(e);
+    if (s.host_flags) (void)hipHostFree(s.host_flags);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+  }
+  for (int k = 0; k < 2; ++k) { c->table[k].release(); c->table_base[k].release(); }
+  c->lines_tmp.release();
+  c->tmp.release();
+  delete c;
+}
+
+int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g2, const uint8_t* tau_g2, kzgmi_srs** out) {
+  CHK(check_ctx(c));
+  if (!g2 || !tau_g2 || !out) return fail(KZGMI_ERR_ARG, "null srs argument");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    Slot& s = c->slots[0];
+    const size_t gb = g2_bytes(Cv::ID);
+    kzgmi_srs* srs = new kzgmi_srs();
+    srs->curve = Cv::ID;
+    srs->ctx = c;
+    int r = 0;
+    if ((r = s.stage.ensure(2 * gb)) || (r = s.flags.ensure(16)) || (r = srs->q.ensure(2 * sizeof(G2Aff<Cv>))) ||
+        (r = srs->q_inf.ensure(16)) || (r = srs->lines.ensure(2 * num_lines<Cv>() * sizeof(Line<Cv>)))) {
+      delete srs;
+      return r;
+    }
+    // slot 0 = [tau]_2, slot 1 = [1]_2
+    std::vector<uint8_t> h(2 * gb);
+    memcpy(h.data(), tau_g2, gb);
+    memcpy(h.data() + gb, g2, gb);
+    hipStream_t st = s.stream;
+    bool okk = hipMemcpyAsync(s.stage.p, h.data(), 2 * gb, hipMemcpyHostToDevice, st) == hipSuccess &&
+               hipMemsetAsync(s.flags.p, 0, 16, st) == hipSuccess;
+    if (okk) {
+      k_convert_g2<Cv><<<1, 64, 0, st>>>(s.stage.template as<uint8_t>(), 2, srs->q.template as<G2Aff<Cv>>(), srs->q_inf.template as<uint8_t>(),
+                                         s.flags.template as<uint32_t>() + 1);
+      k_precompute_lines<Cv><<<1, 64, 0, st>>>(srs->q.template as<G2Aff<Cv>>(), srs->lines.template as<Line<Cv>>());
+      okk = hipGetLastError() == hipSuccess &&
+            hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
+            hipStreamSynchronize(st) == hipSuccess;
+    }
+    if (!okk) {
+      kzgmi_srs_free(srs);
+      return fail(KZGMI_ERR_DEVICE, "srs upload/precompute failed");
+    }
+    int e = map_device_err((uint32_t)s.host_flags[1]);
+    if (e) {
+      kzgmi_srs_free(srs);
+      return e;
+    }
+    *out = srs;
+    return 0;
+  });
+}
+
+void kzgmi_srs_free(kzgmi_srs* srs) {
+  if (!srs) return;
+  if (srs->ctx) (void)hipSetDevice(srs->ctx->device);
+  srs->lines.release();
+  srs->q.release();
+  srs->q_inf.release();
+  delete srs;
+}
+
+int kzgmi_batch_verify_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const void* dC, const void* dz,
+                                    const void* dy, const void* dpi, size_t n, const uint8_t* seed32) {
+  CHK(check_ctx(c, slot));
+  if (!srs || srs->ctx != c) return fail(KZGMI_ERR_ARG, "srs does not belong to this context");
+  if (n && (!dC || !dz || !dy || !dpi)) return fail(KZGMI_ERR_ARG, "null input");
+  if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "batch too large (max 2^26 tuples per call)");
+  Slot& s = c->slots[slot];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_slot_wait first");
+  uint8_t sb[32];
+  Seed seed = make_seed(seed32, sb);
+  if (n == 0) {
+    s.host_flags[0] = 1;
+    s.host_flags[1] = 0;
+    s.pending = true;
+    return 0;
+  }
+  return dispatch(srs->curve, [&](auto cv) -> int {
+    return enqueue_batch<decltype(cv)>(c, s, srs, dC, dz, dy, dpi, n, seed, 0, nullptr);
+  });
+}
+
+int kzgmi_slot_wait(kzgmi_ctx* c, int slot, int* ok_out) {
+  CHK(check_ctx(c, slot));
+  Slot& s = c->slots[slot];
+  if (!s.pending) return fail(KZGMI_ERR_ARG, "slot has no pending batch");
+  return finish_slot(c, s, ok_out);
+}
+
+int kzgmi_batch_verify_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* dC, const void* dz, const void* dy,
+                              const void* dpi, size_t n, const uint8_t* seed32, int* ok_out) {
+  if (!ok_out) return fail(KZGMI_ERR_ARG, "null ok_out");
+  CHK(kzgmi_batch_verify_device_async(c, srs, 0, dC, dz, dy, dpi, n, seed32));
+  return kzgmi_slot_wait(c, 0, ok_out);
+}
+
+int kzgmi_batch_verify(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commitments, const uint8_t* zs,
+                       const uint8_t* ys, const uint8_t* proofs, size_t n, const uint8_t* seed32, int* ok_out) {
+  CHK(check_ctx(c));
+  if (!srs || !ok_out) return fail(KZGMI_ERR_ARG, "null argument");
+  if (n && (!commitments || !zs || !ys || !proofs)) return fail(KZGMI_ERR_ARG, "null input");
+  if (n == 0) return kzgmi_batch_verify_device(c, srs, nullptr, nullptr, nullptr, nullptr, 0, seed32, ok_out);
+  Slot& s = c->slots[0];
+  const size_t gb = g1_bytes(srs->curve);
+  CHK(s.stage.ensure(n * (2 * gb + 64)));
+  uint8_t* base = s.stage.template as<uint8_t>();
+  uint8_t *dC = base, *dpi = base + n * gb, *dz = base + 2 * n * gb, *dy = dz + 32 * n;
+  HIPCHK(hipMemcpyAsync(dC, commitments, n * gb, hipMemcpyHostToDevice, s.stream));
+  HIPCHK(hipMemcpyAsync(dpi, proofs, n * gb, hipMemcpyHostToDevice, s.stream));
+  HIPCHK(hipMemcpyAsync(dz, zs, n * 32, hipMemcpyHostToDevice, s.stream));
+  HIPCHK(hipMemcpyAsync(dy, ys, n * 32, hipMemcpyHostToDevice, s.stream));
+  return kzgmi_batch_verify_device(c, srs, dC, dz, dy, dpi, n, seed32, ok_out);
+}
+
+int kzgmi_last_combination(kzgmi_ctx* c, uint8_t* a_out, uint8_t* b_out) {
+  CHK(check_ctx(c));
+  if (!a_out || !b_out) return fail(KZGMI_ERR_ARG, "null output");
+  Slot& s = c->slots[0];
+  if (!s.res.p) return fail(KZGMI_ERR_ARG, "no batch has run on slot 0");
+  return dispatch(s.curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    const size_t gb = g1_bytes(Cv::ID);
+    CHK(s.outb.ensure(2 * gb));
+    k_encode_points<Cv><<<1, 64, 0, s.stream>>>(s.res.template as<Xyzz<Cv>>(), 2, s.outb.template as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    std::vector<uint8_t> h(2 * gb);
+    HIPCHK(hipMemcpyAsync(h.data(), s.outb.p, 2 * gb, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipStreamSynchronize(s.stream));
+    memcpy(a_out, h.data(), gb);
+    memcpy(b_out, h.data() + gb, gb);
+    return 0;
+  });
+}
+
+// ------------------------------------------------------------------------------ MSM
+}  // extern "C"
+namespace {
+template <class Cv>
+int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t n) {
+  CHK(s.pts.ensure(n * sizeof(Affine<Cv>)));
+  CHK(s.inf.ensure(n));
+  CHK(s.scal_s.ensure(n * 32));
+  CHK(s.flags.ensure(16));
+  hipStream_t st = s.stream;
+  mark(c, s, 0);
+  HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
+  uint32_t* err = s.flags.template as<uint32_t>() + 1;
+  k_convert_points<Cv><<<grid(n, 256), 256, 0, st>>>((const uint8_t*)dpts, (uint32_t)n, s.pts.template as<Affine<Cv>>(),
+                                                     s.inf.template as<uint8_t>(), err);
+  mark(c, s, PH_CONVERT + 1);
+  k_convert_scalars<Cv><<<grid(n, 256), 256, 0, st>>>((const uint8_t*)dsc, (uint32_t)n, s.scal_s.template as<uint32_t>(), err);
+  mark(c, s, PH_SCALARS + 1);
+  TermList tl{};
+  tl.c[0] = {(uint32_t)n, 0, 8, 16, 0, 8, s.scal_s.template as<uint32_t>()};
+  tl.nclass = 1;
+  tl.total = (uint32_t)n;
+  MsmWindows mw{1, {0, 0}, {16, 0}};
+  CHK(run_msm_core<Cv>(c, s, tl, 16, (size_t)16 * n + 16, mw));
+  s.curve = Cv::ID;
+  return 0;
+}
+
+int read_flags_sync(kzgmi_ctx* c, Slot& s) {
+  HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, s.stream));
+  HIPCHK(hipStreamSynchronize(s.stream));
+  collect_phases(c, s);
+  return map_device_err((uint32_t)s.host_flags[1]);
+}
+}  // namespace
+extern "C" {
+
+int kzgmi_msm_g1_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dpts, const void* dsc, size_t n, uint8_t* out) {
+  CHK(check_ctx(c));
+  if (!out || (n && (!dpts || !dsc))) return fail(KZGMI_ERR_ARG, "null argument");
+  if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "MSM too large (max 2^26 points per call)");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    Slot& s = c->slots[0];
+    const size_t gb = g1_bytes(Cv::ID);
+    if (n == 0) {
+      memset(out, 0, gb);
+      if (Cv::ID == 0) out[0] = 0x40;
+      return 0;
+    }
+    CHK(enqueue_msm<Cv>(c, s, dpts, dsc, n));
+    CHK(s.outb.ensure(gb));
+    k_encode_points<Cv><<<1, 64, 0, s.stream>>>(s.res.template as<Xyzz<Cv>>(), 1, s.outb.template as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    CHK(read_flags_sync(c, s));
+    HIPCHK(hipMemcpy(out, s.outb.p, gb, hipMemcpyDeviceToHost));
+    return 0;
+  });
+}
+
+int kzgmi_msm_g1(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* points, const uint8_t* scalars, size_t n,
+                 uint8_t* out) {
+  CHK(check_ctx(c));
+  if (!out || (n && (!points || !scalars))) return fail(KZGMI_ERR_ARG, "null argument");
+  if (curve != KZGMI_BLS12_381 && curve != KZGMI_BN254) return fail(KZGMI_ERR_ARG, "unknown curve");
+  if (n == 0) return kzgmi_msm_g1_device(c, curve, nullptr, nullptr, 0, out);
+  Slot& s = c->slots[0];
+  const size_t gb = g1_bytes(curve);
+  CHK(s.stage.ensure(n * (gb + 32)));
+  uint8_t* dp = s.stage.template as<uint8_t>();
+  uint8_t* ds = dp + n * gb;
+  HIPCHK(hipMemcpyAsync(dp, points, n * gb, hipMemcpyHostToDevice, s.stream));
+  HIPCHK(hipMemcpyAsync(ds, scalars, n * 32, hipMemcpyHostToDevice, s.stream));
+  return kzgmi_msm_g1_device(c, curve, dp, ds, n, out);
+}
+
+// ------------------------------------------------------------------------------ multi-GPU
+size_t kzgmi_partial_bytes(kzgmi_curve curve) {
+  return curve == KZGMI_BLS12_381 ? sizeof(Xyzz<Bls12_381>) : sizeof(Xyzz<Bn254>);
+}
+
+int kzgmi_batch_partial_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* dC, const void* dz, const void* dy,
+                               const void* dpi, size_t n, uint64_t index_offset, const uint8_t* seed32,
+                               void* d_partial_out) {
+  CHK(check_ctx(c));
+  if (!srs || srs->ctx != c || !d_partial_out) return fail(KZGMI_ERR_ARG, "bad argument");
+  if (!seed32) return fail(KZGMI_ERR_ARG, "sharded verification needs an explicit shared seed");
+  Slot& s = c->slots[0];
+  uint8_t sb[32];
+  Seed seed = make_seed(seed32, sb);
+  return dispatch(srs->curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    if (n == 0) {
+      Xyzz<Cv> h[2];
+      for (auto& x : h) memset(&x, 0, sizeof(x));  // zz = 0 -> infinity
+      HIPCHK(hipMemcpy(d_partial_out, h, sizeof(h), hipMemcpyHostToDevice));
+      return 0;
+    }
+    CHK(enqueue_batch<Cv>(c, s, srs, dC, dz, dy, dpi, n, seed, index_offset, d_partial_out));
+    return finish_slot(c, s, nullptr);
+  });
+}
+
+int kzgmi_batch_combine_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* d_partials, int n_parts, int* ok_out) {
+  CHK(check_ctx(c));
+  if (!srs || !d_partials || n_parts < 1 || !ok_out) return fail(KZGMI_ERR_ARG, "bad argument");
+  return dispatch(srs->curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    using XY = Xyzz<Cv>;
+    Slot& s = c->slots[0];
+    CHK(s.res.ensure(2 * sizeof(XY)));
+    CHK(s.flags.ensure(16));
+    hipStream_t st = s.stream;
+    HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
+    mark(c, s, PH_COMBINE);
+    k_sum_partials<Cv><<<1, 64, 0, st>>>((const XY*)d_partials, (uint32_t)n_parts, 2, 2, s.res.template as<XY>());
+    k_pairing_check<Cv><<<1, 64, 0, st>>>(s.res.template as<XY>(), srs->lines.template as<Line<Cv>>(), srs->q_inf.template as<uint8_t>(),
+                                          s.flags.template as<int>());
+    mark(c, s, PH_PAIRING + 1);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
+    s.pending = true;
+    return finish_slot(c, s, ok_out);
+  });
+}
+
+int kzgmi_msm_partial_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dpts, const void* dsc, size_t n,
+                             void* d_partial_out) {
+  CHK(check_ctx(c));
+  if (!d_partial_out || (n && (!dpts || !dsc))) return fail(KZGMI_ERR_ARG, "bad argument");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    Slot& s = c->slots[0];
+    if (n == 0) {
+      Xyzz<Cv> h;
+      memset(&h, 0, sizeof(h));
+      HIPCHK(hipMemcpy(d_partial_out, &h, sizeof(h), hipMemcpyHostToDevice));
+      return 0;
+    }
+    CHK(enqueue_msm<Cv>(c, s, dpts, dsc, n));
+    HIPCHK(hipMemcpyAsync(d_partial_out, s.res.p, sizeof(Xyzz<Cv>), hipMemcpyDeviceToDevice, s.stream));
+    return read_flags_sync(c, s);
+  });
+}
+
+int kzgmi_msm_combine_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_partials, int n_parts, uint8_t* out) {
+  CHK(check_ctx(c));
+  if (!d_partials || n_parts < 1 || !out) return fail(KZGMI_ERR_ARG, "bad argument");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    using XY = Xyzz<Cv>;
+    Slot& s = c->slots[0];
+    const size_t gb = g1_bytes(Cv::ID);
+    CHK(s.res.ensure(2 * sizeof(XY)));
+    CHK(s.outb.ensure(gb));
+    k_sum_partials<Cv><<<1, 64, 0, s.stream>>>((const XY*)d_partials, (uint32_t)n_parts, 1, 1, s.res.template as<XY>());
+    k_encode_points<Cv><<<1, 64, 0, s.stream>>>(s.res.template as<XY>(), 1, s.outb.template as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s.stream));
+    HIPCHK(hipMemcpy(out, s.outb.p, gb, hipMemcpyDeviceToHost));
+    return 0;
+  });
+}
+
+// ------------------------------------------------------------------------------ pairing
+int kzgmi_pairing(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uint8_t* g2, uint8_t* out) {
+  CHK(check_ctx(c));
+  if (!g1 || !g2 || !out) return fail(KZGMI_ERR_ARG, "null argument");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    Slot& s = c->slots[0];
+    const size_t gb1 = g1_bytes(Cv::ID), gb2 = g2_bytes(Cv::ID);
+    const size_t fb = 12 * Cv::FP_BYTES;
+    CHK(s.stage.ensure(gb1 + 2 * gb2 + 64));
+    CHK(s.pts.ensure(sizeof(Affine<Cv>)));
+    CHK(s.inf.ensure(16));
+    CHK(s.flags.ensure(16));
+    CHK(s.outb.ensure(fb));
+    CHK(c->lines_tmp.ensure(2 * num_lines<Cv>() * sizeof(Line<Cv>) + 4 * sizeof(G2Aff<Cv>) + 64));
+    std::vector<uint8_t> h(gb1 + 2 * gb2);
+    memcpy(h.data(), g1, gb1);
+    memcpy(h.data() + gb1, g2, gb2);
+    memcpy(h.data() + gb1 + gb2, g2, gb2);
+    hipStream_t st = s.stream;
+    uint8_t* d = s.stage.template as<uint8_t>();
+    Line<Cv>* lines = c->lines_tmp.template as<Line<Cv>>();
+    G2Aff<Cv>* q = reinterpret_cast<G2Aff<Cv>*>(lines + 2 * num_lines<Cv>());
+    uint8_t* qinf = s.inf.template as<uint8_t>() + 8;
+    HIPCHK(hipMemcpyAsync(d, h.data(), h.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
+    uint32_t* err = s.flags.template as<uint32_t>() + 1;
+    k_convert_points<Cv><<<1, 64, 0, st>>>(d, 1, s.pts.template as<Affine<Cv>>(), s.inf.template as<uint8_t>(), err);
+    k_convert_g2<Cv><<<1, 64, 0, st>>>(d + gb1, 2, q, qinf, err);
+    k_precompute_lines<Cv><<<1, 64, 0, st>>>(q, lines);
+    k_pairing_one<Cv><<<1, 64, 0, st>>>(s.pts.template as<Affine<Cv>>(), s.inf.template as<uint8_t>(), lines, qinf, s.outb.template as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    CHK(read_flags_sync(c, s));
+    HIPCHK(hipMemcpy(out, s.outb.p, fb, hipMemcpyDeviceToHost));
+    return 0;
+  });
+}
+
+// ------------------------------------------------------------------------------ generators
+int kzgmi_gen_g1(kzgmi_ctx* c, kzgmi_curve curve, const void* d_scalars, size_t n, void* d_points_out) {
+  CHK(check_ctx(c));
+  if (n && (!d_scalars || !d_points_out)) return fail(KZGMI_ERR_ARG, "null argument");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    Slot& s = c->slots[0];
+    CHK(ensure_table<Cv>(c, s.stream));
+    CHK(s.flags.ensure(16));
+    HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));
+    if (n)
+      k_gen_g1<Cv><<<grid(n, 256), 256, 0, s.stream>>>((const uint8_t*)d_scalars, (uint32_t)n,
+                                                       c->table[Cv::ID].template as<Affine<Cv>>(), (uint8_t*)d_points_out,
+                                                       s.flags.template as<uint32_t>() + 1);
+    HIPCHK(hipGetLastError());
+    return read_flags_sync(c, s);
+  });
+}
+
+int kzgmi_gen_tuples(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* tau32, const uint8_t* seed32, size_t n,
+                     void* dC, void* dz, void* dy, void* dpi) {
+  CHK(check_ctx(c));
+  if (!tau32 || !seed32 || (n && (!dC || !dz || !dy || !dpi))) return fail(KZGMI_ERR_ARG, "null argument");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    using FrF = Fp<typename Cv::FrP>;
+    Slot& s = c->slots[0];
+    CHK(ensure_table<Cv>(c, s.stream));
+    FrF tau;
+    for (int k = 0; k < 8; ++k)
+      tau.v[k] = (uint32_t)tau32[31 - 4 * k] | (uint32_t)tau32[30 - 4 * k] << 8 | (uint32_t)tau32[29 - 4 * k] << 16 |
+                 (uint32_t)tau32[28 - 4 * k] << 24;
+    // tau must be canonical
+    for (int k = 7; k >= 0; --k) {
+      if (tau.v[k] < Cv::FrP::MOD[k]) break;
+      if (tau.v[k] > Cv::FrP::MOD[k] || k == 0) return fail(KZGMI_ERR_SCALAR, "tau >= r");
+    }
+    uint8_t sb[32];
+    Seed seed = make_seed(seed32, sb);
+    if (n)
+      k_gen_tuples<Cv><<<grid(n, 256), 256, 0, s.stream>>>(seed, tau, (uint32_t)n, c->table[Cv::ID].template as<Affine<Cv>>(),
+                                                           (uint8_t*)dC, (uint8_t*)dz, (uint8_t*)dy, (uint8_t*)dpi);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s.stream));
+    return 0;
+  });
+}
+
+// ------------------------------------------------------------------------------ profiling
+int kzgmi_set_profiling(kzgmi_ctx* c, int on) {
+  if (!c) return fail(KZGMI_ERR_ARG, "null context");
+  c->profiling = on != 0;
+  return 0;
+}
+
+int kzgmi_get_phase_ms(kzgmi_ctx* c, double* out, int max_n) {
+  if (!c || !out) return fail(KZGMI_ERR_ARG, "null argument");
+  int k = max_n < kNumPhases ? max_n : kNumPhases;
+  for (int i = 0; i < k; ++i) out[i] = c->phase_ms[i];
+  return k;
+}
+
+}  // extern "C"

@@ -1,0 +1,384 @@
+// G1 Pippenger MSM kernels for gfx950 (hot-path rows a5/a6 of SURVEY.md 8a).
+//
+// Pipeline (all on one HIP stream; no host synchronisation inside):
+//   k_digits<COUNT>   signed 16-bit window digits of every term -> per-bucket counts
+//   k_scan_*          exclusive scan of the counts -> bucket offsets (+ total entries)
+//   k_digits<SCATTER> same digits, each entry placed at its bucket's next slot
+//   k_accumulate      load-balanced bucket accumulation: every thread owns exactly
+//                     ACC_CHUNK consecutive sorted entries (not a bucket), so Poisson bucket
+//                     sizes do not diverge a wavefront; bucket pieces cut by a chunk
+//                     boundary go to partial slots and are joined by k_fixup.
+//   k_reduce_segments sum_b b*S_b per window: 16-bucket segments (running sums) ...
+//   k_reduce_finish   ... combined per window by one workgroup with LDS tree sums
+//   k_window_combine  Horner over the 16-bit windows (2^16 * acc + W_w)
+//
+// A "term list" generalises the two MSMs of batch verification (BASELINE.json:5,
+// SURVEY.md 3.1): MSM#0 = sum r_i pi_i (127-bit scalars, 8 windows) and MSM#1 = sum r_i C_i
+// + sum s_i pi_i - t G1 (windows 8..23), sharing one sort and one accumulation launch.
+// Reference: none (LICENSE only); parity vs the C oracle in tests/test_gpu_parity.py.
+#pragma once
+#include "common.hpp"
+
+namespace kzgmi {
+
+constexpr int WBITS = 16;                      // window width c
+constexpr int NBUCKETS = 1 << (WBITS - 1);     // signed digits: |d| in [1, 2^15]
+constexpr int ACC_CHUNK = 32;                  // entries per accumulation thread
+constexpr int SEG = 16;                        // buckets per reduction segment
+constexpr int MAX_CLASSES = 4;
+
+struct TermClass {
+  uint32_t count;       // number of terms in the class
+  uint32_t pt_base;     // index of the first point in the point array
+  uint32_t scal_words;  // 4 (127-bit randomisers) or 8 (full Fr)
+  uint32_t nwin;        // windows to emit
+  uint32_t set_base;    // bucket set (= msm window) of window 0
+  uint32_t scal_stride; // 0: one shared scalar for the whole class, else = scal_words
+  const uint32_t* scal; // LE words, standard (non-Montgomery) form
+};
+struct TermList {
+  TermClass c[MAX_CLASSES];
+  uint32_t nclass;
+  uint32_t total;
+};
+
+// ------------------------------------------------------------------------------ digits
+template <bool SCATTER>
+__global__ void __launch_bounds__(256) k_digits(TermList tl, const uint8_t* __restrict__ inf,
+                                                uint32_t* __restrict__ cnt_or_cursor,
+                                                uint32_t* __restrict__ sorted_val,
+                                                uint32_t* __restrict__ sorted_key) {
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= tl.total) return;
+  int k = 0;
+  uint32_t local = t;
+  while (k < (int)tl.nclass - 1 && local >= tl.c[k].count) { local -= tl.c[k].count; ++k; }
+  const TermClass& C = tl.c[k];
+  uint32_t pt = C.pt_base + local;
+  if (inf[pt]) return;
+  uint32_t w8[8];
+  const uint32_t* s = C.scal + (size_t)local * C.scal_stride;
+  if (C.scal_words == 4) {
+    uint4 q = *reinterpret_cast<const uint4*>(s);
+    w8[0] = q.x; w8[1] = q.y; w8[2] = q.z; w8[3] = q.w;
+    w8[4] = w8[5] = w8[6] = w8[7] = 0;
+  } else {
+    uint4 q0 = *reinterpret_cast<const uint4*>(s);
+    uint4 q1 = *reinterpret_cast<const uint4*>(s + 4);
+    w8[0] = q0.x; w8[1] = q0.y; w8[2] = q0.z; w8[3] = q0.w;
+    w8[4] = q1.x; w8[5] = q1.y; w8[6] = q1.z; w8[7] = q1.w;
+  }
+  uint32_t carry = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    if (w >= (int)C.nwin) break;
+    uint32_t raw = (w8[w >> 1] >> ((w & 1) * 16)) & 0xffffu;
+    int d = (int)(raw + carry);
+    if (d > NBUCKETS) { d -= (1 << WBITS); carry = 1; } else { carry = 0; }
+    if (d != 0) {
+      uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+      uint32_t key = (C.set_base + w) * NBUCKETS + (mag - 1);
+      if (!SCATTER) {
+        atomicAdd(&cnt_or_cursor[key], 1u);
+      } else {
+        uint32_t pos = atomicAdd(&cnt_or_cursor[key], 1u);
+        sorted_val[pos] = (pt << 1) | (d < 0 ? 1u : 0u);
+        sorted_key[pos] = key;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ scan
+constexpr int SCAN_BLOCK = 256;
+constexpr int SCAN_ITEMS = 16;  // 4096 counts per block
+
+__global__ void __launch_bounds__(SCAN_BLOCK) k_scan_blocks(const uint32_t* __restrict__ cnt, uint32_t nb,
+                                                           uint32_t* __restrict__ off, uint32_t* __restrict__ block_tot) {
+  __shared__ uint32_t s[SCAN_BLOCK];
+  uint32_t base = blockIdx.x * SCAN_BLOCK * SCAN_ITEMS + threadIdx.x * SCAN_ITEMS;
+  uint32_t v[SCAN_ITEMS];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_ITEMS; ++i) {
+    v[i] = (base + i < nb) ? cnt[base + i] : 0u;
+    sum += v[i];
+  }
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  for (int d = 1; d < SCAN_BLOCK; d <<= 1) {
+    uint32_t x = threadIdx.x >= (unsigned)d ? s[threadIdx.x - d] : 0u;
+    __syncthreads();
+    s[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint32_t run = s[threadIdx.x] - sum;  // exclusive prefix within block
+#pragma unroll
+  for (int i = 0; i < SCAN_ITEMS; ++i) {
+    if (base + i < nb) off[base + i] = run;
+    run += v[i];
+  }
+  if (threadIdx.x == SCAN_BLOCK - 1) block_tot[blockIdx.x] = s[threadIdx.x];
+}
+
+// single block: exclusive scan of block totals (<= 1024 blocks), writes grand total
+__global__ void __launch_bounds__(1024) k_scan_totals(uint32_t* __restrict__ block_tot, uint32_t nblocks,
+                                                      uint32_t* __restrict__ total) {
+  __shared__ uint32_t s[1024];
+  uint32_t v = threadIdx.x < nblocks ? block_tot[threadIdx.x] : 0u;
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    uint32_t x = threadIdx.x >= (unsigned)d ? s[threadIdx.x - d] : 0u;
+    __syncthreads();
+    s[threadIdx.x] += x;
+    __syncthreads();
+  }
+  if (threadIdx.x < nblocks) block_tot[threadIdx.x] = s[threadIdx.x] - v;
+  if (threadIdx.x == 1023) *total = s[1023];
+}
+
+__global__ void __launch_bounds__(256) k_scan_add(uint32_t* __restrict__ off, uint32_t nb,
+                                                  const uint32_t* __restrict__ block_tot,
+                                                  uint32_t* __restrict__ cursor) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb) return;
+  uint32_t o = off[i] + block_tot[i / (SCAN_BLOCK * SCAN_ITEMS)];
+  off[i] = o;
+  cursor[i] = o;
+}
+
+// ------------------------------------------------------------------------------ points I/O
+template <class Cv>
+KZ_DEV Affine<Cv> load_affine(const Affine<Cv>* pts, uint32_t i) {
+  // 96 B (BLS) / 64 B (BN) per point: 16-byte vector loads
+  Affine<Cv> a;
+  constexpr int W = 2 * Cv::FpP::N;  // 32-bit words per point
+  const uint4* src = reinterpret_cast<const uint4*>(pts + i);
+  uint32_t w[W];
+#pragma unroll
+  for (int k = 0; k < W / 4; ++k) {
+    uint4 q = src[k];
+    w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w;
+  }
+#pragma unroll
+  for (int k = 0; k < Cv::FpP::N; ++k) { a.x.v[k] = w[k]; a.y.v[k] = w[Cv::FpP::N + k]; }
+  return a;
+}
+
+template <class Cv>
+KZ_DEV void store_xyzz(Xyzz<Cv>* dst, const Xyzz<Cv>& p) {
+  constexpr int N = Cv::FpP::N;
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  uint32_t w[4 * N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) { w[k] = p.x.v[k]; w[N + k] = p.y.v[k]; w[2 * N + k] = p.zz.v[k]; w[3 * N + k] = p.zzz.v[k]; }
+#pragma unroll
+  for (int k = 0; k < N; ++k) d[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+}
+template <class Cv>
+KZ_DEV Xyzz<Cv> load_xyzz(const Xyzz<Cv>* src) {
+  constexpr int N = Cv::FpP::N;
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint32_t w[4 * N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) { uint4 q = s[k]; w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w; }
+  Xyzz<Cv> p;
+#pragma unroll
+  for (int k = 0; k < N; ++k) { p.x.v[k] = w[k]; p.y.v[k] = w[N + k]; p.zz.v[k] = w[2 * N + k]; p.zzz.v[k] = w[3 * N + k]; }
+  return p;
+}
+
+// ------------------------------------------------------------------------------ accumulation
+template <class Cv>
+KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_t start,
+                      const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
+                      Xyzz<Cv>* __restrict__ buckets, Xyzz<Cv>* __restrict__ part_first,
+                      Xyzz<Cv>* __restrict__ part_last) {
+  uint32_t o = off[key];
+  bool started_before = o < start;
+  bool ends_after = o + cnt[key] > start + ACC_CHUNK;
+  Xyzz<Cv>* dst = started_before ? &part_first[chunk] : ends_after ? &part_last[chunk] : &buckets[key];
+  store_xyzz(dst, acc);
+}
+
+template <class Cv>
+__global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__ total_p,
+                                                    const uint32_t* __restrict__ sorted_val,
+                                                    const uint32_t* __restrict__ sorted_key,
+                                                    const uint32_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ cnt,
+                                                    const Affine<Cv>* __restrict__ pts,
+                                                    Xyzz<Cv>* __restrict__ buckets,
+                                                    Xyzz<Cv>* __restrict__ part_first,
+                                                    Xyzz<Cv>* __restrict__ part_last) {
+  const uint32_t total = *total_p;
+  const uint32_t chunk = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t start = chunk * ACC_CHUNK;
+  if (start >= total) return;
+  const uint32_t end = min(start + ACC_CHUNK, total);
+  Xyzz<Cv> acc = Xyzz<Cv>::inf();
+  uint32_t cur = sorted_key[start];
+  for (uint32_t e = start; e < end; ++e) {
+    uint32_t key = sorted_key[e];
+    if (key != cur) {
+      acc_flush(acc, cur, chunk, start, off, cnt, buckets, part_first, part_last);
+      acc = Xyzz<Cv>::inf();
+      cur = key;
+    }
+    uint32_t v = sorted_val[e];
+    Affine<Cv> p = load_affine(pts, v >> 1);
+    p.y = fp_cneg(p.y, (v & 1) != 0);
+    acc = xyzz_add_affine(acc, p);
+  }
+  acc_flush(acc, cur, chunk, start, off, cnt, buckets, part_first, part_last);
+}
+
+// joins the pieces of buckets that cross chunk boundaries
+template <class Cv>
+__global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ total_p,
+                                               const uint32_t* __restrict__ sorted_key,
+                                               const uint32_t* __restrict__ off,
+                                               const uint32_t* __restrict__ cnt,
+                                               const Xyzz<Cv>* __restrict__ part_first,
+                                               const Xyzz<Cv>* __restrict__ part_last,
+                                               Xyzz<Cv>* __restrict__ buckets) {
+  const uint32_t total = *total_p;
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x + 1;
+  const uint32_t start = c * ACC_CHUNK;
+  if (start >= total) return;
+  uint32_t key = sorted_key[start];
+  uint32_t o = off[key];
+  if (o >= start) return;                 // bucket starts inside this chunk
+  uint32_t c0 = o / ACC_CHUNK;
+  if (c0 != c - 1) return;                // a later continuation chunk: handled by c0+1
+  uint32_t c1 = (o + cnt[key] - 1) / ACC_CHUNK;
+  Xyzz<Cv> acc = load_xyzz(&part_last[c0]);
+  for (uint32_t cc = c; cc <= c1; ++cc) acc = xyzz_add(acc, load_xyzz(&part_first[cc]));
+  store_xyzz(&buckets[key], acc);
+}
+
+// ------------------------------------------------------------------------------ reduction
+// Segment g covers buckets [g*SEG, (g+1)*SEG) of one set (SEG divides NBUCKETS).
+//   R_g = sum_{i} i * S_{g*SEG+i},  U_g = sum_i S_{g*SEG+i}
+template <class Cv>
+__global__ void __launch_bounds__(256) k_reduce_segments(uint32_t nseg, const uint32_t* __restrict__ cnt,
+                                                         const Xyzz<Cv>* __restrict__ buckets,
+                                                         Xyzz<Cv>* __restrict__ R, Xyzz<Cv>* __restrict__ U) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nseg) return;
+  Xyzz<Cv> run = Xyzz<Cv>::inf(), acc = Xyzz<Cv>::inf();
+  for (int i = SEG - 1; i >= 1; --i) {
+    uint32_t key = g * SEG + i;
+    if (cnt[key]) run = xyzz_add(run, load_xyzz(&buckets[key]));
+    acc = xyzz_add(acc, run);
+  }
+  uint32_t key0 = g * SEG;
+  if (cnt[key0]) run = xyzz_add(run, load_xyzz(&buckets[key0]));
+  store_xyzz(&R[g], acc);
+  store_xyzz(&U[g], run);
+}
+
+// LDS tree sum over a 256-thread block (all threads must call).
+template <class Cv>
+KZ_DEV Xyzz<Cv> block_sum256(Xyzz<Cv> v, Xyzz<Cv>* lds) {
+  const int t = threadIdx.x;
+  for (int s = 128; s >= 1; s >>= 1) {
+    if (t >= s && t < 2 * s) store_xyzz(&lds[t - s], v);
+    __syncthreads();
+    if (t < s) v = xyzz_add(v, load_xyzz(&lds[t]));
+    __syncthreads();
+  }
+  return v;  // valid in thread 0
+}
+
+// sum_{i<16} i*X_i and sum X_i for X_i = src[base + i*stride .. ] (serial, one thread)
+template <class Cv>
+KZ_DEV void weighted16(const Xyzz<Cv>* src, uint32_t count, Xyzz<Cv>& R, Xyzz<Cv>& U) {
+  Xyzz<Cv> run = Xyzz<Cv>::inf(), acc = Xyzz<Cv>::inf();
+  for (int i = (int)count - 1; i >= 1; --i) {
+    run = xyzz_add(run, load_xyzz(&src[i]));
+    acc = xyzz_add(acc, run);
+  }
+  if (count) run = xyzz_add(run, load_xyzz(&src[0]));
+  R = acc;
+  U = run;
+}
+
+template <class Cv>
+KZ_DEV Xyzz<Cv> xyzz_mul_pow2(Xyzz<Cv> p, int k) {
+  for (int i = 0; i < k; ++i) p = xyzz_dbl(p);
+  return p;
+}
+
+// One 256-thread workgroup per window (set).  Window sum
+//   W = sum_b (b+1) S_b = sum_g (R_g + U_g) + SEG * sum_g g U_g.
+// sum_g g U_g (2048 terms) is itself split into 16-term segments twice (in LDS scratch).
+template <class Cv>
+__global__ void __launch_bounds__(256) k_reduce_finish(const Xyzz<Cv>* __restrict__ R, const Xyzz<Cv>* __restrict__ U,
+                                                       Xyzz<Cv>* __restrict__ scratch, Xyzz<Cv>* __restrict__ winsum) {
+  constexpr uint32_t NSEG = NBUCKETS / SEG;  // 2048
+  __shared__ __attribute__((aligned(16))) Xyzz<Cv> lds[128];
+  const uint32_t set = blockIdx.x;
+  const Xyzz<Cv>* Rs = R + (size_t)set * NSEG;
+  const Xyzz<Cv>* Us = U + (size_t)set * NSEG;
+  Xyzz<Cv>* R2 = scratch + (size_t)set * 2 * (NSEG / SEG + 16);  // 128 + 8
+  Xyzz<Cv>* U2 = R2 + NSEG / SEG + 8;
+  const int t = threadIdx.x;
+  // (1) sum_g (R_g + U_g)
+  Xyzz<Cv> s = Xyzz<Cv>::inf();
+  for (uint32_t g = t; g < NSEG; g += 256) s = xyzz_add(xyzz_add(s, load_xyzz(&Rs[g])), load_xyzz(&Us[g]));
+  Xyzz<Cv> part1 = block_sum256(s, lds);
+  // (2) level 2: 128 threads, 16 U's each -> R2_j, U2_j
+  if (t < (int)(NSEG / SEG)) {
+    Xyzz<Cv> r, u;
+    weighted16(&Us[t * SEG], SEG, r, u);
+    store_xyzz(&R2[t], r);
+    store_xyzz(&U2[t], u);
+  }
+  __threadfence_block();
+  __syncthreads();
+  // sum_j R2_j (128 items): tree
+  Xyzz<Cv> v = (t < (int)(NSEG / SEG)) ? load_xyzz(&R2[t]) : Xyzz<Cv>::inf();
+  Xyzz<Cv> sumR2 = block_sum256(v, lds);
+  // (3) level 3: 8 threads over U2 (128 items) -> R3_j, U3_j (8 items); then serial
+  __shared__ __attribute__((aligned(16))) Xyzz<Cv> r3[8], u3[8];
+  if (t < 8) {
+    Xyzz<Cv> r, u;
+    weighted16(&U2[t * SEG], SEG, r, u);
+    store_xyzz(&r3[t], r);
+    store_xyzz(&u3[t], u);
+  }
+  __syncthreads();
+  if (t == 0) {
+    Xyzz<Cv> sumR3 = Xyzz<Cv>::inf();
+    for (int j = 0; j < 8; ++j) sumR3 = xyzz_add(sumR3, load_xyzz(&r3[j]));
+    Xyzz<Cv> r, u;
+    weighted16(u3, 8, r, u);                      // W3 = sum_j j U3_j
+    Xyzz<Cv> W2 = xyzz_add(sumR3, xyzz_mul_pow2(r, 4));   // sum_j j U2_j
+    Xyzz<Cv> V = xyzz_add(sumR2, xyzz_mul_pow2(W2, 4));   // sum_g g U_g
+    Xyzz<Cv> W = xyzz_add(part1, xyzz_mul_pow2(V, 4));
+    store_xyzz(&winsum[set], W);
+  }
+}
+
+// Horner over windows for each MSM: res[m] = sum_w 2^(16 w) winsum[set_base_m + w]
+struct MsmWindows {
+  uint32_t nmsm;
+  uint32_t set_base[2];
+  uint32_t nwin[2];
+};
+template <class Cv>
+__global__ void k_window_combine(MsmWindows mw, const Xyzz<Cv>* __restrict__ winsum, Xyzz<Cv>* __restrict__ res) {
+  uint32_t m = threadIdx.x;
+  if (m >= mw.nmsm) return;
+  const Xyzz<Cv>* W = winsum + mw.set_base[m];
+  Xyzz<Cv> acc = load_xyzz(&W[mw.nwin[m] - 1]);
+  for (int w = (int)mw.nwin[m] - 2; w >= 0; --w) {
+    acc = xyzz_mul_pow2(acc, WBITS);
+    acc = xyzz_add(acc, load_xyzz(&W[w]));
+  }
+  store_xyzz(&res[m], acc);
+}
+
+}  // namespace kzgmi
