@@ -126,10 +126,19 @@ int kzgmi_gen_g1(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_scalars, size_
 int kzgmi_gen_tuples(kzgmi_ctx* ctx, kzgmi_curve curve, const uint8_t* tau32, const uint8_t* seed32,
                      size_t n, void* d_commitments, void* d_zs, void* d_ys, void* d_proofs);
 
+/* [k]Q for a G2 point Q (host encodings; k = 32 B BE, < r): toy-SRS generation
+ * ([tau]_2 from a known tau, SURVEY.md 2 "test-only toy-tau generator"). */
+int kzgmi_g2_mul(kzgmi_ctx* ctx, kzgmi_curve curve, const uint8_t* g2, const uint8_t* k32, uint8_t* out);
+
+/* Compute-roofline probe: Montgomery Fp multiplications per second on this GPU (many
+ * independent products per thread, whole chip), written to *muls_per_s. */
+int kzgmi_probe_fpmul(kzgmi_ctx* ctx, kzgmi_curve curve, double* muls_per_s);
+
 /* ---- profiling -----------------------------------------------------------------------
- * When enabled, synchronous calls record HIP events around each phase on the context's
- * stream; kzgmi_get_phase_ms() returns the last call's per-phase device times (ms) in
- * the order of kzgmi_phase_names() (comma-separated). */
+ * When enabled, every batch / MSM call records HIP events around each phase on the stream
+ * its kernels run on; kzgmi_get_phase_ms() returns the per-phase device time (ms) averaged
+ * over all calls completed since profiling was (re)enabled, in the order of
+ * kzgmi_phase_names() (comma-separated).  Enabling resets the averages. */
 int kzgmi_set_profiling(kzgmi_ctx* ctx, int on);
 const char* kzgmi_phase_names(void);
 int kzgmi_get_phase_ms(kzgmi_ctx* ctx, double* out, int max_n);

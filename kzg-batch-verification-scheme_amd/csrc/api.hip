@@ -5,7 +5,7 @@
 // grown on demand (never inside a timed steady state).  Every compute path is HIP-only:
 // without a device the calls fail with KZGMI_ERR_DEVICE (no CPU fallback).
 // Reference: none (LICENSE only); boundary contract = SURVEY.md 8b, BASELINE.json:5.
-#include "kernels.hpp"
+#include "launch.hpp"
 #include "kzgmi.h"
 
 #include <sys/random.h>
@@ -79,7 +79,8 @@ struct kzgmi_ctx {
   int device = 0;
   std::vector<Slot> slots;
   bool profiling = false;
-  double phase_ms[kNumPhases] = {};
+  double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
+  int phase_calls = 0;
   DevBuf table[2], table_base[2];
   bool table_ready[2] = {false, false};
   DevBuf lines_tmp, tmp;
@@ -111,14 +112,14 @@ void collect_phases(kzgmi_ctx* c, Slot& s) {
   if (!c->profiling) return;
   // phase k spans from the latest earlier recorded mark to mark k+1
   for (int k = 0; k < kNumPhases; ++k) {
-    c->phase_ms[k] = 0;
     if (!s.ev_used[k + 1]) continue;
     int j = k;
     while (j >= 0 && !s.ev_used[j]) --j;
     if (j < 0) continue;
     float ms = 0;
-    if (hipEventElapsedTime(&ms, s.ev[j], s.ev[k + 1]) == hipSuccess) c->phase_ms[k] = ms;
+    if (hipEventElapsedTime(&ms, s.ev[j], s.ev[k + 1]) == hipSuccess) c->phase_ms[k] += ms;
   }
+  c->phase_calls += 1;
   for (int k = 0; k <= kNumPhases; ++k) s.ev_used[k] = false;
 }
 
@@ -170,30 +171,22 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl, uint32_t nsets, size
   CHK(s.winsum.ensure((size_t)nsets * sizeof(XY)));
   CHK(s.res.ensure(2 * sizeof(XY)));
   hipStream_t st = s.stream;
+  using L = Launch<Cv>;
   HIPCHK(hipMemsetAsync(s.cnt.p, 0, (size_t)NB * 4, st));
-  if (tl.total) {
-    k_digits<false><<<grid(tl.total, 256), 256, 0, st>>>(tl, s.inf.template as<uint8_t>(), s.cnt.template as<uint32_t>(), nullptr, nullptr);
-  }
-  const uint32_t nscan = NB / (SCAN_BLOCK * SCAN_ITEMS);
-  k_scan_blocks<<<nscan, SCAN_BLOCK, 0, st>>>(s.cnt.template as<uint32_t>(), NB, s.off.template as<uint32_t>(), s.blk.template as<uint32_t>());
-  k_scan_totals<<<1, 1024, 0, st>>>(s.blk.template as<uint32_t>(), nscan, s.total.template as<uint32_t>());
-  k_scan_add<<<grid(NB, 256), 256, 0, st>>>(s.off.template as<uint32_t>(), NB, s.blk.template as<uint32_t>(), s.cursor.template as<uint32_t>());
-  if (tl.total) {
-    k_digits<true><<<grid(tl.total, 256), 256, 0, st>>>(tl, s.inf.template as<uint8_t>(), s.cursor.template as<uint32_t>(),
-                                                        s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>());
-  }
+  L::digits(st, false, tl, s.inf.template as<uint8_t>(), s.cnt.template as<uint32_t>(), nullptr, nullptr);
+  L::scan(st, s.cnt.template as<uint32_t>(), NB, s.off.template as<uint32_t>(), s.blk.template as<uint32_t>(),
+          s.total.template as<uint32_t>(), s.cursor.template as<uint32_t>());
+  L::digits(st, true, tl, s.inf.template as<uint8_t>(), s.cursor.template as<uint32_t>(), s.sval.template as<uint32_t>(),
+            s.skey.template as<uint32_t>());
   mark(c, s, PH_SORT + 1);
-  k_accumulate<Cv><<<grid(nchunks, 256), 256, 0, st>>>(s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
-                                                      s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.pts.template as<Affine<Cv>>(),
-                                                      s.buckets.template as<XY>(), s.pfirst.template as<XY>(), s.plast.template as<XY>());
-  k_fixup<Cv><<<grid(nchunks, 256), 256, 0, st>>>(s.total.template as<uint32_t>(), s.skey.template as<uint32_t>(), s.off.template as<uint32_t>(),
-                                                 s.cnt.template as<uint32_t>(), s.pfirst.template as<XY>(), s.plast.template as<XY>(), s.buckets.template as<XY>());
+  L::accumulate(st, nchunks, s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
+                s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.pts.template as<Affine<Cv>>(),
+                s.buckets.template as<XY>(), s.pfirst.template as<XY>(), s.plast.template as<XY>());
   mark(c, s, PH_ACCUM + 1);
-  k_reduce_segments<Cv><<<grid(NB / SEG, 256), 256, 0, st>>>(NB / SEG, s.cnt.template as<uint32_t>(), s.buckets.template as<XY>(),
-                                                            s.R.template as<XY>(), s.U.template as<XY>());
-  k_reduce_finish<Cv><<<nsets, 256, 0, st>>>(s.R.template as<XY>(), s.U.template as<XY>(), s.scratch.template as<XY>(), s.winsum.template as<XY>());
+  L::reduce(st, nsets, s.cnt.template as<uint32_t>(), s.buckets.template as<XY>(), s.R.template as<XY>(),
+            s.U.template as<XY>(), s.scratch.template as<XY>(), s.winsum.template as<XY>());
   mark(c, s, PH_REDUCE + 1);
-  k_window_combine<Cv><<<1, 64, 0, st>>>(mw, s.winsum.template as<XY>(), s.res.template as<XY>());
+  L::window_combine(st, mw, s.winsum.template as<XY>(), s.res.template as<XY>());
   mark(c, s, PH_COMBINE + 1);
   HIPCHK(hipGetLastError());
   return 0;
@@ -206,13 +199,13 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   using XY = Xyzz<Cv>;
   using FrF = Fp<typename Cv::FrP>;
   const size_t npts = 2 * n + 1;
-  const uint32_t nblk = grid(n, PREP_BLOCK);
+  using L = Launch<Cv>;
   CHK(s.pts.ensure(npts * sizeof(Affine<Cv>)));
   CHK(s.inf.ensure(npts));
   CHK(s.scal_r.ensure(n * 16));
   CHK(s.scal_s.ensure(n * 32));
   CHK(s.scal_t.ensure(32));
-  CHK(s.tpart.ensure((size_t)nblk * sizeof(FrF)));
+  CHK(s.tpart.ensure(L::tpart_bytes((uint32_t)n)));
   CHK(s.flags.ensure(16));
   hipStream_t st = s.stream;
   mark(c, s, 0);
@@ -220,13 +213,12 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   uint32_t* err = s.flags.template as<uint32_t>() + 1;
   Affine<Cv>* pts = s.pts.template as<Affine<Cv>>();
   uint8_t* inf = s.inf.template as<uint8_t>();
-  k_convert_points<Cv><<<grid(n, 256), 256, 0, st>>>((const uint8_t*)dpi, (uint32_t)n, pts, inf, err);
-  k_convert_points<Cv><<<grid(n, 256), 256, 0, st>>>((const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err);
-  k_set_generator<Cv><<<1, 1, 0, st>>>(pts + 2 * n, inf + 2 * n);
+  L::convert_points(st, (const uint8_t*)dpi, (uint32_t)n, pts, inf, err);
+  L::convert_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err);
+  L::set_generator(st, pts + 2 * n, inf + 2 * n);
   mark(c, s, PH_CONVERT + 1);
-  k_scalar_prep<Cv><<<nblk, PREP_BLOCK, 0, st>>>(seed, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n,
-                                                 s.scal_r.template as<uint32_t>(), s.scal_s.template as<uint32_t>(), s.tpart.template as<FrF>(), err);
-  k_tsum<Cv><<<1, 256, 0, st>>>(s.tpart.template as<FrF>(), nblk, s.scal_t.template as<uint32_t>());
+  L::scalar_prep(st, seed, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n, s.scal_r.template as<uint32_t>(),
+                 s.scal_s.template as<uint32_t>(), s.tpart.p, s.scal_t.template as<uint32_t>(), err);
   mark(c, s, PH_SCALARS + 1);
   TermList tl{};
   const uint32_t nn = (uint32_t)n;
@@ -241,8 +233,8 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   if (d_partial_out) {
     HIPCHK(hipMemcpyAsync(d_partial_out, s.res.p, 2 * sizeof(XY), hipMemcpyDeviceToDevice, st));
   } else {
-    k_pairing_check<Cv><<<1, 64, 0, st>>>(s.res.template as<XY>(), srs->lines.template as<Line<Cv>>(), srs->q_inf.template as<uint8_t>(),
-                                          s.flags.template as<int>());
+    L::pairing_check(st, s.res.template as<XY>(), srs->lines.template as<Line<Cv>>(), srs->q_inf.template as<uint8_t>(),
+                     s.flags.template as<int>());
     mark(c, s, PH_PAIRING + 1);
   }
   HIPCHK(hipGetLastError());
@@ -283,8 +275,7 @@ int ensure_table(kzgmi_ctx* c, hipStream_t st) {
   if (c->table_ready[Cv::ID]) return 0;
   CHK(c->table_base[Cv::ID].ensure(32 * sizeof(Xyzz<Cv>)));
   CHK(c->table[Cv::ID].ensure(32 * 256 * sizeof(Affine<Cv>)));
-  k_gen_table_base<Cv><<<1, 64, 0, st>>>(c->table_base[Cv::ID].template as<Xyzz<Cv>>());
-  k_gen_table<Cv><<<32, 256, 0, st>>>(c->table_base[Cv::ID].template as<Xyzz<Cv>>(), c->table[Cv::ID].template as<Affine<Cv>>());
+  Launch<Cv>::gen_table(st, c->table_base[Cv::ID].template as<Xyzz<Cv>>(), c->table[Cv::ID].template as<Affine<Cv>>());
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(st));
   c->table_ready[Cv::ID] = true;
@@ -353,7 +344,7 @@ int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g2, const uin
     srs->ctx = c;
     int r = 0;
     if ((r = s.stage.ensure(2 * gb)) || (r = s.flags.ensure(16)) || (r = srs->q.ensure(2 * sizeof(G2Aff<Cv>))) ||
-        (r = srs->q_inf.ensure(16)) || (r = srs->lines.ensure(2 * num_lines<Cv>() * sizeof(Line<Cv>)))) {
+        (r = srs->q_inf.ensure(16)) || (r = srs->lines.ensure(2 * Launch<Cv>::num_lines() * sizeof(Line<Cv>)))) {
       delete srs;
       return r;
     }
@@ -365,9 +356,9 @@ int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g2, const uin
     bool okk = hipMemcpyAsync(s.stage.p, h.data(), 2 * gb, hipMemcpyHostToDevice, st) == hipSuccess &&
                hipMemsetAsync(s.flags.p, 0, 16, st) == hipSuccess;
     if (okk) {
-      k_convert_g2<Cv><<<1, 64, 0, st>>>(s.stage.template as<uint8_t>(), 2, srs->q.template as<G2Aff<Cv>>(), srs->q_inf.template as<uint8_t>(),
+      Launch<Cv>::convert_g2(st, s.stage.template as<uint8_t>(), 2, srs->q.template as<G2Aff<Cv>>(), srs->q_inf.template as<uint8_t>(),
                                          s.flags.template as<uint32_t>() + 1);
-      k_precompute_lines<Cv><<<1, 64, 0, st>>>(srs->q.template as<G2Aff<Cv>>(), srs->lines.template as<Line<Cv>>());
+      Launch<Cv>::precompute_lines(st, srs->q.template as<G2Aff<Cv>>(), srs->lines.template as<Line<Cv>>());
       okk = hipGetLastError() == hipSuccess &&
             hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
             hipStreamSynchronize(st) == hipSuccess;
@@ -457,7 +448,7 @@ int kzgmi_last_combination(kzgmi_ctx* c, uint8_t* a_out, uint8_t* b_out) {
     using Cv = decltype(cv);
     const size_t gb = g1_bytes(Cv::ID);
     CHK(s.outb.ensure(2 * gb));
-    k_encode_points<Cv><<<1, 64, 0, s.stream>>>(s.res.template as<Xyzz<Cv>>(), 2, s.outb.template as<uint8_t>());
+    Launch<Cv>::encode_points(s.stream, s.res.template as<Xyzz<Cv>>(), 2, s.outb.template as<uint8_t>());
     HIPCHK(hipGetLastError());
     std::vector<uint8_t> h(2 * gb);
     HIPCHK(hipMemcpyAsync(h.data(), s.outb.p, 2 * gb, hipMemcpyDeviceToHost, s.stream));
@@ -481,10 +472,10 @@ int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t
   mark(c, s, 0);
   HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
   uint32_t* err = s.flags.template as<uint32_t>() + 1;
-  k_convert_points<Cv><<<grid(n, 256), 256, 0, st>>>((const uint8_t*)dpts, (uint32_t)n, s.pts.template as<Affine<Cv>>(),
-                                                     s.inf.template as<uint8_t>(), err);
+  Launch<Cv>::convert_points(st, (const uint8_t*)dpts, (uint32_t)n, s.pts.template as<Affine<Cv>>(),
+                             s.inf.template as<uint8_t>(), err);
   mark(c, s, PH_CONVERT + 1);
-  k_convert_scalars<Cv><<<grid(n, 256), 256, 0, st>>>((const uint8_t*)dsc, (uint32_t)n, s.scal_s.template as<uint32_t>(), err);
+  Launch<Cv>::convert_scalars(st, (const uint8_t*)dsc, (uint32_t)n, s.scal_s.template as<uint32_t>(), err);
   mark(c, s, PH_SCALARS + 1);
   TermList tl{};
   tl.c[0] = {(uint32_t)n, 0, 8, 16, 0, 8, s.scal_s.template as<uint32_t>()};
@@ -520,7 +511,7 @@ int kzgmi_msm_g1_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dpts, const
     }
     CHK(enqueue_msm<Cv>(c, s, dpts, dsc, n));
     CHK(s.outb.ensure(gb));
-    k_encode_points<Cv><<<1, 64, 0, s.stream>>>(s.res.template as<Xyzz<Cv>>(), 1, s.outb.template as<uint8_t>());
+    Launch<Cv>::encode_points(s.stream, s.res.template as<Xyzz<Cv>>(), 1, s.outb.template as<uint8_t>());
     HIPCHK(hipGetLastError());
     CHK(read_flags_sync(c, s));
     HIPCHK(hipMemcpy(out, s.outb.p, gb, hipMemcpyDeviceToHost));
@@ -583,8 +574,8 @@ int kzgmi_batch_combine_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* d
     hipStream_t st = s.stream;
     HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
     mark(c, s, PH_COMBINE);
-    k_sum_partials<Cv><<<1, 64, 0, st>>>((const XY*)d_partials, (uint32_t)n_parts, 2, 2, s.res.template as<XY>());
-    k_pairing_check<Cv><<<1, 64, 0, st>>>(s.res.template as<XY>(), srs->lines.template as<Line<Cv>>(), srs->q_inf.template as<uint8_t>(),
+    Launch<Cv>::sum_partials(st, (const XY*)d_partials, (uint32_t)n_parts, 2, 2, s.res.template as<XY>());
+    Launch<Cv>::pairing_check(st, s.res.template as<XY>(), srs->lines.template as<Line<Cv>>(), srs->q_inf.template as<uint8_t>(),
                                           s.flags.template as<int>());
     mark(c, s, PH_PAIRING + 1);
     HIPCHK(hipGetLastError());
@@ -623,8 +614,8 @@ int kzgmi_msm_combine_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_part
     const size_t gb = g1_bytes(Cv::ID);
     CHK(s.res.ensure(2 * sizeof(XY)));
     CHK(s.outb.ensure(gb));
-    k_sum_partials<Cv><<<1, 64, 0, s.stream>>>((const XY*)d_partials, (uint32_t)n_parts, 1, 1, s.res.template as<XY>());
-    k_encode_points<Cv><<<1, 64, 0, s.stream>>>(s.res.template as<XY>(), 1, s.outb.template as<uint8_t>());
+    Launch<Cv>::sum_partials(s.stream, (const XY*)d_partials, (uint32_t)n_parts, 1, 1, s.res.template as<XY>());
+    Launch<Cv>::encode_points(s.stream, s.res.template as<XY>(), 1, s.outb.template as<uint8_t>());
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s.stream));
     HIPCHK(hipMemcpy(out, s.outb.p, gb, hipMemcpyDeviceToHost));
@@ -646,7 +637,7 @@ int kzgmi_pairing(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uint
     CHK(s.inf.ensure(16));
     CHK(s.flags.ensure(16));
     CHK(s.outb.ensure(fb));
-    CHK(c->lines_tmp.ensure(2 * num_lines<Cv>() * sizeof(Line<Cv>) + 4 * sizeof(G2Aff<Cv>) + 64));
+    CHK(c->lines_tmp.ensure(2 * Launch<Cv>::num_lines() * sizeof(Line<Cv>) + 4 * sizeof(G2Aff<Cv>) + 64));
     std::vector<uint8_t> h(gb1 + 2 * gb2);
     memcpy(h.data(), g1, gb1);
     memcpy(h.data() + gb1, g2, gb2);
@@ -654,15 +645,15 @@ int kzgmi_pairing(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uint
     hipStream_t st = s.stream;
     uint8_t* d = s.stage.template as<uint8_t>();
     Line<Cv>* lines = c->lines_tmp.template as<Line<Cv>>();
-    G2Aff<Cv>* q = reinterpret_cast<G2Aff<Cv>*>(lines + 2 * num_lines<Cv>());
+    G2Aff<Cv>* q = reinterpret_cast<G2Aff<Cv>*>(lines + 2 * Launch<Cv>::num_lines());
     uint8_t* qinf = s.inf.template as<uint8_t>() + 8;
     HIPCHK(hipMemcpyAsync(d, h.data(), h.size(), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
     uint32_t* err = s.flags.template as<uint32_t>() + 1;
-    k_convert_points<Cv><<<1, 64, 0, st>>>(d, 1, s.pts.template as<Affine<Cv>>(), s.inf.template as<uint8_t>(), err);
-    k_convert_g2<Cv><<<1, 64, 0, st>>>(d + gb1, 2, q, qinf, err);
-    k_precompute_lines<Cv><<<1, 64, 0, st>>>(q, lines);
-    k_pairing_one<Cv><<<1, 64, 0, st>>>(s.pts.template as<Affine<Cv>>(), s.inf.template as<uint8_t>(), lines, qinf, s.outb.template as<uint8_t>());
+    Launch<Cv>::convert_points(st, d, 1, s.pts.template as<Affine<Cv>>(), s.inf.template as<uint8_t>(), err);
+    Launch<Cv>::convert_g2(st, d + gb1, 2, q, qinf, err);
+    Launch<Cv>::precompute_lines(st, q, lines);
+    Launch<Cv>::pairing_one(st, s.pts.template as<Affine<Cv>>(), s.inf.template as<uint8_t>(), lines, qinf, s.outb.template as<uint8_t>());
     HIPCHK(hipGetLastError());
     CHK(read_flags_sync(c, s));
     HIPCHK(hipMemcpy(out, s.outb.p, fb, hipMemcpyDeviceToHost));
@@ -681,9 +672,8 @@ int kzgmi_gen_g1(kzgmi_ctx* c, kzgmi_curve curve, const void* d_scalars, size_t 
     CHK(s.flags.ensure(16));
     HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));
     if (n)
-      k_gen_g1<Cv><<<grid(n, 256), 256, 0, s.stream>>>((const uint8_t*)d_scalars, (uint32_t)n,
-                                                       c->table[Cv::ID].template as<Affine<Cv>>(), (uint8_t*)d_points_out,
-                                                       s.flags.template as<uint32_t>() + 1);
+      Launch<Cv>::gen_g1(s.stream, (const uint8_t*)d_scalars, (uint32_t)n, c->table[Cv::ID].template as<Affine<Cv>>(),
+                         (uint8_t*)d_points_out, s.flags.template as<uint32_t>() + 1);
     HIPCHK(hipGetLastError());
     return read_flags_sync(c, s);
   });
@@ -710,10 +700,68 @@ int kzgmi_gen_tuples(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* tau32, cons
     uint8_t sb[32];
     Seed seed = make_seed(seed32, sb);
     if (n)
-      k_gen_tuples<Cv><<<grid(n, 256), 256, 0, s.stream>>>(seed, tau, (uint32_t)n, c->table[Cv::ID].template as<Affine<Cv>>(),
+      Launch<Cv>::gen_tuples(s.stream, seed, tau.v, (uint32_t)n, c->table[Cv::ID].template as<Affine<Cv>>(),
                                                            (uint8_t*)dC, (uint8_t*)dz, (uint8_t*)dy, (uint8_t*)dpi);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s.stream));
+    return 0;
+  });
+}
+
+int kzgmi_g2_mul(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g2, const uint8_t* k32, uint8_t* out) {
+  CHK(check_ctx(c));
+  if (!g2 || !k32 || !out) return fail(KZGMI_ERR_ARG, "null argument");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    Slot& s = c->slots[0];
+    const size_t gb = g2_bytes(Cv::ID);
+    CHK(s.stage.ensure(2 * gb + 64));
+    CHK(s.inf.ensure(16));
+    CHK(s.flags.ensure(16));
+    CHK(c->tmp.ensure(2 * sizeof(G2Aff<Cv>)));
+    uint32_t k[8];
+    for (int j = 0; j < 8; ++j)
+      k[j] = (uint32_t)k32[31 - 4 * j] | (uint32_t)k32[30 - 4 * j] << 8 | (uint32_t)k32[29 - 4 * j] << 16 |
+             (uint32_t)k32[28 - 4 * j] << 24;
+    for (int j = 7; j >= 0; --j) {
+      if (k[j] < Cv::FrP::MOD[j]) break;
+      if (k[j] > Cv::FrP::MOD[j] || j == 0) return fail(KZGMI_ERR_SCALAR, "k >= r");
+    }
+    hipStream_t st = s.stream;
+    uint8_t* d = s.stage.template as<uint8_t>();
+    HIPCHK(hipMemcpyAsync(d, g2, gb, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
+    Launch<Cv>::convert_g2(st, d, 1, c->tmp.template as<G2Aff<Cv>>(), s.inf.template as<uint8_t>(),
+                           s.flags.template as<uint32_t>() + 1);
+    Launch<Cv>::g2_mul(st, c->tmp.template as<G2Aff<Cv>>(), s.inf.template as<uint8_t>(), k, d + gb);
+    HIPCHK(hipGetLastError());
+    CHK(read_flags_sync(c, s));
+    HIPCHK(hipMemcpy(out, d + gb, gb, hipMemcpyDeviceToHost));
+    return 0;
+  });
+}
+
+int kzgmi_probe_fpmul(kzgmi_ctx* c, kzgmi_curve curve, double* muls_per_s) {
+  CHK(check_ctx(c));
+  if (!muls_per_s) return fail(KZGMI_ERR_ARG, "null argument");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    Slot& s = c->slots[0];
+    const uint32_t blocks = 256 * 16, iters = 2048;
+    CHK(c->tmp.ensure((size_t)blocks * 256 * 4));
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    Launch<Cv>::fpmul_probe(s.stream, blocks, 16, c->tmp.template as<uint32_t>());  // warm-up
+    HIPCHK(hipEventRecord(e0, s.stream));
+    Launch<Cv>::fpmul_probe(s.stream, blocks, iters, c->tmp.template as<uint32_t>());
+    HIPCHK(hipEventRecord(e1, s.stream));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *muls_per_s = (double)blocks * 256.0 * iters * 8.0 / (ms * 1e-3);
     return 0;
   });
 }
@@ -722,13 +770,15 @@ int kzgmi_gen_tuples(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* tau32, cons
 int kzgmi_set_profiling(kzgmi_ctx* c, int on) {
   if (!c) return fail(KZGMI_ERR_ARG, "null context");
   c->profiling = on != 0;
+  for (int k = 0; k < kNumPhases; ++k) c->phase_ms[k] = 0;
+  c->phase_calls = 0;
   return 0;
 }
 
 int kzgmi_get_phase_ms(kzgmi_ctx* c, double* out, int max_n) {
   if (!c || !out) return fail(KZGMI_ERR_ARG, "null argument");
   int k = max_n < kNumPhases ? max_n : kNumPhases;
-  for (int i = 0; i < k; ++i) out[i] = c->phase_ms[i];
+  for (int i = 0; i < k; ++i) out[i] = c->phase_calls ? c->phase_ms[i] / c->phase_calls : 0.0;
   return k;
 }
 

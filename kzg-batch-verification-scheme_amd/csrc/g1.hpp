@@ -113,6 +113,18 @@ KZ_DEV Xyzz<Cv> xyzz_add(const Xyzz<Cv>& p, const Xyzz<Cv>& q) {
   return r;
 }
 
+// Call (non-inlined) forms for everything outside the bucket-accumulation hot loop:
+// reductions, window combination, generators, fix-ups.  Keeps code size and compile time
+// bounded (a fully inlined point addition is ~12k instructions).
+template <class Cv>
+__device__ __noinline__ Xyzz<Cv> xyzz_add_c(const Xyzz<Cv>& p, const Xyzz<Cv>& q) { return xyzz_add(p, q); }
+template <class Cv>
+__device__ __noinline__ Xyzz<Cv> xyzz_dbl_c(const Xyzz<Cv>& p) { return xyzz_dbl(p); }
+template <class Cv>
+__device__ __noinline__ Xyzz<Cv> xyzz_add_affine_c(const Xyzz<Cv>& p, const Affine<Cv>& q) { return xyzz_add_affine(p, q); }
+template <class P>
+__device__ __noinline__ Fp<P> fp_inv_c(const Fp<P>& a) { return fp_inv(a); }
+
 template <class Cv>
 KZ_DEV Xyzz<Cv> xyzz_neg(const Xyzz<Cv>& p) { return {p.x, fp_neg(p.y), p.zz, p.zzz}; }
 
@@ -120,7 +132,7 @@ KZ_DEV Xyzz<Cv> xyzz_neg(const Xyzz<Cv>& p) { return {p.x, fp_neg(p.y), p.zz, p.
 template <class Cv>
 KZ_DEV bool xyzz_to_affine(const Xyzz<Cv>& p, Affine<Cv>& out) {
   if (p.is_inf()) return false;
-  auto I = fp_inv(fp_mul(p.zz, p.zzz));
+  auto I = fp_inv_c(fp_mul(p.zz, p.zzz));
   out.x = fp_mul(p.x, fp_mul(p.zzz, I));
   out.y = fp_mul(p.y, fp_mul(p.zz, I));
   return true;

@@ -278,7 +278,7 @@ __global__ void k_sum_partials(const Xyzz<Cv>* __restrict__ parts, uint32_t npar
   uint32_t k = threadIdx.x;
   if (k >= nout) return;
   Xyzz<Cv> acc = Xyzz<Cv>::inf();
-  for (uint32_t j = 0; j < nparts; ++j) acc = xyzz_add(acc, load_xyzz(&parts[j * stride + k]));
+  for (uint32_t j = 0; j < nparts; ++j) acc = xyzz_add_c(acc, load_xyzz(&parts[j * stride + k]));
   store_xyzz(&out[k], acc);
 }
 
@@ -291,7 +291,7 @@ __global__ void k_gen_table_base(Xyzz<Cv>* __restrict__ base) {
   using P = typename Cv::FpP;
   Affine<Cv> g = {Fp<P>::from_const(Cv::K::G1X_M), Fp<P>::from_const(Cv::K::G1Y_M)};
   Xyzz<Cv> b = xyzz_from_affine(g);
-  for (uint32_t i = 0; i < 8 * j; ++i) b = xyzz_dbl(b);
+  for (uint32_t i = 0; i < 8 * j; ++i) b = xyzz_dbl_c(b);
   store_xyzz(&base[j], b);
 }
 template <class Cv>
@@ -301,8 +301,8 @@ __global__ void __launch_bounds__(256) k_gen_table(const Xyzz<Cv>* __restrict__ 
   Xyzz<Cv> b = load_xyzz(&base[j]);
   Xyzz<Cv> acc = Xyzz<Cv>::inf();
   for (int bit = 7; bit >= 0; --bit) {
-    acc = xyzz_dbl(acc);
-    if ((d >> bit) & 1) acc = xyzz_add(acc, b);
+    acc = xyzz_dbl_c(acc);
+    if ((d >> bit) & 1) acc = xyzz_add_c(acc, b);
   }
   Affine<Cv> a;
   xyzz_to_affine(acc, a);
@@ -315,7 +315,7 @@ KZ_DEV Xyzz<Cv> comb_mul(const Affine<Cv>* __restrict__ table, const Fp<typename
 #pragma unroll 4
   for (int j = 0; j < 32; ++j) {
     uint32_t byte = (k.v[j >> 2] >> (8 * (j & 3))) & 0xffu;
-    if (byte) acc = xyzz_add_affine(acc, load_affine(table, j * 256 + byte));
+    if (byte) acc = xyzz_add_affine_c(acc, load_affine(table, j * 256 + byte));
   }
   return acc;
 }
@@ -378,7 +378,7 @@ __global__ void __launch_bounds__(256) k_gen_tuples(Seed seed, Fp<typename Cv::F
   // q = (c - y) / (tau - z) mod r   (Montgomery domain for the product)
   F num = fp_sub(c, y);
   F den = fp_sub(tau, z);
-  F q = fp_from_mont(fp_mul(fp_to_mont(num), fp_inv(fp_to_mont(den))));
+  F q = fp_from_mont(fp_mul(fp_to_mont(num), fp_inv_c(fp_to_mont(den))));
   uint32_t wz[8], wy[8];
   fp_to_be_words(z, wz, 0);
   fp_to_be_words(y, wy, 0);
@@ -386,6 +386,70 @@ __global__ void __launch_bounds__(256) k_gen_tuples(Seed seed, Fp<typename Cv::F
   store_words(ys + (size_t)i * 32, wy);
   encode_xyzz_to(comb_mul(table, c), cm + (size_t)i * 8 * Cv::FpP::N);
   encode_xyzz_to(comb_mul(table, q), pf + (size_t)i * 8 * Cv::FpP::N);
+}
+
+}  // namespace kzgmi
+
+namespace kzgmi {
+
+// [k]_2 = k * Q on the twist by affine double-and-add (toy-SRS generation: one thread).
+template <class Cv>
+__global__ void k_g2_mul(const G2Aff<Cv>* __restrict__ q_in, const uint8_t* __restrict__ q_inf,
+                         Fp<typename Cv::FrP> k, uint8_t* __restrict__ out) {
+  using P = typename Cv::FpP;
+  if (threadIdx.x != 0) return;
+  G2Aff<Cv> Q = q_in[0], T = Q;
+  bool t_inf = true;
+  Line<Cv> dummy;
+  for (int i = 255; i >= 0; --i) {
+    if (!t_inf) {
+      if (T.y.is_zero()) t_inf = true;  // 2-torsion (not in the prime-order subgroup)
+      else line_dbl(T, dummy);
+    }
+    if ((k.v[i >> 5] >> (i & 31)) & 1) {
+      if (t_inf) { T = Q; t_inf = false; }
+      else if (T.x == Q.x) {
+        if (T.y == Q.y) line_dbl(T, dummy);
+        else t_inf = true;
+      } else line_add(T, Q, dummy);
+    }
+  }
+  constexpr int NW = 4 * P::N;
+  uint32_t w[NW];
+  if (t_inf || q_inf[0]) {
+    for (int j = 0; j < NW; ++j) w[j] = 0;
+    if constexpr (Cv::ID == 0) w[0] = 0x40u;
+  } else {
+    fp_to_be_words(fp_from_mont(T.x.c1), w, 0);
+    fp_to_be_words(fp_from_mont(T.x.c0), w, P::N);
+    fp_to_be_words(fp_from_mont(T.y.c1), w, 2 * P::N);
+    fp_to_be_words(fp_from_mont(T.y.c0), w, 3 * P::N);
+  }
+  store_words(out, w);
+}
+
+// Fp-multiplication throughput probe (compute roofline of the MSM): every thread runs
+// `iters` rounds of 8 independent Montgomery products.  out[] keeps the results live.
+template <class Cv>
+__global__ void __launch_bounds__(256) k_fpmul_probe(uint32_t iters, uint32_t* __restrict__ out) {
+  using P = typename Cv::FpP;
+  using F = Fp<P>;
+  F a[8];
+  F b = F::one();
+  b.v[0] ^= threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = F::one();
+    a[j].v[1] ^= (blockIdx.x * 8 + j);
+  }
+  for (uint32_t it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = fp_mul(a[j], b);
+  }
+  uint32_t x = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x ^= a[j].v[0] ^ a[j].v[P::N - 1];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
 }
 
 }  // namespace kzgmi

@@ -1,0 +1,61 @@
+// Host-side launchers for every kernel, one set per curve.  Each group of launchers is
+// defined in its own translation unit (launch_*.hip) compiled once per curve (-DKZ_CURVE=0
+// BLS12-381, 1 BN254), so the device code builds in parallel; api.hip only calls these.
+#pragma once
+#include "kernels.hpp"
+
+namespace kzgmi {
+
+template <class Cv>
+struct Launch {
+  using XY = Xyzz<Cv>;
+  using AF = Affine<Cv>;
+  // ---- MSM (launch_msm.hip)
+  static void digits(hipStream_t st, bool scatter, const TermList& tl, const uint8_t* inf, uint32_t* cnt_or_cursor,
+                     uint32_t* sval, uint32_t* skey);
+  static void scan(hipStream_t st, const uint32_t* cnt, uint32_t nb, uint32_t* off, uint32_t* blk, uint32_t* total,
+                   uint32_t* cursor);
+  static void accumulate(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* sval,
+                         const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts, XY* buckets,
+                         XY* pfirst, XY* plast);
+  static void reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const XY* buckets, XY* R, XY* U,
+                     XY* scratch, XY* winsum);
+  static void window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res);
+  // ---- I/O and scalars (launch_io.hip)
+  static void convert_points(hipStream_t st, const uint8_t* bytes, uint32_t n, AF* pts, uint8_t* inf, uint32_t* err);
+  static void set_generator(hipStream_t st, AF* pt, uint8_t* inf);
+  static void convert_scalars(hipStream_t st, const uint8_t* bytes, uint32_t n, uint32_t* out, uint32_t* err);
+  static void convert_g2(hipStream_t st, const uint8_t* bytes, uint32_t n, G2Aff<Cv>* out, uint8_t* inf,
+                         uint32_t* err);
+  static void scalar_prep(hipStream_t st, const Seed& seed, uint64_t index_offset, const uint8_t* zs,
+                          const uint8_t* ys, uint32_t n, uint32_t* r_out, uint32_t* s_out, void* tpart,
+                          uint32_t* negt, uint32_t* err);
+  static size_t tpart_bytes(uint32_t n);
+  static void encode_points(hipStream_t st, const XY* res, uint32_t count, uint8_t* out);
+  static void sum_partials(hipStream_t st, const XY* parts, uint32_t nparts, uint32_t stride, uint32_t nout, XY* out);
+  // ---- pairing (launch_pairing.hip)
+  static int num_lines();
+  static void precompute_lines(hipStream_t st, const G2Aff<Cv>* q, Line<Cv>* lines);
+  static void pairing_check(hipStream_t st, const XY* res, const Line<Cv>* lines, const uint8_t* q_inf, int* ok);
+  static void pairing_one(hipStream_t st, const AF* p, const uint8_t* p_inf, const Line<Cv>* lines,
+                          const uint8_t* q_inf, uint8_t* out);
+  // ---- generators (launch_gen.hip)
+  static void gen_table(hipStream_t st, XY* base, AF* table);
+  static void gen_g1(hipStream_t st, const uint8_t* scalars, uint32_t n, const AF* table, uint8_t* out, uint32_t* err);
+  static void g2_mul(hipStream_t st, const G2Aff<Cv>* q, const uint8_t* q_inf, const uint32_t (&k_le)[8], uint8_t* out);
+  static void fpmul_probe(hipStream_t st, uint32_t blocks, uint32_t iters, uint32_t* out);
+  static void gen_tuples(hipStream_t st, const Seed& seed, const uint32_t (&tau_le)[8], uint32_t n, const AF* table,
+                         uint8_t* cm, uint8_t* zs, uint8_t* ys, uint8_t* pf);
+};
+
+inline unsigned grid_for(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+}  // namespace kzgmi
+
+#if defined(KZ_CURVE)
+#if KZ_CURVE == 0
+#define KZ_CURVE_T ::kzgmi::Bls12_381
+#else
+#define KZ_CURVE_T ::kzgmi::Bn254
+#endif
+#endif

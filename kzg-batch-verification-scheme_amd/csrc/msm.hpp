@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(256) k_digits(TermList tl, const uint8_t* __re
 constexpr int SCAN_BLOCK = 256;
 constexpr int SCAN_ITEMS = 16;  // 4096 counts per block
 
-__global__ void __launch_bounds__(SCAN_BLOCK) k_scan_blocks(const uint32_t* __restrict__ cnt, uint32_t nb,
+static __global__ void __launch_bounds__(SCAN_BLOCK) k_scan_blocks(const uint32_t* __restrict__ cnt, uint32_t nb,
                                                            uint32_t* __restrict__ off, uint32_t* __restrict__ block_tot) {
   __shared__ uint32_t s[SCAN_BLOCK];
   uint32_t base = blockIdx.x * SCAN_BLOCK * SCAN_ITEMS + threadIdx.x * SCAN_ITEMS;
@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(SCAN_BLOCK) k_scan_blocks(const uint32_t* __re
 }
 
 // single block: exclusive scan of block totals (<= 1024 blocks), writes grand total
-__global__ void __launch_bounds__(1024) k_scan_totals(uint32_t* __restrict__ block_tot, uint32_t nblocks,
+static __global__ void __launch_bounds__(1024) k_scan_totals(uint32_t* __restrict__ block_tot, uint32_t nblocks,
                                                       uint32_t* __restrict__ total) {
   __shared__ uint32_t s[1024];
   uint32_t v = threadIdx.x < nblocks ? block_tot[threadIdx.x] : 0u;
@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(1024) k_scan_totals(uint32_t* __restrict__ blo
   if (threadIdx.x == 1023) *total = s[1023];
 }
 
-__global__ void __launch_bounds__(256) k_scan_add(uint32_t* __restrict__ off, uint32_t nb,
+static __global__ void __launch_bounds__(256) k_scan_add(uint32_t* __restrict__ off, uint32_t nb,
                                                   const uint32_t* __restrict__ block_tot,
                                                   uint32_t* __restrict__ cursor) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
   if (c0 != c - 1) return;                // a later continuation chunk: handled by c0+1
   uint32_t c1 = (o + cnt[key] - 1) / ACC_CHUNK;
   Xyzz<Cv> acc = load_xyzz(&part_last[c0]);
-  for (uint32_t cc = c; cc <= c1; ++cc) acc = xyzz_add(acc, load_xyzz(&part_first[cc]));
+  for (uint32_t cc = c; cc <= c1; ++cc) acc = xyzz_add_c(acc, load_xyzz(&part_first[cc]));
   store_xyzz(&buckets[key], acc);
 }
 
@@ -270,11 +270,11 @@ __global__ void __launch_bounds__(256) k_reduce_segments(uint32_t nseg, const ui
   Xyzz<Cv> run = Xyzz<Cv>::inf(), acc = Xyzz<Cv>::inf();
   for (int i = SEG - 1; i >= 1; --i) {
     uint32_t key = g * SEG + i;
-    if (cnt[key]) run = xyzz_add(run, load_xyzz(&buckets[key]));
-    acc = xyzz_add(acc, run);
+    if (cnt[key]) run = xyzz_add_c(run, load_xyzz(&buckets[key]));
+    acc = xyzz_add_c(acc, run);
   }
   uint32_t key0 = g * SEG;
-  if (cnt[key0]) run = xyzz_add(run, load_xyzz(&buckets[key0]));
+  if (cnt[key0]) run = xyzz_add_c(run, load_xyzz(&buckets[key0]));
   store_xyzz(&R[g], acc);
   store_xyzz(&U[g], run);
 }
@@ -286,7 +286,7 @@ KZ_DEV Xyzz<Cv> block_sum256(Xyzz<Cv> v, Xyzz<Cv>* lds) {
   for (int s = 128; s >= 1; s >>= 1) {
     if (t >= s && t < 2 * s) store_xyzz(&lds[t - s], v);
     __syncthreads();
-    if (t < s) v = xyzz_add(v, load_xyzz(&lds[t]));
+    if (t < s) v = xyzz_add_c(v, load_xyzz(&lds[t]));
     __syncthreads();
   }
   return v;  // valid in thread 0
@@ -297,17 +297,17 @@ template <class Cv>
 KZ_DEV void weighted16(const Xyzz<Cv>* src, uint32_t count, Xyzz<Cv>& R, Xyzz<Cv>& U) {
   Xyzz<Cv> run = Xyzz<Cv>::inf(), acc = Xyzz<Cv>::inf();
   for (int i = (int)count - 1; i >= 1; --i) {
-    run = xyzz_add(run, load_xyzz(&src[i]));
-    acc = xyzz_add(acc, run);
+    run = xyzz_add_c(run, load_xyzz(&src[i]));
+    acc = xyzz_add_c(acc, run);
   }
-  if (count) run = xyzz_add(run, load_xyzz(&src[0]));
+  if (count) run = xyzz_add_c(run, load_xyzz(&src[0]));
   R = acc;
   U = run;
 }
 
 template <class Cv>
 KZ_DEV Xyzz<Cv> xyzz_mul_pow2(Xyzz<Cv> p, int k) {
-  for (int i = 0; i < k; ++i) p = xyzz_dbl(p);
+  for (int i = 0; i < k; ++i) p = xyzz_dbl_c(p);
   return p;
 }
 
@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(256) k_reduce_finish(const Xyzz<Cv>* __restric
   const int t = threadIdx.x;
   // (1) sum_g (R_g + U_g)
   Xyzz<Cv> s = Xyzz<Cv>::inf();
-  for (uint32_t g = t; g < NSEG; g += 256) s = xyzz_add(xyzz_add(s, load_xyzz(&Rs[g])), load_xyzz(&Us[g]));
+  for (uint32_t g = t; g < NSEG; g += 256) s = xyzz_add_c(xyzz_add_c(s, load_xyzz(&Rs[g])), load_xyzz(&Us[g]));
   Xyzz<Cv> part1 = block_sum256(s, lds);
   // (2) level 2: 128 threads, 16 U's each -> R2_j, U2_j
   if (t < (int)(NSEG / SEG)) {
@@ -352,12 +352,12 @@ __global__ void __launch_bounds__(256) k_reduce_finish(const Xyzz<Cv>* __restric
   __syncthreads();
   if (t == 0) {
     Xyzz<Cv> sumR3 = Xyzz<Cv>::inf();
-    for (int j = 0; j < 8; ++j) sumR3 = xyzz_add(sumR3, load_xyzz(&r3[j]));
+    for (int j = 0; j < 8; ++j) sumR3 = xyzz_add_c(sumR3, load_xyzz(&r3[j]));
     Xyzz<Cv> r, u;
     weighted16(u3, 8, r, u);                      // W3 = sum_j j U3_j
-    Xyzz<Cv> W2 = xyzz_add(sumR3, xyzz_mul_pow2(r, 4));   // sum_j j U2_j
-    Xyzz<Cv> V = xyzz_add(sumR2, xyzz_mul_pow2(W2, 4));   // sum_g g U_g
-    Xyzz<Cv> W = xyzz_add(part1, xyzz_mul_pow2(V, 4));
+    Xyzz<Cv> W2 = xyzz_add_c(sumR3, xyzz_mul_pow2(r, 4));   // sum_j j U2_j
+    Xyzz<Cv> V = xyzz_add_c(sumR2, xyzz_mul_pow2(W2, 4));   // sum_g g U_g
+    Xyzz<Cv> W = xyzz_add_c(part1, xyzz_mul_pow2(V, 4));
     store_xyzz(&winsum[set], W);
   }
 }
@@ -376,7 +376,7 @@ __global__ void k_window_combine(MsmWindows mw, const Xyzz<Cv>* __restrict__ win
   Xyzz<Cv> acc = load_xyzz(&W[mw.nwin[m] - 1]);
   for (int w = (int)mw.nwin[m] - 2; w >= 0; --w) {
     acc = xyzz_mul_pow2(acc, WBITS);
-    acc = xyzz_add(acc, load_xyzz(&W[w]));
+    acc = xyzz_add_c(acc, load_xyzz(&W[w]));
   }
   store_xyzz(&res[m], acc);
 }

@@ -77,6 +77,8 @@ def lib():
         "kzgmi_pairing": ([vp, c.c_int, u8p, u8p, u8p], c.c_int),
         "kzgmi_gen_g1": ([vp, c.c_int, vp, sz, vp], c.c_int),
         "kzgmi_gen_tuples": ([vp, c.c_int, u8p, u8p, sz, vp, vp, vp, vp], c.c_int),
+        "kzgmi_g2_mul": ([vp, c.c_int, u8p, u8p, u8p], c.c_int),
+        "kzgmi_probe_fpmul": ([vp, c.c_int, c.POINTER(c.c_double)], c.c_int),
         "kzgmi_set_profiling": ([vp, c.c_int], c.c_int),
         "kzgmi_get_phase_ms": ([vp, c.POINTER(c.c_double), c.c_int], c.c_int),
     }
@@ -96,7 +98,7 @@ def exported_symbols():
         "kzgmi_last_combination", "kzgmi_msm_g1", "kzgmi_msm_g1_device", "kzgmi_partial_bytes",
         "kzgmi_batch_partial_device", "kzgmi_batch_combine_device", "kzgmi_msm_partial_device",
         "kzgmi_msm_combine_device", "kzgmi_pairing", "kzgmi_gen_g1", "kzgmi_gen_tuples",
-        "kzgmi_set_profiling", "kzgmi_get_phase_ms",
+        "kzgmi_g2_mul", "kzgmi_probe_fpmul", "kzgmi_set_profiling", "kzgmi_get_phase_ms",
     ]
 
 
@@ -262,6 +264,21 @@ class Context:
         _check(lib().kzgmi_gen_tuples(self.handle, CURVES[curve], int(tau).to_bytes(32, "big"), bytes(seed), n,
                                       _dptr(C), _dptr(z), _dptr(y), _dptr(pi)))
 
+    def g2_mul(self, curve: str, g2: bytes, k: int) -> bytes:
+        out = ctypes.create_string_buffer(4 * FP_BYTES[curve])
+        _check(lib().kzgmi_g2_mul(self.handle, CURVES[curve], bytes(g2), int(k).to_bytes(32, "big"), out))
+        return out.raw
+
+    def toy_srs(self, curve: str, tau: int):
+        """(G2 generator, [tau]_2) encodings computed on the GPU (test/bench SRS)."""
+        g2 = G2_GENERATOR[curve]
+        return g2, self.g2_mul(curve, g2, tau)
+
+    def probe_fpmul(self, curve: str) -> float:
+        v = ctypes.c_double()
+        _check(lib().kzgmi_probe_fpmul(self.handle, CURVES[curve], ctypes.byref(v)))
+        return v.value
+
     def set_profiling(self, on: bool):
         _check(lib().kzgmi_set_profiling(self.handle, 1 if on else 0))
 
@@ -272,6 +289,20 @@ class Context:
 
 
 # ---------------------------------------------------------------------- north-star API
+# Standard G2 generators (ZCash / EIP-197 encodings, imaginary part first)
+G2_GENERATOR = {
+    "bls12_381": bytes.fromhex(
+        "13e02b6052719f607dacd3a088274f65596bd0d09920b61ab5da61bbdc7f5049334cf11213945d57e5ac7d055d042b7e"
+        "024aa2b2f08f0a91260805272dc51051c6e47ad4fa403b02b4510b647ae3d1770bac0326a805bbefd48056c8c121bdb8"
+        "0606c4a02ea734cc32acd2b02bc28b99cb3e287e85a763af267492ab572e99ab3f370d275cec1da1aaa9075ff05f79be"
+        "0ce5d527727d6e118cc9cdc6da2e351aadfd9baa8cbdd3a76d429a695160d12c923ac9cc3baca289e193548608b82801"),
+    "bn254": b"".join(v.to_bytes(32, "big") for v in (
+        11559732032986387107991004021392285783925812861821192530917403151452391805634,
+        10857046999023057135944570762232829481370756359578518086990519993285655852781,
+        4082367875863433681332203403145435568316851327593401208105741076214120093531,
+        8495653923123431417604973247489272438418190587263600148770280649306958101930)),
+}
+
 _default_ctx: Optional[Context] = None
 
 
