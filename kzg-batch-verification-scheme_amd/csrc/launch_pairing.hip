@@ -1,5 +1,6 @@
 // Pairing launchers (compiled once per curve).  Kernels: pairing.hpp / kernels.hpp.
 #include "launch.hpp"
+#include "pairing_par.hpp"
 
 namespace kzgmi {
 
@@ -11,12 +12,12 @@ void Launch<Cv>::precompute_lines(hipStream_t st, const G2Aff<Cv>* q, Line<Cv>* 
 }
 template <class Cv>
 void Launch<Cv>::pairing_check(hipStream_t st, const XY* res, const Line<Cv>* lines, const uint8_t* q_inf, int* ok) {
-  k_pairing_check<Cv><<<1, 64, 0, st>>>(res, lines, q_inf, ok);
+  k_pairing_check_par<Cv><<<1, PAR_THREADS, 0, st>>>(res, lines, q_inf, ok);
 }
 template <class Cv>
 void Launch<Cv>::pairing_one(hipStream_t st, const AF* p, const uint8_t* p_inf, const Line<Cv>* lines,
                              const uint8_t* q_inf, uint8_t* out) {
-  k_pairing_one<Cv><<<1, 64, 0, st>>>(p, p_inf, lines, q_inf, out);
+  k_pairing_one_par<Cv><<<1, PAR_THREADS, 0, st>>>(p, p_inf, lines, q_inf, out);
 }
 
 using C_ = KZ_CURVE_T;

@@ -1,0 +1,548 @@
+"""Generate csrc/bilinear_gen.hpp: one-round bilinear programs for the wavefront-parallel pairing.
+
+Every Fp12 operation of the pairing (Karatsuba multiplication, complex squaring,
+Granger-Scott cyclotomic squaring, sparse line products, Frobenius, the steps of the Fp12
+inversion, line evaluation) has the shape
+
+    out_k = sum_t c_kt * X_t  +  sum_j d_kj * (L_j . R_j)
+
+where X_t are input Fp coefficients, L_j / R_j are linear forms (small integer coefficients)
+over the inputs (or constants), and c, d are small integers.  Symbolically executing the
+tower formulas with "linear-form" field elements yields those tables.  On the GPU one
+workgroup evaluates a table in one round: lane j computes L_j, R_j and one Montgomery
+product, then lane k sums its output -- the latency of ONE Fp product instead of ~54 in a row.
+
+Sources: 0 = operand A, 1 = operand B, 2 = constant table (Frobenius gammas, per curve).
+Reference: none (LICENSE only); formulas as in csrc/tower.hpp; tables are self-checked here
+numerically against direct tower arithmetic on random inputs, and on the GPU against the oracle.
+
+    python kzg-batch-verification-scheme_amd/tools/gen_bilinear.py
+"""
+import os
+import random
+
+# ----------------------------------------------------------------------------- symbolic Fp
+
+
+class Ctx:
+    def __init__(self):
+        self.prods = []   # list of (left dict, right dict)
+        self.cache = {}
+
+    def product(self, L, R):
+        # canonical, deduplicate identical products
+        key = (tuple(sorted(L.items())), tuple(sorted(R.items())))
+        key2 = (key[1], key[0])
+        if key in self.cache:
+            return self.cache[key]
+        if key2 in self.cache:
+            return self.cache[key2]
+        j = len(self.prods)
+        self.prods.append((dict(L), dict(R)))
+        self.cache[key] = j
+        return j
+
+
+class S:
+    """Symbolic Fp element: linear form {atom: coeff}; atom = ('A'|'B'|'K', i) or ('P', j)."""
+    ctx = None
+
+    def __init__(self, d=None):
+        self.d = {k: v for k, v in (d or {}).items() if v != 0}
+
+    @staticmethod
+    def atom(src, i):
+        return S({(src, i): 1})
+
+    @staticmethod
+    def zero():
+        return S()
+
+    def __add__(self, o):
+        d = dict(self.d)
+        for k, v in o.d.items():
+            d[k] = d.get(k, 0) + v
+        return S(d)
+
+    def __sub__(self, o):
+        d = dict(self.d)
+        for k, v in o.d.items():
+            d[k] = d.get(k, 0) - v
+        return S(d)
+
+    def __neg__(self):
+        return S({k: -v for k, v in self.d.items()})
+
+    def smul(self, c):
+        return S({k: v * c for k, v in self.d.items()})
+
+    def is_zero(self):
+        return not self.d
+
+    def __mul__(self, o):
+        if self.is_zero() or o.is_zero():
+            return S()
+        for k in list(self.d) + list(o.d):
+            assert k[0] != "P", "operand depends on a product: not a one-round map"
+        # pure constant x constant never happens here
+        j = S.ctx.product(self.d, o.d)
+        return S({("P", j): 1})
+
+
+# ----------------------------------------------------------------------------- tower (symbolic)
+class F2:
+    def __init__(self, c0, c1):
+        self.c0, self.c1 = c0, c1
+
+    @staticmethod
+    def zero():
+        return F2(S.zero(), S.zero())
+
+    def __add__(self, o): return F2(self.c0 + o.c0, self.c1 + o.c1)
+    def __sub__(self, o): return F2(self.c0 - o.c0, self.c1 - o.c1)
+    def __neg__(self): return F2(-self.c0, -self.c1)
+    def dbl(self): return self + self
+    def conj(self): return F2(self.c0, -self.c1)
+    def is_zero(self): return self.c0.is_zero() and self.c1.is_zero()
+
+    def __mul__(self, o):
+        if self.is_zero() or o.is_zero():
+            return F2.zero()
+        if self.c1.is_zero() and o.c1.is_zero():
+            return F2(self.c0 * o.c0, S.zero())
+        if self.c1.is_zero():
+            return F2(self.c0 * o.c0, self.c0 * o.c1)
+        if o.c1.is_zero():
+            return F2(self.c0 * o.c0, self.c1 * o.c0)
+        t0 = self.c0 * o.c0
+        t1 = self.c1 * o.c1
+        t2 = (self.c0 + self.c1) * (o.c0 + o.c1)
+        return F2(t0 - t1, t2 - t0 - t1)
+
+    def sqr(self):
+        if self.c1.is_zero():
+            return F2(self.c0 * self.c0, S.zero())
+        t = self.c0 * self.c1
+        return F2((self.c0 + self.c1) * (self.c0 - self.c1), t + t)
+
+    def mul_fp(self, s):
+        return F2(self.c0 * s, self.c1 * s)
+
+    def mul_xi(self, curve):
+        if curve == "bls12_381":
+            return F2(self.c0 - self.c1, self.c0 + self.c1)
+        return F2(self.c0.smul(9) - self.c1, self.c0 + self.c1.smul(9))
+
+
+class F6:
+    def __init__(self, c0, c1, c2, curve):
+        self.c0, self.c1, self.c2, self.cv = c0, c1, c2, curve
+
+    def __add__(self, o): return F6(self.c0 + o.c0, self.c1 + o.c1, self.c2 + o.c2, self.cv)
+    def __sub__(self, o): return F6(self.c0 - o.c0, self.c1 - o.c1, self.c2 - o.c2, self.cv)
+    def __neg__(self): return F6(-self.c0, -self.c1, -self.c2, self.cv)
+    def mul_v(self): return F6(self.c2.mul_xi(self.cv), self.c0, self.c1, self.cv)
+
+    def __mul__(self, b):
+        a = self
+        t0, t1, t2 = a.c0 * b.c0, a.c1 * b.c1, a.c2 * b.c2
+        c0 = t0 + ((a.c1 + a.c2) * (b.c1 + b.c2) - t1 - t2).mul_xi(self.cv)
+        c1 = (a.c0 + a.c1) * (b.c0 + b.c1) - t0 - t1 + t2.mul_xi(self.cv)
+        c2 = (a.c0 + a.c2) * (b.c0 + b.c2) - t0 - t2 + t1
+        return F6(c0, c1, c2, self.cv)
+
+    def mul_f2(self, s): return F6(self.c0 * s, self.c1 * s, self.c2 * s, self.cv)
+
+
+class F12:
+    def __init__(self, c0, c1):
+        self.c0, self.c1 = c0, c1
+
+    def __mul__(self, b):
+        a = self
+        t0 = a.c0 * b.c0
+        t1 = a.c1 * b.c1
+        c1 = (a.c0 + a.c1) * (b.c0 + b.c1) - t0 - t1
+        return F12(t0 + t1.mul_v(), c1)
+
+    def sqr(self):
+        ab = self.c0 * self.c1
+        t = (self.c0 + self.c1) * (self.c0 + self.c1.mul_v())
+        return F12(t - ab - ab.mul_v(), ab + ab)
+
+    def conj(self): return F12(self.c0, -self.c1)
+
+    def coeffs(self):  # tower order: c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2 (each c0, c1)
+        out = []
+        for f6 in (self.c0, self.c1):
+            for f2 in (f6.c0, f6.c1, f6.c2):
+                out += [f2.c0, f2.c1]
+        return out
+
+
+def f12_from(src, cv):
+    a = [S.atom(src, i) for i in range(12)]
+    f2 = [F2(a[2 * k], a[2 * k + 1]) for k in range(6)]
+    return F12(F6(f2[0], f2[1], f2[2], cv), F6(f2[3], f2[4], f2[5], cv))
+
+
+def fp4_sqr(a, b, cv):
+    t0 = a.sqr()
+    t1 = b.sqr()
+    return t1.mul_xi(cv) + t0, (a + b).sqr() - t0 - t1
+
+
+def cyclo_sqr(f, cv):
+    z0, z1 = f.c0.c0, f.c1.c1
+    z2, z3 = f.c1.c0, f.c0.c2
+    z4, z5 = f.c0.c1, f.c1.c2
+    t0, t1 = fp4_sqr(z0, z1, cv)
+    t2, t3 = fp4_sqr(z2, z3, cv)
+    t4, t5 = fp4_sqr(z4, z5, cv)
+    r00 = (t0 - z0).dbl() + t0
+    r11 = (t1 + z1).dbl() + t1
+    xt5 = t5.mul_xi(cv)
+    r10 = (xt5 + z2).dbl() + xt5
+    r02 = (t4 - z3).dbl() + t4
+    r01 = (t2 - z4).dbl() + t2
+    r12 = (t3 + z5).dbl() + t3
+    return F12(F6(r00, r01, r02, cv), F6(r10, r11, r12, cv))
+
+
+def line_f12(a, b, c, cv):
+    """Sparse line as an Fp12: M-type a + b w^2 + c w^3; D-type a + b w + c w^3."""
+    z = F2.zero()
+    if cv == "bls12_381":
+        return F12(F6(a, b, z, cv), F6(z, c, z, cv))
+    return F12(F6(a, z, z, cv), F6(b, c, z, cv))
+
+
+def line_from(src, cv):
+    x = [S.atom(src, i) for i in range(6)]
+    return line_f12(F2(x[0], x[1]), F2(x[2], x[3]), F2(x[4], x[5]), cv)
+
+
+# ----------------------------------------------------------------------------- programs
+def build_op(fn, cv):
+    S.ctx = Ctx()
+    outs = fn(cv)
+    prods = S.ctx.prods
+    return prods, outs
+
+
+def op_mul(cv):
+    return (f12_from("A", cv) * f12_from("B", cv)).coeffs()
+
+
+def op_sqr(cv):
+    return f12_from("A", cv).sqr().coeffs()
+
+
+def op_cyc(cv):
+    return cyclo_sqr(f12_from("A", cv), cv).coeffs()
+
+
+def op_conj(cv):
+    return f12_from("A", cv).conj().coeffs()
+
+
+def op_line(cv):  # f * line(B)
+    return (f12_from("A", cv) * line_from("B", cv)).coeffs()
+
+
+def op_ll(cv):  # line(A) * line(B)
+    return (line_from("A", cv) * line_from("B", cv)).coeffs()
+
+
+def op_frob(k):
+    def fn(cv):
+        f = f12_from("A", cv)
+        out = []
+        # w^i order: c0.c0 w0, c1.c0 w1, c0.c1 w2, c1.c1 w3, c0.c2 w4, c1.c2 w5
+        pos = {("c0", 0): 0, ("c1", 0): 1, ("c0", 1): 2, ("c1", 1): 3, ("c0", 2): 4, ("c1", 2): 5}
+        res = {}
+        for half in ("c0", "c1"):
+            f6 = getattr(f, half)
+            for j, f2 in enumerate((f6.c0, f6.c1, f6.c2)):
+                i = pos[(half, j)]
+                y = f2.conj() if k & 1 else f2
+                if i > 0:
+                    g = F2(S.atom("K", 12 * (k - 1) + 2 * i), S.atom("K", 12 * (k - 1) + 2 * i + 1))
+                    y = y * g
+                res[(half, j)] = y
+        for half in ("c0", "c1"):
+            for j in range(3):
+                out += [res[(half, j)].c0, res[(half, j)].c1]
+        return out
+    return fn
+
+
+# Fp12 inverse, split in one-round stages (A/B = stage inputs)
+def op_inv_norm(cv):  # A = f (12) -> t = c0^2 - v c1^2 (Fp6, 6)
+    f = f12_from("A", cv)
+    t = f.c0 * f.c0 - (f.c1 * f.c1).mul_v()
+    return [t.c0.c0, t.c0.c1, t.c1.c0, t.c1.c1, t.c2.c0, t.c2.c1]
+
+
+def f6_from(src, cv):
+    a = [S.atom(src, i) for i in range(6)]
+    return F6(F2(a[0], a[1]), F2(a[2], a[3]), F2(a[4], a[5]), cv)
+
+
+def op_inv6_t(cv):  # A = a (Fp6) -> (t0, t1, t2)
+    a = f6_from("A", cv)
+    t0 = a.c0.sqr() - (a.c1 * a.c2).mul_xi(cv)
+    t1 = a.c2.sqr().mul_xi(cv) - a.c0 * a.c1
+    t2 = a.c1.sqr() - a.c0 * a.c2
+    return [t0.c0, t0.c1, t1.c0, t1.c1, t2.c0, t2.c1]
+
+
+def op_inv6_d(cv):  # A = a (Fp6), B = t (Fp6) -> d = a0 t0 + xi (a2 t1 + a1 t2) (Fp2)
+    a = f6_from("A", cv)
+    t = f6_from("B", cv)
+    d = a.c0 * t.c0 + (a.c2 * t.c1 + a.c1 * t.c2).mul_xi(cv)
+    return [d.c0, d.c1]
+
+
+def op_inv2_n(cv):  # A = d (Fp2) -> d0^2 + d1^2
+    d0, d1 = S.atom("A", 0), S.atom("A", 1)
+    return [d0 * d0 + d1 * d1]
+
+
+def op_inv2_fin(cv):  # A = d (2), B = ninv (1) -> (d0 ninv, -d1 ninv)
+    d0, d1, ni = S.atom("A", 0), S.atom("A", 1), S.atom("B", 0)
+    return [d0 * ni, -(d1 * ni)]
+
+
+def op_inv6_fin(cv):  # A = t (6), B = dinv (2) -> t * dinv (Fp6)
+    t = f6_from("A", cv)
+    di = F2(S.atom("B", 0), S.atom("B", 1))
+    r = t.mul_f2(di)
+    return [r.c0.c0, r.c0.c1, r.c1.c0, r.c1.c1, r.c2.c0, r.c2.c1]
+
+
+def op_inv12_fin(cv):  # A = f (12), B = tinv (Fp6) -> (c0 tinv, -c1 tinv)
+    f = f12_from("A", cv)
+    ti = f6_from("B", cv)
+    r = F12(f.c0 * ti, -(f.c1 * ti))
+    return r.coeffs()
+
+
+def op_leval(cv):
+    """Line value at a homogeneous G1 point.  A = (c.c0, c.c1, lam.c0, lam.c1), B = (X, Y, Z).
+    M-type: (c Z, lam X, -Y);  D-type: (-Y, lam X, c Z)  as 3 Fp2 = 6 Fp."""
+    c = F2(S.atom("A", 0), S.atom("A", 1))
+    lam = F2(S.atom("A", 2), S.atom("A", 3))
+    X, Y, Z = S.atom("B", 0), S.atom("B", 1), S.atom("B", 2)
+    cz = c.mul_fp(Z)
+    lx = lam.mul_fp(X)
+    ny = F2(-Y, S.zero())
+    if cv == "bls12_381":
+        parts = (cz, lx, ny)
+    else:
+        parts = (ny, lx, cz)
+    out = []
+    for p in parts:
+        out += [p.c0, p.c1]
+    return out
+
+
+OPS = [
+    ("MUL", op_mul), ("SQR", op_sqr), ("CYC", op_cyc), ("CONJ", op_conj), ("LINE", op_line), ("LL", op_ll),
+    ("FROB1", op_frob(1)), ("FROB2", op_frob(2)), ("FROB3", op_frob(3)),
+    ("INV_NORM", op_inv_norm), ("INV6_T", op_inv6_t), ("INV6_D", op_inv6_d), ("INV2_N", op_inv2_n),
+    ("INV2_FIN", op_inv2_fin), ("INV6_FIN", op_inv6_fin), ("INV12_FIN", op_inv12_fin), ("LEVAL", op_leval),
+]
+
+SRC = {"A": 0, "B": 1, "K": 2}
+
+# ----------------------------------------------------------------------------- numeric self-check
+P = {"bls12_381": 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB,
+     "bn254": 21888242871839275222246405745257275088696311157297823662689037894645226208583}
+XI = {"bls12_381": (1, 1), "bn254": (9, 1)}
+
+
+def f2m(a, b, p):
+    return ((a[0] * b[0] - a[1] * b[1]) % p, (a[0] * b[1] + a[1] * b[0]) % p)
+
+
+def f2pow(a, e, p):
+    r = (1, 0)
+    for bit in bin(e)[2:]:
+        r = f2m(r, r, p)
+        if bit == "1":
+            r = f2m(r, a, p)
+    return r
+
+
+def consts(cv):
+    p = P[cv]
+    out = []
+    for k in (1, 2, 3):
+        for i in range(6):
+            g = f2pow(XI[cv], i * (p ** k - 1) // 6, p)
+            out += [g[0], g[1]]
+    return out
+
+
+def evaluate(prods, outs, A, B, K, p):
+    def ev(d, pv):
+        s = 0
+        for (src, i), c in d.items():
+            if src == "A":
+                s += c * A[i]
+            elif src == "B":
+                s += c * B[i]
+            elif src == "K":
+                s += c * K[i]
+            else:
+                s += c * pv[i]
+        return s % p
+    pv = [ev(L, None) * ev(R, None) % p for L, R in prods]
+    return [ev(o.d, pv) for o in outs]
+
+
+# direct numeric tower for the check (schoolbook over w: Fp12 = Fp2[w]/(w^6 - xi))
+def to_w(c12):
+    # tower coeff order -> w-power order list of Fp2
+    f2 = [(c12[2 * k], c12[2 * k + 1]) for k in range(6)]  # c0.c0,c0.c1,c0.c2,c1.c0,c1.c1,c1.c2
+    return [f2[0], f2[3], f2[1], f2[4], f2[2], f2[5]]
+
+
+def from_w(w):
+    order = [w[0], w[2], w[4], w[1], w[3], w[5]]
+    out = []
+    for x in order:
+        out += [x[0], x[1]]
+    return out
+
+
+def wmul(a, b, cv):
+    p = P[cv]
+    r = [(0, 0)] * 12
+    for i in range(6):
+        for j in range(6):
+            t = f2m(a[i], b[j], p)
+            r[i + j] = ((r[i + j][0] + t[0]) % p, (r[i + j][1] + t[1]) % p)
+    out = []
+    for k in range(6):
+        hi = f2m(r[k + 6], XI[cv], p)
+        out.append(((r[k][0] + hi[0]) % p, (r[k][1] + hi[1]) % p))
+    return out
+
+
+def selfcheck(cv, tables):
+    p = P[cv]
+    rnd = random.Random(1)
+    K = consts(cv)
+    A = [rnd.randrange(p) for _ in range(12)]
+    B = [rnd.randrange(p) for _ in range(12)]
+    prods, outs = tables["MUL"]
+    assert evaluate(prods, outs, A, B, K, p) == from_w(wmul(to_w(A), to_w(B), cv)), "MUL"
+    prods, outs = tables["SQR"]
+    assert evaluate(prods, outs, A, B, K, p) == from_w(wmul(to_w(A), to_w(A), cv)), "SQR"
+    # frobenius = A^(p^k)
+    for k in (1, 2, 3):
+        prods, outs = tables["FROB%d" % k]
+        got = evaluate(prods, outs, A, B, K, p)
+        w = to_w(A)
+        r = [(1, 0)] + [(0, 0)] * 5
+        # naive power would be too slow; check frob1 via frob1(a*b) == frob1(a)*frob1(b)
+        got_b = evaluate(prods, outs, B, A, K, p)
+        ab = from_w(wmul(to_w(A), to_w(B), cv))
+        got_ab = evaluate(prods, outs, ab, A, K, p)
+        assert got_ab == from_w(wmul(to_w(got), to_w(got_b), cv)), "FROB%d multiplicative" % k
+        del r, w
+    # inverse pipeline
+    f = A
+
+    def run(name, X, Y=None):
+        pr, ou = tables[name]
+        return evaluate(pr, ou, X, Y or [0] * 12, K, p)
+    t = run("INV_NORM", f)
+    t6 = run("INV6_T", t)
+    d = run("INV6_D", t, t6)
+    nrm = run("INV2_N", d)
+    ni = [pow(nrm[0], -1, p)]
+    di = run("INV2_FIN", d, ni)
+    ti = run("INV6_FIN", t6, di)
+    finv = run("INV12_FIN", f, ti)
+    one = from_w(wmul(to_w(f), to_w(finv), cv))
+    assert one == [1] + [0] * 11, "INV"
+    # sparse line products
+    L = [rnd.randrange(p) for _ in range(6)]
+    L2 = [rnd.randrange(p) for _ in range(6)]
+
+    def line_full(x):
+        z = (0, 0)
+        a, b, c = (x[0], x[1]), (x[2], x[3]), (x[4], x[5])
+        if cv == "bls12_381":
+            w = [a, z, b, c, z, z]
+        else:
+            w = [a, b, z, c, z, z]
+        return from_w(w)
+    assert run("LINE", A, L) == from_w(wmul(to_w(A), to_w(line_full(L)), cv)), "LINE"
+    assert run("LL", L, L2) == from_w(wmul(to_w(line_full(L)), to_w(line_full(L2)), cv)), "LL"
+    assert run("CONJ", A) == A[:6] + [(-x) % p for x in A[6:]], "CONJ"
+
+
+# ----------------------------------------------------------------------------- emit
+def emit():
+    lines = ["// GENERATED by tools/gen_bilinear.py -- do not edit.",
+             "// One-round bilinear programs for the wavefront-parallel pairing (pairing_par.hpp).",
+             "#pragma once", "#include <hip/hip_runtime.h>", "#include <cstdint>", "namespace kzgmi {", ""]
+    stats = {}
+    for cv, tag in (("bls12_381", "Bls"), ("bn254", "Bn")):
+        tables = {name: build_op(fn, cv) for name, fn in OPS}
+        selfcheck(cv, tables)
+        # flatten: terms are (src<<5 | idx, coeff)
+        terms = []
+        desc = []
+        for name, _ in OPS:
+            prods, outs = tables[name]
+            base_prod = len(terms)
+            prod_idx = []
+            for L, R in prods:
+                for side in (L, R):
+                    prod_idx.append(len(terms))
+                    for (src, i), c in sorted(side.items()):
+                        terms.append((SRC[src] << 6 | i, c))
+                    terms.append((255, 0))  # end marker
+            out_idx = []
+            for o in outs:
+                out_idx.append(len(terms))
+                for (src, i), c in sorted(o.d.items(), key=lambda kv: (kv[0][0] != "P", kv[0])):
+                    code = (3 << 6 | i) if src == "P" else (SRC[src] << 6 | i)
+                    terms.append((code, c))
+                terms.append((255, 0))
+            desc.append((name, len(prods), len(outs), prod_idx, out_idx))
+            stats[(cv, name)] = (len(prods), len(outs), max([len(o.d) for o in outs] or [0]))
+        assert len(terms) < 65536
+        pfx = "k%s_" % tag
+        nl = 12 if cv == "bls12_381" else 8
+        R = 1 << (32 * nl)
+        Kv = [k * R % p_mod for k in consts(cv)] if (p_mod := P[cv]) else []
+        lines.append("static __constant__ uint8_t %sTERM_CODE[%d] = {%s};" % (pfx, len(terms), ", ".join(str(t[0]) for t in terms)))
+        lines.append("static __constant__ int8_t %sTERM_COEF[%d] = {%s};" % (pfx, len(terms), ", ".join(str(t[1]) for t in terms)))
+        lines.append("static __constant__ uint32_t %sK[36][%d] = {%s};" % (pfx, nl, ", ".join(
+            "{" + ", ".join("0x%08xu" % ((v >> (32 * i)) & 0xffffffff) for i in range(nl)) + "}" for v in Kv)))
+        for name, np_, no, pidx, oidx in desc:
+            lines.append("// %s: %d products, %d outputs" % (name, np_, no))
+            lines.append("static __constant__ uint16_t %s%s_P[%d] = {%s};" % (pfx, name, max(1, len(pidx)), ", ".join(map(str, pidx or [0]))))
+            lines.append("static __constant__ uint16_t %s%s_O[%d] = {%s};" % (pfx, name, len(oidx), ", ".join(map(str, oidx))))
+        lines.append("struct %sOpsInfo {" % tag)
+        for name, np_, no, pidx, oidx in desc:
+            lines.append("  static constexpr int %s_NP = %d, %s_NO = %d;" % (name, np_, name, no))
+        lines.append("};")
+        lines.append("")
+    lines.append("}  // namespace kzgmi")
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "bilinear_gen.hpp")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    for k, v in sorted(stats.items()):
+        print("%-10s %-10s products=%3d outputs=%2d max_out_terms=%d" % (k[0], k[1], v[0], v[1], v[2]))
+    print("wrote", path)
+
+
+if __name__ == "__main__":
+    emit()
