@@ -108,7 +108,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=1 << 20, help="tuples per GPU")
     ap.add_argument("--curve", default="bls12_381", choices=["bls12_381", "bn254"])
-    ap.add_argument("--slots", type=int, default=2, help="pipeline depth (single GPU)")
+    ap.add_argument("--slots", type=int, default=3, help="pipeline depth (single GPU)")
     ap.add_argument("--msm-steps", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -195,6 +195,7 @@ def main():
 
     # ---- single-batch latency (not pipelined), rank 0 view
     lat = None
+    phases_single = None
     if world == 1:
         ts = []
         for _ in range(3):
@@ -203,6 +204,11 @@ def main():
             assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n)
             ts.append(time.perf_counter() - a)
         lat = 1e3 * min(ts)
+        ctx.set_profiling(True)
+        for _ in range(2):
+            assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n)
+        phases_single = ctx.phase_ms()
+        ctx.set_profiling(False)
 
     # ---- secondary: G1 MSM pts/s at n points per GPU (commitments as points, z as scalars)
     msm_rate = None
@@ -298,6 +304,7 @@ def main():
             "msm_n_per_gpu": n,
             "single_batch_latency_ms": lat,
             "phase_ms_avg_in_timed_region": phases,
+            "phase_ms_single_batch": phases_single,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu and "value" in cpu else None,
         },
     }

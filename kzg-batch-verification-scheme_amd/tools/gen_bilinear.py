@@ -486,6 +486,237 @@ def selfcheck(cv, tables):
     assert run("CONJ", A) == A[:6] + [(-x) % p for x in A[6:]], "CONJ"
 
 
+
+# ----------------------------------------------------------------------------- pairing bytecode
+# Register file (in Fp units, LDS): [K consts 36][E lines NL*12][P 6][SCAL 4][G0..G15 x 12]
+K_ROUND, K_ROUND2, K_COPY, K_INV = 0, 1, 2, 3
+OPNUM = {name: i for i, (name, _) in enumerate(OPS)}
+NONE = 0xFFFF
+LOOP = {"bls12_381": 0xD201000000010000, "bn254": 6 * 4965661367192848881 + 2}
+XABS = 0xD201000000010000
+BN_U = 4965661367192848881
+
+
+def num_lines(cv):
+    lp = LOOP[cv]
+    n = 0
+    for i in range(lp.bit_length() - 2, -1, -1):
+        n += 1 + ((lp >> i) & 1)
+    return n if cv == "bls12_381" else n + 2
+
+
+class Prog:
+    def __init__(self, cv):
+        self.cv = cv
+        self.nl = num_lines(cv)
+        self.R_K = 0
+        self.R_E = 36
+        self.R_P = self.R_E + 12 * self.nl
+        self.R_SCAL = self.R_P + 6
+        self.R_G = self.R_SCAL + 4
+        self.NG = 16
+        self.NR = self.R_G + 12 * self.NG
+        self.code = []
+
+    def g(self, i):
+        assert 0 <= i < self.NG
+        return self.R_G + 12 * i
+
+    def e(self, idx):  # E[idx][0] (12 contiguous: pair 0 then pair 1)
+        return self.R_E + 12 * idx
+
+    def op(self, name, a, b, out):
+        self._check_alias(name, a, b, out)
+        self.code.append([K_ROUND, OPNUM[name], a, NONE if b is None else b, out, 0, 0, 0, 0, 0])
+
+    def op2(self, n1, a1, b1, o1, n2, a2, b2, o2):
+        self._check_alias(n1, a1, b1, o1)
+        self._check_alias(n2, a2, b2, o2)
+        assert o1 not in (a2, b2) and o2 not in (a1, b1)
+        self.code.append([K_ROUND2, OPNUM[n1], a1, NONE if b1 is None else b1, o1,
+                          OPNUM[n2], a2, NONE if b2 is None else b2, o2, 0])
+
+    def copy(self, dst, src):
+        self.code.append([K_COPY, 0, src, NONE, dst, 0, 0, 0, 0, 0])
+
+    def inv(self, dst, src):
+        self.code.append([K_INV, 0, src, NONE, dst, 0, 0, 0, 0, 0])
+
+    @staticmethod
+    def _check_alias(name, a, b, out):
+        assert out != a and out != b, "%s: output aliases an input" % name
+
+
+def build_program(cv):
+    P = Prog(cv)
+    f, t, g = P.g(0), P.g(1), P.g(2)
+    lp = LOOP[cv]
+    idx = 0
+    first = True
+    for i in range(lp.bit_length() - 2, -1, -1):
+        if first:
+            P.op("LL", P.e(idx), P.e(idx) + 6, f)
+            first = False
+        else:
+            P.op2("SQR", f, None, t, "LL", P.e(idx), P.e(idx) + 6, g)
+            P.op("MUL", t, g, f)
+        idx += 1
+        if (lp >> i) & 1:
+            P.op("LL", P.e(idx), P.e(idx) + 6, g)
+            P.op("MUL", f, g, t)
+            P.copy(f, t)
+            idx += 1
+    if cv == "bls12_381":
+        P.op("CONJ", f, None, t)
+        P.copy(f, t)
+    else:
+        for _ in range(2):
+            P.op("LL", P.e(idx), P.e(idx) + 6, g)
+            P.op("MUL", f, g, t)
+            P.copy(f, t)
+            idx += 1
+    assert idx == P.nl
+    # ---- easy part
+    r3, r4, r5, r6, r7 = P.g(3), P.g(4), P.g(5), P.g(6), P.g(7)
+    sc = P.R_SCAL
+    P.op("INV_NORM", f, None, r3)
+    P.op("INV6_T", r3, None, r4)
+    P.op("INV6_D", r3, r4, r5)
+    P.op("INV2_N", r5, None, sc)
+    P.inv(sc + 1, sc)
+    P.op("INV2_FIN", r5, sc + 1, r6)
+    P.op("INV6_FIN", r4, r6, r3)
+    P.op("INV12_FIN", f, r3, r4)
+    P.op("CONJ", f, None, r5)
+    P.op("MUL", r5, r4, g)
+    P.op("FROB2", g, None, r5)
+    P.op("MUL", r5, g, r6)           # r6 = gg (cyclotomic)
+    gg = r6
+
+    def cyclo_pow(dst, a, tmp, e):
+        # ping-pong between dst and tmp; a copy only if the result ends in tmp
+        cur, oth = None, None
+        for i in range(e.bit_length() - 2, -1, -1):
+            src = a if cur is None else cur
+            nxt = tmp if cur != tmp else dst
+            P.op("CYC", src, None, nxt)
+            cur = nxt
+            if (e >> i) & 1:
+                nxt = dst if cur == tmp else tmp
+                P.op("MUL", cur, a, nxt)
+                cur = nxt
+        if cur != dst:
+            P.copy(dst, cur)
+
+    def conj(dst, src):
+        P.op("CONJ", src, None, dst)
+
+    res = P.g(15)
+    if cv == "bls12_381":
+        X = XABS
+        cyclo_pow(r3, gg, t, X); conj(r4, r3); conj(r5, gg); P.op("MUL", r4, r5, r3)      # a = g^(x-1)
+        cyclo_pow(r4, r3, t, X); conj(r5, r4); conj(r4, r3); P.op("MUL", r5, r4, r3)      # a = a^(x-1)
+        cyclo_pow(r4, r3, t, X); conj(r5, r4); P.op("FROB1", r3, None, r4); P.op("MUL", r5, r4, f)  # b
+        cyclo_pow(r3, f, t, X); conj(r4, r3); cyclo_pow(r3, r4, t, X); conj(r5, r3)       # b^(x^2)
+        P.op("FROB2", f, None, r3); P.op("MUL", r5, r3, r4); conj(r3, f); P.op("MUL", r4, r3, r5)  # c
+        P.op("CYC", gg, None, r3); P.op("MUL", r3, gg, r4)                                  # g^3
+        P.op("MUL", r5, r4, res)
+    else:
+        U = BN_U
+        fu, fu2, fu3 = P.g(8), P.g(9), P.g(10)
+        cyclo_pow(fu, gg, t, U)
+        cyclo_pow(fu2, fu, t, U)
+        cyclo_pow(fu3, fu2, t, U)
+        sq = lambda d, a: P.op("CYC", a, None, d)  # noqa: E731
+        mul = lambda d, a, b: P.op("MUL", a, b, d)  # noqa: E731
+        x1, x2, x3 = r4, r5, r7
+        k_t2, k_a, k_b, k_c, k_d, k_e = P.g(11), P.g(12), P.g(13), P.g(14), P.g(3), P.g(0)
+        sq(x1, fu2); sq(x2, x1); mul(t, x2, x1); mul(k_t2, t, gg)             # t2 = fu2^6 g
+        sq(x3, x2); sq(g, x3); mul(x2, g, x3); mul(k_a, x2, t)                # fu2^30
+        mul(k_b, g, x1)                                                       # fu2^18
+        sq(x1, fu3); sq(x2, x1); sq(x3, x2); sq(x1, x3); sq(g, x1)             # g = fu3^32, x2 = fu3^4
+        mul(k_c, g, x2)                                                       # fu3^36
+        sq(x1, fu); sq(x2, x1); sq(x3, x2); mul(k_d, x3, x2)                  # fu^12
+        sq(g, x3); mul(k_e, g, x1)                                            # fu^18
+        mul(x1, k_c, k_b); mul(x2, x1, k_d); conj(x1, x2); mul(x3, x1, gg)     # t1
+        mul(x1, k_c, k_a); mul(x2, x1, k_e); sq(g, gg); mul(t, x2, g); conj(x1, t)  # t0
+        P.op("FROB1", x3, None, x2); mul(t, x1, x2)
+        P.op("FROB2", k_t2, None, x2); mul(x1, t, x2)
+        P.op("FROB3", gg, None, x2); mul(res, x1, x2)
+    return P, res
+
+
+def check_program(cv, tables, P, res):
+    """Run the bytecode numerically on random line values and compare with a direct
+    evaluation (Miller product over the same lines, naive final exponentiation)."""
+    p = globals()["P"][cv]
+    rnd = random.Random(7)
+    K = consts(cv)
+    R = [0] * P.NR
+    R[P.R_K:P.R_K + 36] = K
+    nl = P.nl
+    for i in range(nl * 12):
+        R[P.R_E + i] = rnd.randrange(p)
+    names = [n for n, _ in OPS]
+    for ins in P.code:
+        kind = ins[0]
+        if kind in (K_ROUND, K_ROUND2):
+            insts = [ins[1:5]] + ([ins[5:9]] if kind == K_ROUND2 else [])
+            outs = []
+            for opn, a, b, o in insts:
+                pr, ou = tables[names[opn]]
+                A = R[a:a + 12]
+                B = R[b:b + 12] if b != NONE else [0] * 12
+                outs.append((o, evaluate(pr, ou, A, B, K, p)))
+            for o, vals in outs:
+                R[o:o + len(vals)] = vals
+        elif kind == K_COPY:
+            R[ins[4]:ins[4] + 12] = R[ins[2]:ins[2] + 12]
+        elif kind == K_INV:
+            R[ins[4]] = pow(R[ins[2]], -1, p)
+    got = R[res:res + 12]
+
+    def line_full(x):
+        z = (0, 0)
+        a, b, c = (x[0], x[1]), (x[2], x[3]), (x[4], x[5])
+        return from_w([a, z, b, c, z, z] if cv == "bls12_381" else [a, b, z, c, z, z])
+    one = [1] + [0] * 11
+    f = one
+    lp = LOOP[cv]
+    idx = 0
+    first = True
+    for i in range(lp.bit_length() - 2, -1, -1):
+        l = from_w(wmul(to_w(line_full(R[P.R_E + 12 * idx:P.R_E + 12 * idx + 6])),
+                        to_w(line_full(R[P.R_E + 12 * idx + 6:P.R_E + 12 * idx + 12])), cv))
+        f = l if first else from_w(wmul(to_w(from_w(wmul(to_w(f), to_w(f), cv))), to_w(l), cv))
+        first = False
+        idx += 1
+        if (lp >> i) & 1:
+            l = from_w(wmul(to_w(line_full(R[P.R_E + 12 * idx:P.R_E + 12 * idx + 6])),
+                            to_w(line_full(R[P.R_E + 12 * idx + 6:P.R_E + 12 * idx + 12])), cv))
+            f = from_w(wmul(to_w(f), to_w(l), cv))
+            idx += 1
+    if cv == "bls12_381":
+        f = f[:6] + [(-x) % p for x in f[6:]]
+    else:
+        for _ in range(2):
+            l = from_w(wmul(to_w(line_full(R[P.R_E + 12 * idx:P.R_E + 12 * idx + 6])),
+                            to_w(line_full(R[P.R_E + 12 * idx + 6:P.R_E + 12 * idx + 12])), cv))
+            f = from_w(wmul(to_w(f), to_w(l), cv))
+            idx += 1
+    r_ord = {"bls12_381": 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001,
+             "bn254": 21888242871839275222246405745257275088548364400416034343698204186575808495617}[cv]
+    e = (p ** 12 - 1) // r_ord * (3 if cv == "bls12_381" else 1)
+    acc = one
+    w = to_w(f)
+    a = to_w(acc)
+    for bit in bin(e)[2:]:
+        a = wmul(a, a, cv)
+        if bit == "1":
+            a = wmul(a, w, cv)
+    want = from_w(a)
+    assert got == want, "bytecode program mismatch for %s" % cv
+
 # ----------------------------------------------------------------------------- emit
 def emit():
     lines = ["// GENERATED by tools/gen_bilinear.py -- do not edit.",
@@ -530,7 +761,15 @@ def emit():
             lines.append("// %s: %d products, %d outputs" % (name, np_, no))
             lines.append("static __constant__ uint16_t %s%s_P[%d] = {%s};" % (pfx, name, max(1, len(pidx)), ", ".join(map(str, pidx or [0]))))
             lines.append("static __constant__ uint16_t %s%s_O[%d] = {%s};" % (pfx, name, len(oidx), ", ".join(map(str, oidx))))
+        prog, res = build_program(cv)
+        check_program(cv, tables, prog, res)
+        flat = [v for ins in prog.code for v in ins]
+        lines.append("static __constant__ uint16_t %sPROG[%d] = {%s};" % (pfx, len(flat), ", ".join(map(str, flat))))
         lines.append("struct %sOpsInfo {" % tag)
+        lines.append("  static constexpr int NTERMS = %d;" % len(terms))
+        lines.append("  static constexpr int NPROG = %d, R_K = %d, R_E = %d, R_P = %d, R_SCAL = %d, R_G = %d, NR = %d, R_RES = %d;" % (
+            len(prog.code), prog.R_K, prog.R_E, prog.R_P, prog.R_SCAL, prog.R_G, prog.NR, res))
+        stats[(cv, "PROGRAM")] = (len(prog.code), sum(1 for i in prog.code if i[0] in (0, 1)), 0)
         for name, np_, no, pidx, oidx in desc:
             lines.append("  static constexpr int %s_NP = %d, %s_NO = %d;" % (name, np_, name, no))
         lines.append("};")
