@@ -105,7 +105,7 @@ KZ_DEV Fp<P> fp_select(bool c, const Fp<P>& a, const Fp<P>& b) {
 //   for j>0: (A, t[j]) = t[j] + a[j]*b[i] + A;  (C, t[j-1]) = t[j] + m*p[j] + C
 //   t[N-1] = C + A
 template <class P>
-KZ_DEV Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
+KZ_DEV Fp<P> fp_mul_cios(const Fp<P>& a, const Fp<P>& b) {
   constexpr int N = P::N;
   uint32_t t[N];
   _Pragma("unroll") for (int i = 0; i < N; ++i) t[i] = 0;
@@ -132,6 +132,72 @@ KZ_DEV Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
   _Pragma("unroll") for (int i = 0; i < N; ++i) d.v[i] = __builtin_subc(t[i], P::MOD[i], bw, &bw);
   _Pragma("unroll") for (int i = 0; i < N; ++i) r.v[i] = bw ? t[i] : d.v[i];
   return r;
+}
+
+// ---------------------------------------------------------------------------- mul (product scanning)
+// Same result as fp_mul (CIOS), different schedule: column-wise (FIPS) Montgomery with a
+// 96-bit column accumulator {acc64, top}.  Each limb product is ONE v_mad_u64_u32 that
+// accumulates into the 64-bit pair and writes its carry-out to an SGPR pair, plus ONE
+// v_addc_co_u32 folding that carry into `top`.  hipcc's lowering of the CIOS form needs a
+// zero-extended 64-bit addend per product (~3 extra v_mov/v_lshl_add per product: measured
+// 803 v_mov_b32 per BLS12-381 product in the probe kernel's ISA); this form needs none.
+KZ_DEV void mac32(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b) {
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"
+      "v_addc_co_u32_e64 %2, %1, %2, 0, %1"
+      : "+v"(acc), "=&s"(cc), "+v"(top)
+      : "v"(a), "v"(b));
+}
+KZ_DEV void mac32s(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b_uniform) {
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"
+      "v_addc_co_u32_e64 %2, %1, %2, 0, %1"
+      : "+v"(acc), "=&s"(cc), "+v"(top)
+      : "v"(a), "s"(b_uniform));
+}
+
+template <class P>
+KZ_DEV Fp<P> fp_mul_ps(const Fp<P>& a, const Fp<P>& b) {
+  constexpr int N = P::N;
+  uint32_t m[N], t[N];
+  uint64_t acc = 0;
+  uint32_t top = 0;
+  _Pragma("unroll") for (int k = 0; k < N; ++k) {
+    _Pragma("unroll") for (int i = 0; i < k; ++i) {
+      mac32(acc, top, a.v[i], b.v[k - i]);
+      mac32s(acc, top, m[i], P::MOD[k - i]);
+    }
+    mac32(acc, top, a.v[k], b.v[0]);
+    m[k] = (uint32_t)acc * P::INV;
+    mac32s(acc, top, m[k], P::MOD[0]);  // low word becomes 0
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+    top = 0;
+  }
+  _Pragma("unroll") for (int k = N; k < 2 * N - 1; ++k) {
+    _Pragma("unroll") for (int i = k - N + 1; i < N; ++i) {
+      mac32(acc, top, a.v[i], b.v[k - i]);
+      mac32s(acc, top, m[i], P::MOD[k - i]);
+    }
+    t[k - N] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+    top = 0;
+  }
+  t[N - 1] = (uint32_t)acc;  // (ab + mp)/R < 2p < 2^(32N): no further words
+  Fp<P> r, d;
+  uint32_t bw = 0;
+  _Pragma("unroll") for (int i = 0; i < N; ++i) d.v[i] = __builtin_subc(t[i], P::MOD[i], bw, &bw);
+  _Pragma("unroll") for (int i = 0; i < N; ++i) r.v[i] = bw ? t[i] : d.v[i];
+  return r;
+}
+
+// Default multiplication used by every kernel.
+template <class P>
+KZ_DEV Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
+#ifdef KZ_MUL_CIOS
+  return fp_mul_cios(a, b);
+#else
+  return fp_mul_ps(a, b);
+#endif
 }
 
 template <class P>
