@@ -34,6 +34,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import kzgmi  # noqa: E402
+from kzgmi.distributed import sharded_batch_verify, sharded_msm  # noqa: E402
 
 METRIC = "batch-verifies/sec + G1 MSM pts/sec at n=2^20, BLS12-381; 1/2/4/8 GPU"
 HBM_PEAK = 8.0e12          # B/s, MI355X spec (MI355X_MICROARCH.md)
@@ -135,16 +136,10 @@ def main():
     Cm, z, y, P = gen_inputs(ctx, curve, n, gseed)
     torch.cuda.synchronize()
     log("[rank %d] generated %d tuples in %.2f s" % (rank, n, time.perf_counter() - t0))
-    pb = ctx.partial_bytes(curve)
-    parts_local = torch.empty(2 * pb, dtype=torch.uint8, device="cuda")
-    parts_all = torch.empty(world * 2 * pb, dtype=torch.uint8, device="cuda")
-
     def step_sharded():
-        ctx.batch_partial(srs, Cm, z, y, P, n, rank * n, vseed, parts_local)
-        dist.all_gather_into_tensor(parts_all, parts_local)
-        if rank == 0:
-            ok = ctx.batch_combine(srs, parts_all, world)
-            assert ok, "batch rejected"
+        # every rank holds n tuples of a global batch of world*n; one RCCL all-gather
+        ok = sharded_batch_verify(ctx, srs, Cm, z, y, P, n, rank * n, vseed)
+        assert ok, "batch rejected"
 
     pending = [False] * slots
 
@@ -213,15 +208,9 @@ def main():
     # ---- secondary: G1 MSM pts/s at n points per GPU (commitments as points, z as scalars)
     msm_rate = None
     if args.msm_steps > 0:
-        mparts_local = torch.empty(pb, dtype=torch.uint8, device="cuda")
-        mparts_all = torch.empty(world * pb, dtype=torch.uint8, device="cuda")
-
         def msm_step():
             if world > 1:
-                ctx.msm_partial(curve, Cm, z, n, mparts_local)
-                dist.all_gather_into_tensor(mparts_all, mparts_local)
-                if rank == 0:
-                    ctx.msm_combine(curve, mparts_all, world)
+                sharded_msm(ctx, curve, Cm, z, n)
             else:
                 ctx.msm_g1(curve, Cm, z, n=n)
         msm_step()

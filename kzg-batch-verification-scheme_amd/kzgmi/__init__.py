@@ -229,6 +229,10 @@ class Context:
         return out.raw
 
     # ------------------------------------------------------------------ multi-GPU pieces
+    def tensor_device(self):
+        import torch
+        return torch.device("cuda", self.device)
+
     def partial_bytes(self, curve: str) -> int:
         return int(lib().kzgmi_partial_bytes(CURVES[curve]))
 

@@ -250,8 +250,23 @@ int kzgo_batch_verify(int curve, const uint8_t* cm, const uint8_t* zs, const uin
                       size_t n, const uint8_t* g2, const uint8_t* tau_g2, const uint8_t* seed, int* ok,
                       uint8_t* a_out, uint8_t* b_out) {
   if (!ok || !seed || !g2 || !tau_g2 || (n && (!cm || !zs || !ys || !pf))) return KZGO_ERR_ARG;
-  return CURVE_DISPATCH(curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out),
-                        bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out));
+  return CURVE_DISPATCH(curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, 1),
+                        bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, 1));
+}
+
+/* A, B of tuples [offset, offset+n) of a global batch (no pairing): the shard partials */
+int kzgo_batch_combination(int curve, const uint8_t* cm, const uint8_t* zs, const uint8_t* ys, const uint8_t* pf,
+                           size_t n, uint64_t offset, const uint8_t* g2, const uint8_t* tau_g2, const uint8_t* seed,
+                           uint8_t* a_out, uint8_t* b_out) {
+  int ok = -1;
+  if (!seed || !g2 || !tau_g2 || !a_out || !b_out || (n && (!cm || !zs || !ys || !pf))) return KZGO_ERR_ARG;
+  return CURVE_DISPATCH(curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, &ok, a_out, b_out, offset, 0),
+                        bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, &ok, a_out, b_out, offset, 0));
+}
+
+int kzgo_pairing_check(int curve, const uint8_t* a, const uint8_t* b, const uint8_t* g2, const uint8_t* tau_g2, int* ok) {
+  if (!a || !b || !g2 || !tau_g2 || !ok) return KZGO_ERR_ARG;
+  return CURVE_DISPATCH(curve, bls_pairing_check_api(a, b, g2, tau_g2, ok), bn_pairing_check_api(a, b, g2, tau_g2, ok));
 }
 
 #define DEF_MSM(C)                                                                         \

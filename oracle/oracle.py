@@ -32,6 +32,9 @@ def lib():
         L.kzgo_batch_verify.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p,
                                         c.c_size_t, c.c_char_p, c.c_char_p, c.c_char_p,
                                         c.POINTER(c.c_int), c.c_char_p, c.c_char_p]
+        L.kzgo_batch_combination.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p, c.c_size_t,
+                                             c.c_uint64, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p]
+        L.kzgo_pairing_check.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p, c.POINTER(c.c_int)]
         L.kzgo_msm_g1.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_size_t, c.c_char_p]
         L.kzgo_g1_mul_gen.argtypes = [c.c_int, c.c_char_p, c.c_size_t, c.c_char_p]
         L.kzgo_pairing.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p]
@@ -73,6 +76,22 @@ def batch_verify(curve, commitments: bytes, zs: bytes, ys: bytes, proofs: bytes,
                                    seed, ctypes.byref(ok), a, b))
     if want_ab:
         return bool(ok.value), a.raw, b.raw
+    return bool(ok.value)
+
+
+def batch_combination(curve, commitments, zs, ys, proofs, n, offset, g2, tau_g2, seed):
+    """(A, B) encodings for tuples [offset, offset + n) of a global batch (shard partials)."""
+    g1b = 2 * FP_BYTES[curve]
+    a = ctypes.create_string_buffer(g1b)
+    b = ctypes.create_string_buffer(g1b)
+    _check(lib().kzgo_batch_combination(CURVE_IDS[curve], commitments, zs, ys, proofs, n, offset, g2, tau_g2,
+                                        seed, a, b))
+    return a.raw, b.raw
+
+
+def pairing_check(curve, A: bytes, B: bytes, g2: bytes, tau_g2: bytes) -> bool:
+    ok = ctypes.c_int(-1)
+    _check(lib().kzgo_pairing_check(CURVE_IDS[curve], A, B, g2, tau_g2, ctypes.byref(ok)))
     return bool(ok.value)
 
 

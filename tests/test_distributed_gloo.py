@@ -1,0 +1,113 @@
+"""World-size-2 gloo test of the multi-GPU orchestration (kzgmi.distributed) on CPU.
+
+The GPU backend (kzgmi.Context) is replaced by a test double that computes each shard's
+partial (A_k, B_k) with the C oracle (with the shard's GLOBAL index offset, as the HIP path
+does) and combines gathered partials with the Python spec + the oracle pairing check.  This
+exercises the product's sharding, offsets, all-gather layout and combine semantics; the real
+GPU partials are checked against the same decomposition in tests/test_gpu_parity.py.
+"""
+import os
+import socket
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class OracleBackend:
+    """Stand-in for kzgmi.Context with the three methods kzgmi.distributed uses."""
+
+    def __init__(self, curve, g2, tau_g2):
+        from oracle.pyspec import curves as pc
+        self.curve = curve
+        self.C = pc.CURVES[curve]
+        self.g2, self.tau_g2 = g2, tau_g2
+
+    def tensor_device(self):
+        return "cpu"
+
+    def partial_bytes(self, curve):
+        return 2 * self.C.fp_bytes  # one G1 encoding per record
+
+    def batch_partial(self, srs, commitments, zs, ys, proofs, n, offset, seed, out):
+        import torch
+        from oracle import oracle as O
+        A, B = O.batch_combination(self.curve, bytes(commitments), bytes(zs), bytes(ys), bytes(proofs), n,
+                                   offset, self.g2, self.tau_g2, seed)
+        out.copy_(torch.frombuffer(bytearray(A + B), dtype=torch.uint8))
+
+    def batch_combine(self, srs, gathered, n_parts):
+        from oracle import oracle as O
+        from oracle.pyspec import curves as pc
+        from oracle.pyspec import kzg as pk
+        raw = gathered.numpy().tobytes()
+        g1b = 2 * self.C.fp_bytes
+        A = B = None
+        for k in range(n_parts):
+            rec = raw[k * 2 * g1b:(k + 1) * 2 * g1b]
+            A = pc.g1_add(A, pk.g1_from_bytes(rec[:g1b], self.C), self.C)
+            B = pc.g1_add(B, pk.g1_from_bytes(rec[g1b:], self.C), self.C)
+        return O.pairing_check(self.curve, pk.g1_to_bytes(A, self.C), pk.g1_to_bytes(B, self.C),
+                               self.g2, self.tau_g2)
+
+
+class FakeSrs:
+    def __init__(self, curve):
+        self.curve = curve
+
+
+def _worker(rank, world, port, curve, n_total, corrupt_index, result_q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "kzg-batch-verification-scheme_amd"))
+    import json
+    import torch.distributed as dist
+    from kzgmi.distributed import shard_range, sharded_batch_verify
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    with open(os.path.join(ROOT, "tests", "golden", "%s_batch_n%d.json" % (curve, n_total))) as f:
+        g = json.load(f)
+    h = bytes.fromhex
+    C, z, y, P = (h(g[k]) for k in ("commitments", "zs", "ys", "proofs"))
+    if corrupt_index is not None:
+        yb = bytearray(y)
+        yb[32 * corrupt_index + 31] ^= 1
+        y = bytes(yb)
+    off, cnt = shard_range(n_total, world, rank)
+    g1b = len(C) // n_total
+    be = OracleBackend(curve, h(g["g2"]), h(g["tau_g2"]))
+    ok = sharded_batch_verify(be, FakeSrs(curve), C[off * g1b:(off + cnt) * g1b], z[off * 32:(off + cnt) * 32],
+                              y[off * 32:(off + cnt) * 32], P[off * g1b:(off + cnt) * g1b], cnt, off, h(g["seed"]))
+    result_q.put((rank, ok))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("curve,n,corrupt,expect", [
+    ("bls12_381", 16, None, True),
+    ("bls12_381", 16, 13, False),   # bad tuple in rank 1's shard
+    ("bn254", 64, None, True),
+    ("bn254", 64, 2, False),        # bad tuple in rank 0's shard
+])
+def test_sharded_verify_world2(curve, n, corrupt, expect):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, curve, n, corrupt, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    res = sorted(q.get() for _ in range(2))
+    assert [ok for _, ok in res] == [expect, expect]
