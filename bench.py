@@ -12,7 +12,8 @@ Single GPU: steps are issued round-robin over `--slots` independent workspaces/s
 the latency-bound tail of one batch (bucket reduction, window combination, pairing) runs
 beside the bucket accumulation of the next.  Every verdict is checked (must be True).
 N GPUs: each rank computes its partial (A_k, B_k) over its shard, partials are all-gathered
-over RCCL (torch.distributed 'nccl' backend) and rank 0 runs the pairing check.
+over RCCL (torch.distributed 'nccl' backend) and every rank runs the pairing check; each rank
+keeps `--slots` global batches in flight (kzgmi.distributed.ShardedPipeline).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with `roofline` for the
 dominant kernel (bucket accumulation) and `cpu_baseline` (the C oracle, timed on a bounded
@@ -30,11 +31,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "kzg-batch-verification-scheme_amd"))
 
+# HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default).  The slot
+# pipeline needs about one queue per batch in flight -- batches whose streams share a queue
+# serialise (measured: 12 slots on 4 queues 77/s, on 12-16 queues 106/s).  Read by the HIP
+# runtime when it initialises, so set before torch touches the GPU.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("KZGMI_HW_QUEUES", "16")
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import kzgmi  # noqa: E402
-from kzgmi.distributed import sharded_batch_verify, sharded_msm  # noqa: E402
+from kzgmi.distributed import ShardedPipeline, sharded_msm  # noqa: E402
 
 METRIC = "batch-verifies/sec + G1 MSM pts/sec at n=2^20, BLS12-381; 1/2/4/8 GPU"
 HBM_PEAK = 8.0e12          # B/s, MI355X spec (MI355X_MICROARCH.md)
@@ -109,10 +116,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=1 << 20, help="tuples per GPU")
     ap.add_argument("--curve", default="bls12_381", choices=["bls12_381", "bn254"])
-    ap.add_argument("--slots", type=int, default=3, help="pipeline depth (single GPU)")
+    ap.add_argument("--slots", type=int, default=0,
+                    help="batches in flight (default 12 single-GPU; sharded 6 + 2 combine lanes)")
     ap.add_argument("--msm-steps", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the multi-GPU pipeline (RCCL all-gather per batch) even at world size 1")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -121,11 +131,19 @@ def main():
     if world != args.gpus:
         log("warning: WORLD_SIZE=%d but --gpus=%d; using WORLD_SIZE" % (world, args.gpus))
     torch.cuda.set_device(local)
-    if world > 1:
+    sharded = world > 1 or args.sharded
+    if sharded:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     curve, n = args.curve, args.n
-    slots = args.slots if world == 1 else 1
-    ctx = kzgmi.Context(local, slots)
+    # measured (profiles/r01/slots_sweep.txt): single 12 slots 105.6/s; sharded 6+2 lanes
+    # 103.6/s, 10+2 101.8/s, 12+2 70.5/s (more streams than hardware queues)
+    slots = args.slots if args.slots else (6 if sharded else 12)
+    lanes = 2 if sharded else 0
+    ctx = kzgmi.Context(local, slots + lanes)  # + the combine lanes
     g2 = kzgmi.G2_GENERATOR[curve]
     tg2 = ctx.g2_mul(curve, g2, TAU)
     cpu_baseline.tg2 = tg2
@@ -136,10 +154,13 @@ def main():
     Cm, z, y, P = gen_inputs(ctx, curve, n, gseed)
     torch.cuda.synchronize()
     log("[rank %d] generated %d tuples in %.2f s" % (rank, n, time.perf_counter() - t0))
+    pipe = ShardedPipeline(ctx, srs, slots, lanes) if sharded else None
+
     def step_sharded():
-        # every rank holds n tuples of a global batch of world*n; one RCCL all-gather
-        ok = sharded_batch_verify(ctx, srs, Cm, z, y, P, n, rank * n, vseed)
-        assert ok, "batch rejected"
+        # every rank holds n tuples of a global batch of world*n; one RCCL all-gather per batch,
+        # `slots` global batches in flight
+        for ok in pipe.submit(Cm, z, y, P, n, rank * n, vseed):
+            assert ok, "batch rejected"
 
     pending = [False] * slots
 
@@ -151,6 +172,10 @@ def main():
         pending[s] = True
 
     def drain():
+        if pipe is not None:
+            for ok in pipe.drain():
+                assert ok, "batch rejected"
+            return
         for s in range(slots):
             if pending[s]:
                 assert ctx.wait(s), "batch rejected"
@@ -163,7 +188,7 @@ def main():
 
     # ---- warmup
     for k in range(args.warmup):
-        if world > 1:
+        if sharded:
             step_sharded()
         else:
             step_single(k)
@@ -173,7 +198,7 @@ def main():
     ctx.set_profiling(True)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        if world > 1:
+        if sharded:
             step_sharded()
         else:
             step_single(k)
@@ -254,6 +279,14 @@ def main():
             "achieved_fpmul_per_s": acc_fpmuls / (acc_ms * 1e-3) if acc_ms > 0 else None,
             "peak_fpmul_per_s": fpmul_peak,
             "frac": (acc_fpmuls / (acc_ms * 1e-3)) / fpmul_peak if acc_ms > 0 else None,
+            # whole pipeline: accumulation products per second of wall time (batches/s x
+            # products per batch) against the probe peak -- what the overlap actually sustains
+            "pipeline_frac": acc_fpmuls * value / world / fpmul_peak,
+            # the same kernel timed alone (non-pipelined batch): its own efficiency, without
+            # the time-sharing with other slots' kernels that stretches the in-region figure
+            "single_batch_kernel_ms": (phases_single or {}).get("accumulate"),
+            "single_batch_frac": (acc_fpmuls / (phases_single["accumulate"] * 1e-3)) / fpmul_peak
+            if phases_single and phases_single.get("accumulate") else None,
         },
     }
     cpu = None
@@ -283,7 +316,7 @@ def main():
             "tuples_per_gpu": n,
             "global_batch": world * n,
             "pipeline_slots": slots,
-            "parallelism": "point-range shards" + (", RCCL all_gather of partial sums" if world > 1 else ""),
+            "parallelism": "point-range shards" + (", RCCL all_gather of partial sums" if sharded else ""),
         },
         "roofline": roofline,
         "cpu_baseline": cpu,
@@ -298,7 +331,7 @@ def main():
         },
     }
     print(json.dumps(out), flush=True)
-    if world > 1:
+    if sharded:
         dist.barrier()
         dist.destroy_process_group()
 

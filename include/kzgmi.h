@@ -106,6 +106,15 @@ int kzgmi_batch_partial_device(kzgmi_ctx* ctx, const kzgmi_srs* srs, const void*
                                uint64_t index_offset, const uint8_t* seed32, void* d_partial_out);
 int kzgmi_batch_combine_device(kzgmi_ctx* ctx, const kzgmi_srs* srs, const void* d_partials,
                                int n_parts, int* ok_out);
+/* Pipelined forms of the two calls above on workspace `slot`; kzgmi_slot_wait() completes
+ * them (ok_out = 1 for a partial job, the verdict for a combine job).  A rank keeps several
+ * shards in flight exactly like kzgmi_batch_verify_device_async. */
+int kzgmi_batch_partial_device_async(kzgmi_ctx* ctx, const kzgmi_srs* srs, int slot,
+                                     const void* d_commitments, const void* d_zs, const void* d_ys,
+                                     const void* d_proofs, size_t n, uint64_t index_offset,
+                                     const uint8_t* seed32, void* d_partial_out);
+int kzgmi_batch_combine_device_async(kzgmi_ctx* ctx, const kzgmi_srs* srs, int slot,
+                                     const void* d_partials, int n_parts);
 int kzgmi_msm_partial_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_points,
                              const void* d_scalars, size_t n, void* d_partial_out);
 int kzgmi_msm_combine_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_partials,

@@ -64,12 +64,13 @@ enum Phase { PH_CONVERT = 0, PH_SCALARS, PH_SORT, PH_ACCUM, PH_REDUCE, PH_COMBIN
 
 struct Slot {
   hipStream_t stream = nullptr;
-  DevBuf pts, inf, scal_r, scal_s, scal_t, tpart, cnt, off, cursor, blk, total, sval, skey;
+  DevBuf pts, inf, scal_r, scal_s, scal_t, tpart, cnt, off, coarse, ent, total, sval, skey;
   DevBuf buckets, pfirst, plast, R, U, scratch, winsum, res, flags, stage, outb;
   int* host_flags = nullptr;  // pinned: [ok, err]
   hipEvent_t ev[kNumPhases + 1] = {};
   bool ev_used[kNumPhases + 1] = {};
   bool pending = false;
+  bool partial_job = false;  // pending job produces a partial record, not a verdict
   int curve = 0;
 };
 
@@ -157,8 +158,8 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl, uint32_t nsets, size
   const size_t nchunks = (emax + ACC_CHUNK - 1) / ACC_CHUNK + 1;
   CHK(s.cnt.ensure((size_t)NB * 4));
   CHK(s.off.ensure((size_t)NB * 4));
-  CHK(s.cursor.ensure((size_t)NB * 4));
-  CHK(s.blk.ensure(1024 * 4));
+  CHK(s.coarse.ensure((size_t)3 * nsets * BINS_PER_SET * 4));
+  CHK(s.ent.ensure(emax * 8));
   CHK(s.total.ensure(16));
   CHK(s.sval.ensure(emax * 4));
   CHK(s.skey.ensure(emax * 4));
@@ -172,12 +173,9 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl, uint32_t nsets, size
   CHK(s.res.ensure(2 * sizeof(XY)));
   hipStream_t st = s.stream;
   using L = Launch<Cv>;
-  HIPCHK(hipMemsetAsync(s.cnt.p, 0, (size_t)NB * 4, st));
-  L::digits(st, false, tl, s.inf.template as<uint8_t>(), s.cnt.template as<uint32_t>(), nullptr, nullptr);
-  L::scan(st, s.cnt.template as<uint32_t>(), NB, s.off.template as<uint32_t>(), s.blk.template as<uint32_t>(),
-          s.total.template as<uint32_t>(), s.cursor.template as<uint32_t>());
-  L::digits(st, true, tl, s.inf.template as<uint8_t>(), s.cursor.template as<uint32_t>(), s.sval.template as<uint32_t>(),
-            s.skey.template as<uint32_t>());
+  L::sort(st, tl, nsets, s.inf.template as<uint8_t>(), s.coarse.template as<uint32_t>(), s.ent.template as<uint64_t>(),
+          s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.total.template as<uint32_t>(),
+          s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>());
   mark(c, s, PH_SORT + 1);
   L::accumulate(st, nchunks, s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
                 s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.pts.template as<Affine<Cv>>(),
@@ -240,6 +238,7 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
   s.pending = true;
+  s.partial_job = d_partial_out != nullptr;
   s.curve = Cv::ID;
   return 0;
 }
@@ -250,7 +249,7 @@ int finish_slot(kzgmi_ctx* c, Slot& s, int* ok_out) {
   collect_phases(c, s);
   int e = map_device_err((uint32_t)s.host_flags[1]);
   if (e) return e;
-  if (ok_out) *ok_out = s.host_flags[0];
+  if (ok_out) *ok_out = s.partial_job ? 1 : s.host_flags[0];
   return 0;
 }
 
@@ -317,7 +316,7 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
   (void)hipSetDevice(c->device);
   for (auto& s : c->slots) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
-    DevBuf* bufs[] = {&s.pts, &s.inf, &s.scal_r, &s.scal_s, &s.scal_t, &s.tpart, &s.cnt, &s.off, &s.cursor, &s.blk,
+    DevBuf* bufs[] = {&s.pts, &s.inf, &s.scal_r, &s.scal_s, &s.scal_t, &s.tpart, &s.cnt, &s.off, &s.coarse, &s.ent,
                       &s.total, &s.sval, &s.skey, &s.buckets, &s.pfirst, &s.plast, &s.R, &s.U, &s.scratch,
                       &s.winsum, &s.res, &s.flags, &s.stage, &s.outb};
     for (DevBuf* b : bufs) b->release();
@@ -397,9 +396,12 @@ int kzgmi_batch_verify_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot
   uint8_t sb[32];
   Seed seed = make_seed(seed32, sb);
   if (n == 0) {
+    CHK(set_dev(c));
+    HIPCHK(hipStreamSynchronize(s.stream));  // host_flags may still be the target of a copy
     s.host_flags[0] = 1;
     s.host_flags[1] = 0;
     s.pending = true;
+    s.partial_job = false;
     return 0;
   }
   return dispatch(srs->curve, [&](auto cv) -> int {
@@ -540,49 +542,71 @@ size_t kzgmi_partial_bytes(kzgmi_curve curve) {
   return curve == KZGMI_BLS12_381 ? sizeof(Xyzz<Bls12_381>) : sizeof(Xyzz<Bn254>);
 }
 
-int kzgmi_batch_partial_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* dC, const void* dz, const void* dy,
-                               const void* dpi, size_t n, uint64_t index_offset, const uint8_t* seed32,
-                               void* d_partial_out) {
-  CHK(check_ctx(c));
+int kzgmi_batch_partial_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const void* dC, const void* dz,
+                                     const void* dy, const void* dpi, size_t n, uint64_t index_offset,
+                                     const uint8_t* seed32, void* d_partial_out) {
+  CHK(check_ctx(c, slot));
   if (!srs || srs->ctx != c || !d_partial_out) return fail(KZGMI_ERR_ARG, "bad argument");
   if (!seed32) return fail(KZGMI_ERR_ARG, "sharded verification needs an explicit shared seed");
-  Slot& s = c->slots[0];
+  if (n && (!dC || !dz || !dy || !dpi)) return fail(KZGMI_ERR_ARG, "null input");
+  if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "batch too large (max 2^26 tuples per call)");
+  Slot& s = c->slots[slot];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_slot_wait first");
   uint8_t sb[32];
   Seed seed = make_seed(seed32, sb);
   return dispatch(srs->curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
-    if (n == 0) {
-      Xyzz<Cv> h[2];
-      for (auto& x : h) memset(&x, 0, sizeof(x));  // zz = 0 -> infinity
-      HIPCHK(hipMemcpy(d_partial_out, h, sizeof(h), hipMemcpyHostToDevice));
+    if (n == 0) {  // empty shard: both partials are the point at infinity (zz = 0)
+      HIPCHK(hipMemsetAsync(d_partial_out, 0, 2 * sizeof(Xyzz<Cv>), s.stream));
+      HIPCHK(hipStreamSynchronize(s.stream));
+      s.host_flags[0] = 1;
+      s.host_flags[1] = 0;
+      s.pending = true;
+      s.partial_job = true;
       return 0;
     }
-    CHK(enqueue_batch<Cv>(c, s, srs, dC, dz, dy, dpi, n, seed, index_offset, d_partial_out));
-    return finish_slot(c, s, nullptr);
+    return enqueue_batch<Cv>(c, s, srs, dC, dz, dy, dpi, n, seed, index_offset, d_partial_out);
   });
 }
 
-int kzgmi_batch_combine_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* d_partials, int n_parts, int* ok_out) {
-  CHK(check_ctx(c));
-  if (!srs || !d_partials || n_parts < 1 || !ok_out) return fail(KZGMI_ERR_ARG, "bad argument");
+int kzgmi_batch_partial_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* dC, const void* dz, const void* dy,
+                               const void* dpi, size_t n, uint64_t index_offset, const uint8_t* seed32,
+                               void* d_partial_out) {
+  CHK(kzgmi_batch_partial_device_async(c, srs, 0, dC, dz, dy, dpi, n, index_offset, seed32, d_partial_out));
+  return kzgmi_slot_wait(c, 0, nullptr);
+}
+
+int kzgmi_batch_combine_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const void* d_partials,
+                                     int n_parts) {
+  CHK(check_ctx(c, slot));
+  if (!srs || srs->ctx != c || !d_partials || n_parts < 1) return fail(KZGMI_ERR_ARG, "bad argument");
+  Slot& s = c->slots[slot];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_slot_wait first");
   return dispatch(srs->curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     using XY = Xyzz<Cv>;
-    Slot& s = c->slots[0];
     CHK(s.res.ensure(2 * sizeof(XY)));
     CHK(s.flags.ensure(16));
     hipStream_t st = s.stream;
     HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
     mark(c, s, PH_COMBINE);
     Launch<Cv>::sum_partials(st, (const XY*)d_partials, (uint32_t)n_parts, 2, 2, s.res.template as<XY>());
-    Launch<Cv>::pairing_check(st, s.res.template as<XY>(), srs->lines.template as<Line<Cv>>(), srs->q_inf.template as<uint8_t>(),
-                                          s.flags.template as<int>());
+    Launch<Cv>::pairing_check(st, s.res.template as<XY>(), srs->lines.template as<Line<Cv>>(),
+                              srs->q_inf.template as<uint8_t>(), s.flags.template as<int>());
     mark(c, s, PH_PAIRING + 1);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
     s.pending = true;
-    return finish_slot(c, s, ok_out);
+    s.partial_job = false;
+    s.curve = Cv::ID;
+    return 0;
   });
+}
+
+int kzgmi_batch_combine_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* d_partials, int n_parts, int* ok_out) {
+  if (!ok_out) return fail(KZGMI_ERR_ARG, "null ok_out");
+  CHK(kzgmi_batch_combine_device_async(c, srs, 0, d_partials, n_parts));
+  return kzgmi_slot_wait(c, 0, ok_out);
 }
 
 int kzgmi_msm_partial_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dpts, const void* dsc, size_t n,

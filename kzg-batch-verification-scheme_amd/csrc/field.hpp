@@ -141,6 +141,11 @@ KZ_DEV Fp<P> fp_mul_cios(const Fp<P>& a, const Fp<P>& b) {
 // v_addc_co_u32 folding that carry into `top`.  hipcc's lowering of the CIOS form needs a
 // zero-extended 64-bit addend per product (~3 extra v_mov/v_lshl_add per product: measured
 // 803 v_mov_b32 per BLS12-381 product in the probe kernel's ISA); this form needs none.
+// Each multiply-add is its own asm statement, so hipcc pads every boundary with `s_nop 0`
+// (~1 nop per product).  Fusing 2-4 (a*b, m*p) pairs per statement removes them but measured
+// no gain (tools/probes/macfuse.hip: 63.2 vs 64.1 G 12x12 products/s -- other waves fill the
+// pad) and produced wrong products inside the library kernels (not in the isolated probe), so
+// the verified one-product-per-statement form stays.
 KZ_DEV void mac32(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b) {
   uint64_t cc;
   asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"

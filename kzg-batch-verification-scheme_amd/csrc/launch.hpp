@@ -11,10 +11,9 @@ struct Launch {
   using XY = Xyzz<Cv>;
   using AF = Affine<Cv>;
   // ---- MSM (launch_msm.hip)
-  static void digits(hipStream_t st, bool scatter, const TermList& tl, const uint8_t* inf, uint32_t* cnt_or_cursor,
-                     uint32_t* sval, uint32_t* skey);
-  static void scan(hipStream_t st, const uint32_t* cnt, uint32_t nb, uint32_t* off, uint32_t* blk, uint32_t* total,
-                   uint32_t* cursor);
+  // coarse: 3 * nsets * 256 u32 (counts, offsets, cursors), ent: emax u64
+  static void sort(hipStream_t st, const TermList& tl, uint32_t nsets, const uint8_t* inf, uint32_t* coarse,
+                   uint64_t* ent, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval, uint32_t* skey);
   static void accumulate(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* sval,
                          const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts, XY* buckets,
                          XY* pfirst, XY* plast);

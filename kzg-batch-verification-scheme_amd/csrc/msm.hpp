@@ -1,9 +1,8 @@
 // G1 Pippenger MSM kernels for gfx950 (hot-path rows a5/a6 of SURVEY.md 8a).
 //
 // Pipeline (all on one HIP stream; no host synchronisation inside):
-//   k_digits<COUNT>   signed 16-bit window digits of every term -> per-bucket counts
-//   k_scan_*          exclusive scan of the counts -> bucket offsets (+ total entries)
-//   k_digits<SCATTER> same digits, each entry placed at its bucket's next slot
+//   k_bin_count .. k_fine_sort  signed 16-bit window digits of every term, grouped by
+//                     bucket with a two-pass LDS-privatised MSD partition (see "sort")
 //   k_accumulate      load-balanced bucket accumulation: every thread owns exactly
 //                     ACC_CHUNK consecutive sorted entries (not a bucket), so Poisson bucket
 //                     sizes do not diverge a wavefront; bucket pieces cut by a chunk
@@ -42,22 +41,43 @@ struct TermList {
   uint32_t total;
 };
 
-// ------------------------------------------------------------------------------ digits
-template <bool SCATTER>
-__global__ void __launch_bounds__(256) k_digits(TermList tl, const uint8_t* __restrict__ inf,
-                                                uint32_t* __restrict__ cnt_or_cursor,
-                                                uint32_t* __restrict__ sorted_val,
-                                                uint32_t* __restrict__ sorted_key) {
-  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= tl.total) return;
+// ------------------------------------------------------------------------------ sort
+// Entries (one per nonzero signed window digit) are grouped by global bucket id
+// key = set * 2^15 + (|d| - 1) with a two-pass MSD partition that keeps the atomics in LDS:
+//   k_bin_count   tile = (class, window, 4096 terms): LDS histogram over the window's 256
+//                 coarse bins (key >> 7), then one global atomic per non-empty bin
+//   k_bin_scan    exclusive scan of the nsets*256 coarse counts (+ total entries)
+//   k_bin_scatter same digits; LDS ranks, one global atomic per bin reserves the tile's run,
+//                 entries written as (key << 32 | value) into their coarse bin
+//   k_fine_sort   one workgroup per coarse bin (128 buckets): LDS counting sort, writes the
+//                 sorted (value, key) arrays and every bucket's offset/count
+// Sorting is unstable inside a bucket; bucket sums (and the final affine result) do not
+// depend on the order.
+constexpr int COARSE_SHIFT = 7;
+constexpr int FINE = 1 << COARSE_SHIFT;                 // buckets per coarse bin
+constexpr int BINS_PER_SET = NBUCKETS >> COARSE_SHIFT;  // 256
+constexpr int TILE_TERMS = 4096;                        // terms per tile (16 per thread)
+
+struct TileRef {
+  int k, w;
+  uint32_t c;
+};
+KZ_DEV TileRef tile_decode(const TermList& tl, uint32_t t) {
   int k = 0;
-  uint32_t local = t;
-  while (k < (int)tl.nclass - 1 && local >= tl.c[k].count) { local -= tl.c[k].count; ++k; }
-  const TermClass& C = tl.c[k];
-  uint32_t pt = C.pt_base + local;
-  if (inf[pt]) return;
-  uint32_t w8[8];
+  for (; k < (int)tl.nclass - 1; ++k) {
+    uint32_t chunks = (tl.c[k].count + TILE_TERMS - 1) / TILE_TERMS;
+    uint32_t nt = chunks * tl.c[k].nwin;
+    if (t < nt) break;
+    t -= nt;
+  }
+  uint32_t chunks = (tl.c[k].count + TILE_TERMS - 1) / TILE_TERMS;
+  return {k, (int)(t / chunks), t % chunks};
+}
+
+// signed 16-bit digit of window w (recoding windows 0..w; carry-propagating)
+KZ_DEV int signed_digit(const TermClass& C, uint32_t local, int w) {
   const uint32_t* s = C.scal + (size_t)local * C.scal_stride;
+  uint32_t w8[8];
   if (C.scal_words == 4) {
     uint4 q = *reinterpret_cast<const uint4*>(s);
     w8[0] = q.x; w8[1] = q.y; w8[2] = q.z; w8[3] = q.w;
@@ -69,64 +89,53 @@ __global__ void __launch_bounds__(256) k_digits(TermList tl, const uint8_t* __re
     w8[4] = q1.x; w8[5] = q1.y; w8[6] = q1.z; w8[7] = q1.w;
   }
   uint32_t carry = 0;
+  int d = 0;
 #pragma unroll
-  for (int w = 0; w < 16; ++w) {
-    if (w >= (int)C.nwin) break;
-    uint32_t raw = (w8[w >> 1] >> ((w & 1) * 16)) & 0xffffu;
-    int d = (int)(raw + carry);
+  for (int i = 0; i < 16; ++i) {
+    if (i > w) break;
+    uint32_t raw = (w8[i >> 1] >> ((i & 1) * 16)) & 0xffffu;
+    d = (int)(raw + carry);
     if (d > NBUCKETS) { d -= (1 << WBITS); carry = 1; } else { carry = 0; }
-    if (d != 0) {
-      uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-      uint32_t key = (C.set_base + w) * NBUCKETS + (mag - 1);
-      if (!SCATTER) {
-        atomicAdd(&cnt_or_cursor[key], 1u);
-      } else {
-        uint32_t pos = atomicAdd(&cnt_or_cursor[key], 1u);
-        sorted_val[pos] = (pt << 1) | (d < 0 ? 1u : 0u);
-        sorted_key[pos] = key;
-      }
-    }
   }
+  return d;
 }
 
-// ------------------------------------------------------------------------------ scan
-constexpr int SCAN_BLOCK = 256;
-constexpr int SCAN_ITEMS = 16;  // 4096 counts per block
+static __global__ void __launch_bounds__(256) k_bin_count(TermList tl, const uint8_t* __restrict__ inf,
+                                                   uint32_t* __restrict__ coarse_cnt) {
+  __shared__ uint32_t hist[BINS_PER_SET];
+  const TileRef T = tile_decode(tl, blockIdx.x);
+  const TermClass& C = tl.c[T.k];
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  for (int j = 0; j < TILE_TERMS / 256; ++j) {
+    uint32_t local = T.c * TILE_TERMS + j * 256 + threadIdx.x;
+    if (local >= C.count || inf[C.pt_base + local]) continue;
+    int d = signed_digit(C, local, T.w);
+    if (d != 0) {
+      uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+      atomicAdd(&hist[(mag - 1) >> COARSE_SHIFT], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t h = hist[threadIdx.x];
+  if (h) atomicAdd(&coarse_cnt[(C.set_base + T.w) * BINS_PER_SET + threadIdx.x], h);
+}
 
-static __global__ void __launch_bounds__(SCAN_BLOCK) k_scan_blocks(const uint32_t* __restrict__ cnt, uint32_t nb,
-                                                           uint32_t* __restrict__ off, uint32_t* __restrict__ block_tot) {
-  __shared__ uint32_t s[SCAN_BLOCK];
-  uint32_t base = blockIdx.x * SCAN_BLOCK * SCAN_ITEMS + threadIdx.x * SCAN_ITEMS;
-  uint32_t v[SCAN_ITEMS];
+// single block: exclusive scan of nbins (<= 8192) coarse counts; cursor copy; total
+static __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __restrict__ cnt, uint32_t nbins,
+                                                          uint32_t* __restrict__ off, uint32_t* __restrict__ cursor,
+                                                          uint32_t* __restrict__ total) {
+  __shared__ uint32_t s[1024];
+  constexpr int PER = 8;
+  uint32_t v[PER];
   uint32_t sum = 0;
+  const uint32_t base = threadIdx.x * PER;
 #pragma unroll
-  for (int i = 0; i < SCAN_ITEMS; ++i) {
-    v[i] = (base + i < nb) ? cnt[base + i] : 0u;
+  for (int i = 0; i < PER; ++i) {
+    v[i] = base + i < nbins ? cnt[base + i] : 0u;
     sum += v[i];
   }
   s[threadIdx.x] = sum;
-  __syncthreads();
-  for (int d = 1; d < SCAN_BLOCK; d <<= 1) {
-    uint32_t x = threadIdx.x >= (unsigned)d ? s[threadIdx.x - d] : 0u;
-    __syncthreads();
-    s[threadIdx.x] += x;
-    __syncthreads();
-  }
-  uint32_t run = s[threadIdx.x] - sum;  // exclusive prefix within block
-#pragma unroll
-  for (int i = 0; i < SCAN_ITEMS; ++i) {
-    if (base + i < nb) off[base + i] = run;
-    run += v[i];
-  }
-  if (threadIdx.x == SCAN_BLOCK - 1) block_tot[blockIdx.x] = s[threadIdx.x];
-}
-
-// single block: exclusive scan of block totals (<= 1024 blocks), writes grand total
-static __global__ void __launch_bounds__(1024) k_scan_totals(uint32_t* __restrict__ block_tot, uint32_t nblocks,
-                                                      uint32_t* __restrict__ total) {
-  __shared__ uint32_t s[1024];
-  uint32_t v = threadIdx.x < nblocks ? block_tot[threadIdx.x] : 0u;
-  s[threadIdx.x] = v;
   __syncthreads();
   for (int d = 1; d < 1024; d <<= 1) {
     uint32_t x = threadIdx.x >= (unsigned)d ? s[threadIdx.x - d] : 0u;
@@ -134,18 +143,90 @@ static __global__ void __launch_bounds__(1024) k_scan_totals(uint32_t* __restric
     s[threadIdx.x] += x;
     __syncthreads();
   }
-  if (threadIdx.x < nblocks) block_tot[threadIdx.x] = s[threadIdx.x] - v;
+  uint32_t run = s[threadIdx.x] - sum;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    if (base + i < nbins) { off[base + i] = run; cursor[base + i] = run; }
+    run += v[i];
+  }
   if (threadIdx.x == 1023) *total = s[1023];
 }
 
-static __global__ void __launch_bounds__(256) k_scan_add(uint32_t* __restrict__ off, uint32_t nb,
-                                                  const uint32_t* __restrict__ block_tot,
-                                                  uint32_t* __restrict__ cursor) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nb) return;
-  uint32_t o = off[i] + block_tot[i / (SCAN_BLOCK * SCAN_ITEMS)];
-  off[i] = o;
-  cursor[i] = o;
+static __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint8_t* __restrict__ inf,
+                                                     uint32_t* __restrict__ coarse_cursor,
+                                                     uint64_t* __restrict__ tmp) {
+  __shared__ uint32_t hist[BINS_PER_SET];
+  __shared__ uint32_t base[BINS_PER_SET];
+  const TileRef T = tile_decode(tl, blockIdx.x);
+  const TermClass& C = tl.c[T.k];
+  const uint32_t set = C.set_base + T.w;
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t rank[TILE_TERMS / 256], key[TILE_TERMS / 256], ent[TILE_TERMS / 256];
+#pragma unroll
+  for (int j = 0; j < TILE_TERMS / 256; ++j) {
+    key[j] = 0xffffffffu;
+    uint32_t local = T.c * TILE_TERMS + j * 256 + threadIdx.x;
+    if (local >= C.count) continue;
+    uint32_t pt = C.pt_base + local;
+    if (inf[pt]) continue;
+    int d = signed_digit(C, local, T.w);
+    if (d == 0) continue;
+    uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+    key[j] = set * NBUCKETS + (mag - 1);
+    ent[j] = (pt << 1) | (d < 0 ? 1u : 0u);
+    rank[j] = atomicAdd(&hist[(mag - 1) >> COARSE_SHIFT], 1u);
+  }
+  __syncthreads();
+  uint32_t h = hist[threadIdx.x];
+  base[threadIdx.x] = h ? atomicAdd(&coarse_cursor[set * BINS_PER_SET + threadIdx.x], h) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TILE_TERMS / 256; ++j) {
+    if (key[j] == 0xffffffffu) continue;
+    tmp[base[(key[j] >> COARSE_SHIFT) & (BINS_PER_SET - 1)] + rank[j]] = ((uint64_t)key[j] << 32) | ent[j];
+  }
+}
+
+// one workgroup per coarse bin g: LDS counting sort of its entries by the low 7 key bits
+static __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ coarse_off,
+                                                   const uint32_t* __restrict__ coarse_cnt,
+                                                   const uint64_t* __restrict__ tmp,
+                                                   uint32_t* __restrict__ off, uint32_t* __restrict__ cnt,
+                                                   uint32_t* __restrict__ sorted_val,
+                                                   uint32_t* __restrict__ sorted_key) {
+  __shared__ uint32_t fine[FINE];
+  __shared__ uint32_t cursor[FINE];
+  const uint32_t g = blockIdx.x;
+  const uint32_t start = coarse_off[g], count = coarse_cnt[g];
+  if (threadIdx.x < FINE) fine[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t e = threadIdx.x; e < count; e += 256) atomicAdd(&fine[(uint32_t)(tmp[start + e] >> 32) & (FINE - 1)], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // 128-entry exclusive scan
+    uint32_t run = 0;
+    for (int f = 0; f < FINE; ++f) { cursor[f] = run; run += fine[f]; }
+  }
+  __syncthreads();
+  if (threadIdx.x < FINE) {
+    uint32_t key = g * FINE + threadIdx.x;
+    off[key] = start + cursor[threadIdx.x];
+    cnt[key] = fine[threadIdx.x];
+  }
+  __syncthreads();
+  for (uint32_t e = threadIdx.x; e < count; e += 256) {
+    uint64_t v = tmp[start + e];
+    uint32_t key = (uint32_t)(v >> 32);
+    uint32_t pos = start + atomicAdd(&cursor[key & (FINE - 1)], 1u);
+    sorted_val[pos] = (uint32_t)v;
+    sorted_key[pos] = key;
+  }
+}
+
+inline uint32_t num_tiles_host(const TermList& tl) {
+  uint32_t t = 0;
+  for (uint32_t k = 0; k < tl.nclass; ++k) t += ((tl.c[k].count + TILE_TERMS - 1) / TILE_TERMS) * tl.c[k].nwin;
+  return t;
 }
 
 // ------------------------------------------------------------------------------ points I/O
@@ -254,7 +335,7 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
   if (c0 != c - 1) return;                // a later continuation chunk: handled by c0+1
   uint32_t c1 = (o + cnt[key] - 1) / ACC_CHUNK;
   Xyzz<Cv> acc = load_xyzz(&part_last[c0]);
-  for (uint32_t cc = c; cc <= c1; ++cc) acc = xyzz_add_c(acc, load_xyzz(&part_first[cc]));
+  for (uint32_t cc = c; cc <= c1; ++cc) acc = xyzz_add(acc, load_xyzz(&part_first[cc]));
   store_xyzz(&buckets[key], acc);
 }
 

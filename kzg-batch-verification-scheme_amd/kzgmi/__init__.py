@@ -72,6 +72,8 @@ def lib():
         "kzgmi_partial_bytes": ([c.c_int], sz),
         "kzgmi_batch_partial_device": ([vp, vp, vp, vp, vp, vp, sz, c.c_uint64, u8p, vp], c.c_int),
         "kzgmi_batch_combine_device": ([vp, vp, vp, c.c_int, ip], c.c_int),
+        "kzgmi_batch_partial_device_async": ([vp, vp, c.c_int, vp, vp, vp, vp, sz, c.c_uint64, u8p, vp], c.c_int),
+        "kzgmi_batch_combine_device_async": ([vp, vp, c.c_int, vp, c.c_int], c.c_int),
         "kzgmi_msm_partial_device": ([vp, c.c_int, vp, vp, sz, vp], c.c_int),
         "kzgmi_msm_combine_device": ([vp, c.c_int, vp, c.c_int, u8p], c.c_int),
         "kzgmi_pairing": ([vp, c.c_int, u8p, u8p, u8p], c.c_int),
@@ -96,7 +98,8 @@ def exported_symbols():
         "kzgmi_ctx_destroy", "kzgmi_srs_load", "kzgmi_srs_free", "kzgmi_batch_verify",
         "kzgmi_batch_verify_device", "kzgmi_batch_verify_device_async", "kzgmi_slot_wait",
         "kzgmi_last_combination", "kzgmi_msm_g1", "kzgmi_msm_g1_device", "kzgmi_partial_bytes",
-        "kzgmi_batch_partial_device", "kzgmi_batch_combine_device", "kzgmi_msm_partial_device",
+        "kzgmi_batch_partial_device", "kzgmi_batch_combine_device", "kzgmi_batch_partial_device_async",
+        "kzgmi_batch_combine_device_async", "kzgmi_msm_partial_device",
         "kzgmi_msm_combine_device", "kzgmi_pairing", "kzgmi_gen_g1", "kzgmi_gen_tuples",
         "kzgmi_g2_mul", "kzgmi_probe_fpmul", "kzgmi_set_profiling", "kzgmi_get_phase_ms",
     ]
@@ -245,6 +248,18 @@ class Context:
         _check(lib().kzgmi_batch_combine_device(self.handle, srs.handle, _dptr(partials), int(n_parts),
                                                 ctypes.byref(ok)))
         return bool(ok.value)
+
+    def batch_partial_async(self, srs: Srs, slot: int, commitments, zs, ys, proofs, n: int, index_offset: int,
+                            seed: bytes, out):
+        """Enqueue this shard's partial (A_k, B_k) on `slot`; complete with wait(slot)."""
+        _check(lib().kzgmi_batch_partial_device_async(self.handle, srs.handle, int(slot), _dptr(commitments),
+                                                      _dptr(zs), _dptr(ys), _dptr(proofs), n, int(index_offset),
+                                                      bytes(seed), _dptr(out)))
+
+    def batch_combine_async(self, srs: Srs, slot: int, partials, n_parts: int):
+        """Enqueue sum-of-partials + pairing check on `slot`; wait(slot) returns the verdict."""
+        _check(lib().kzgmi_batch_combine_device_async(self.handle, srs.handle, int(slot), _dptr(partials),
+                                                      int(n_parts)))
 
     def msm_partial(self, curve: str, points, scalars, n: int, out):
         _check(lib().kzgmi_msm_partial_device(self.handle, CURVES[curve], _dptr(points), _dptr(scalars), n,

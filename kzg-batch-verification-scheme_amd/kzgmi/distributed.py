@@ -11,7 +11,11 @@ two-pairing check, so all ranks return the same verdict without a broadcast.
 RCCL has no elliptic-curve reduction operator (rccl.h:448-454 lists sum/prod/max/min/avg),
 so gather-then-add IS the collective; the payload is ~400 B per rank (latency-bound).
 
-`backend` is anything with the three methods used below (a `kzgmi.Context` on the GPU; the
+`ShardedPipeline` keeps `slots` global batches in flight per rank (async partial on slot
+k % slots, then gather + pairing of the batch that used the slot before), so a rank runs
+at the single-GPU pipelined rate plus one small all-gather per batch.
+
+`backend` is anything with the methods used below (a `kzgmi.Context` on the GPU; the
 CPU tests substitute a double built on the oracle to exercise this orchestration with gloo).
 """
 from __future__ import annotations
@@ -46,6 +50,77 @@ def sharded_batch_verify(backend, srs, commitments, zs, ys, proofs, n_local: int
     gathered = torch.empty(world * 2 * pb, dtype=torch.uint8, device=dev)
     dist.all_gather_into_tensor(gathered, local, group=group)
     return backend.batch_combine(srs, gathered, world)
+
+
+class ShardedPipeline:
+    """Several global batches in flight per rank (the multi-GPU form of the single-GPU slot
+    pipeline).  Batch k's shard partial runs on slot k % slots.  When a slot comes round
+    again its partial (batch k - slots) is all-gathered and the sum-of-partials + pairing
+    check is enqueued on combine lane j % lanes (context slots slots .. slots+lanes-1); a
+    lane's verdict is collected only when the lane is reused, so the host never blocks on a
+    pairing while shard work waits to be issued.  The backend context needs slots + lanes
+    workspaces.  Every rank must submit the same sequence of batches (the all-gathers are
+    collectives); verdicts come back in submission order.
+
+    submit() returns the verdicts of batches that completed during the call;
+    drain() completes everything still in flight.
+    """
+
+    def __init__(self, backend, srs, slots: int = 3, lanes: int = 2, group=None):
+        import torch
+        import torch.distributed as dist
+        self.backend, self.srs, self.group = backend, srs, group
+        self.slots, self.lanes = slots, lanes
+        self.world = dist.get_world_size(group)
+        pb = backend.partial_bytes(srs.curve)
+        self.dev = backend.tensor_device()
+        self.local = [torch.empty(2 * pb, dtype=torch.uint8, device=self.dev) for _ in range(slots)]
+        # one gather buffer per lane: a lane's combine reads it until the lane is reused
+        self.gathered = [torch.empty(self.world * 2 * pb, dtype=torch.uint8, device=self.dev) for _ in range(lanes)]
+        self.pending = [False] * slots
+        self.lane_pending = [False] * lanes
+        self.k = 0      # batches submitted
+        self.j = 0      # combines issued
+
+    def _collect_lane(self, lane: int, out):
+        if self.lane_pending[lane]:
+            out.append(self.backend.wait(self.slots + lane))
+            self.lane_pending[lane] = False
+
+    def _gather_and_combine(self, s: int, out):
+        import torch
+        import torch.distributed as dist
+        self.backend.wait(s)                                   # shard partial ready (errors raise here)
+        self.pending[s] = False
+        lane = self.j % self.lanes
+        self.j += 1
+        self._collect_lane(lane, out)                          # verdict of the batch `lanes` combines ago
+        dist.all_gather_into_tensor(self.gathered[lane], self.local[s], group=self.group)
+        if str(self.dev).startswith("cuda"):
+            torch.cuda.current_stream().synchronize()          # gathered records visible to the lane stream
+        self.backend.batch_combine_async(self.srs, self.slots + lane, self.gathered[lane], self.world)
+        self.lane_pending[lane] = True
+
+    def submit(self, commitments, zs, ys, proofs, n_local: int, offset: int, seed: bytes):
+        s = self.k % self.slots
+        self.k += 1
+        done = []
+        if self.pending[s]:
+            self._gather_and_combine(s, done)
+        self.backend.batch_partial_async(self.srs, s, commitments, zs, ys, proofs, n_local, offset, seed,
+                                         self.local[s])
+        self.pending[s] = True
+        return done
+
+    def drain(self):
+        out = []
+        for i in range(self.slots):
+            s = (self.k + i) % self.slots                      # oldest first
+            if self.pending[s]:
+                self._gather_and_combine(s, out)
+        for i in range(self.lanes):
+            self._collect_lane((self.j + i) % self.lanes, out)
+        return out
 
 
 def sharded_msm(backend, curve: str, points, scalars, n_local: int, group=None) -> bytes:

@@ -36,6 +36,18 @@ class OracleBackend:
                                    offset, self.g2, self.tau_g2, seed)
         out.copy_(torch.frombuffer(bytearray(A + B), dtype=torch.uint8))
 
+    # pipelined forms (kzgmi.distributed.ShardedPipeline): run eagerly, report at wait()
+    def batch_partial_async(self, srs, slot, commitments, zs, ys, proofs, n, offset, seed, out):
+        self.batch_partial(srs, commitments, zs, ys, proofs, n, offset, seed, out)
+        self._slot_result = getattr(self, "_slot_result", {})
+        self._slot_result[slot] = True
+
+    def batch_combine_async(self, srs, slot, gathered, n_parts):
+        self._slot_result[slot] = self.batch_combine(srs, gathered, n_parts)
+
+    def wait(self, slot):
+        return self._slot_result.pop(slot)
+
     def batch_combine(self, srs, gathered, n_parts):
         from oracle import oracle as O
         from oracle.pyspec import curves as pc
@@ -84,6 +96,39 @@ def _worker(rank, world, port, curve, n_total, corrupt_index, result_q):
     dist.destroy_process_group()
 
 
+def _pipeline_worker(rank, world, port, curve, n_total, corrupt_batches, result_q):
+    """4 global batches through a 2-slot ShardedPipeline; batch b corrupts tuple b*3 if listed."""
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "kzg-batch-verification-scheme_amd"))
+    import json
+    import torch.distributed as dist
+    from kzgmi.distributed import ShardedPipeline, shard_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    with open(os.path.join(ROOT, "tests", "golden", "%s_batch_n%d.json" % (curve, n_total))) as f:
+        g = json.load(f)
+    h = bytes.fromhex
+    C, z, y, P = (h(g[k]) for k in ("commitments", "zs", "ys", "proofs"))
+    off, cnt = shard_range(n_total, world, rank)
+    g1b = len(C) // n_total
+    be = OracleBackend(curve, h(g["g2"]), h(g["tau_g2"]))
+    pipe = ShardedPipeline(be, FakeSrs(curve), slots=2, lanes=2)
+    verdicts = []
+    for b in range(4):
+        yb = bytearray(y)
+        if b in corrupt_batches:
+            yb[32 * (3 * b) + 31] ^= 1
+        verdicts += pipe.submit(C[off * g1b:(off + cnt) * g1b], z[off * 32:(off + cnt) * 32],
+                                bytes(yb[off * 32:(off + cnt) * 32]), P[off * g1b:(off + cnt) * g1b], cnt, off,
+                                h(g["seed"]))
+    verdicts += pipe.drain()
+    result_q.put((rank, verdicts))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -111,3 +156,18 @@ def test_sharded_verify_world2(curve, n, corrupt, expect):
         assert p.exitcode == 0
     res = sorted(q.get() for _ in range(2))
     assert [ok for _, ok in res] == [expect, expect]
+
+
+def test_sharded_pipeline_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, 2, port, "bls12_381", 16, (1, 2), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    res = sorted(q.get() for _ in range(2))
+    assert [v for _, v in res] == [[True, False, False, True]] * 2

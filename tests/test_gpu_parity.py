@@ -227,3 +227,41 @@ def test_sharded_partials_equal_unsharded(ctx, torch_dev):
     ctx.msm_partial(curve, pts[: 700 * g1b], sc[: 700 * 32], 700, mp[:pb])
     ctx.msm_partial(curve, pts[700 * g1b:], sc[700 * 32:], 1300, mp[pb:])
     assert ctx.msm_combine(curve, mp, 2) == ctx.msm_g1(curve, pts, sc, n=2000)
+
+
+@pytest.mark.gpu
+def test_sharded_pipeline_rccl_world1(ctx, torch_dev):
+    """kzgmi.distributed.ShardedPipeline on the device over a world-1 RCCL group: async shard
+    partials, all-gather, async combine on the combine slot; verdicts in submission order."""
+    import socket
+    import torch.distributed as dist
+    from kzgmi.distributed import ShardedPipeline
+    torch = torch_dev
+    curve = "bls12_381"
+    C = pc.CURVES[curve]
+    n, tau = 700, 99
+    seed = hashlib.sha256(b"pipe").digest()
+    Cm, z, y, P = _gen_batch(ctx, torch, curve, n, tau, seed)
+    g2 = pk.g2_to_bytes(C.g2, C)
+    srs = ctx.load_srs(curve, g2, O.g2_mul(curve, g2, tau))
+    ybad = y.clone()
+    ybad[31] ^= 1
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    created = not dist.is_initialized()
+    if created:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        pipe = ShardedPipeline(ctx, srs, slots=1, lanes=1)  # ctx has 2 slots: 1 shard slot + 1 combine lane
+        out = []
+        for b in range(5):
+            out += pipe.submit(Cm, z, ybad if b in (1, 4) else y, P, n, 0, seed)
+        out += pipe.drain()
+        assert out == [True, False, True, True, False]
+    finally:
+        if created:
+            dist.destroy_process_group()

@@ -1,5 +1,6 @@
 #!/bin/bash
-# One GPU-box session: parity tests, smoke, bench, rocprof kernel-trace summary.
+# One GPU-box session: parity tests, smoke, bench (+ optional sharded-pipeline bench and
+# rocprof kernel-trace summary).  Every GPU step has its own time limit; steps chain with ||exit.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -10,7 +11,11 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 cat gpurun_out/smoke.log
 timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -30 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
+if [ -n "${SHARDED:-}" ]; then
+  timeout -k 10 600 python bench.py --sharded --no-cpu --msm-steps 0 > gpurun_out/bench_sharded.json 2> gpurun_out/bench_sharded.err || { tail -30 gpurun_out/bench_sharded.err; exit 1; }
+  cat gpurun_out/bench_sharded.json
+fi
 if [ -n "${PROFILE:-}" ]; then
-  cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 4 --warmup 1 --no-cpu --msm-steps 2 > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1 || { tail -20 "$GRAFT_REPO_ROOT/gpurun_out/prof.log"; exit 1; }
-  find "$GRAFT_REPO_ROOT/gpurun_out/prof" -name '*stats*' | head
+  cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 4 --warmup 1 --no-cpu --msm-steps 2 > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1 || { tail -20 "$GRAFT_REPO_ROOT/gpurun_out/prof.log"; exit 1; }
+  find "$GRAFT_REPO_ROOT/gpurun_out/prof" -name '*stats*'
 fi
