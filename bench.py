@@ -90,14 +90,25 @@ def cpu_baseline(curve, Cm, z, y, P, n_full, seed, target_s):
         return time.perf_counter() - t0, ok
 
     tg2_bytes = cpu_baseline.tg2
-    m = 1 << 12
-    dt, ok = run(m)
-    # MSM cost ~ linear in m: pick the largest power of two expected to take <= target_s
-    while m * 2 <= n_full and dt * 2 * (1.15) <= target_s:
-        m *= 2
-        dt *= 2
-    dt, ok = run(m)
-    assert ok, "oracle rejected a valid batch"
+
+    def sized_run(budget_s):
+        m = 1 << 10
+        dt, ok = run(m)
+        # MSM cost ~ linear in m: pick the largest power of two expected to take <= budget_s
+        while m * 2 <= n_full and dt * 2 * (1.15) <= budget_s:
+            m *= 2
+            dt *= 2
+        dt, ok = run(m)
+        assert ok, "oracle rejected a valid batch"
+        return m, dt
+
+    m, dt = sized_run(target_s)
+    # single-core figure (SURVEY.md 8d "also record the single-core time")
+    O.set_threads(1)
+    try:
+        m1, dt1 = sized_run(min(target_s, 4.0))
+    finally:
+        O.set_threads(threads)
     return {
         "value": (m / dt) / n_full,
         "unit": "batch-verifies/s (extrapolated linearly from the sample to n=%d tuples)" % n_full,
@@ -106,14 +117,16 @@ def cpu_baseline(curve, Cm, z, y, P, n_full, seed, target_s):
         "sample": "oracle/c batch_verify on the first %d of the %d tuples, %.2f s on %d OpenMP threads "
                   "(self-authored CPU verifier; the reference has none)" % (m, n_full, dt, threads),
         "sample_tuples_per_s": m / dt,
+        "single_core": {"value": (m1 / dt1) / n_full, "sample_tuples": m1, "seconds": dt1,
+                        "tuples_per_s": m1 / dt1},
     }
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--n", type=int, default=1 << 20, help="tuples per GPU")
     ap.add_argument("--curve", default="bls12_381", choices=["bls12_381", "bn254"])
     ap.add_argument("--slots", type=int, default=0,

@@ -308,6 +308,9 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__
       cur = key;
     }
     uint32_t v = sorted_val[e];
+#ifdef KZ_EXPERIMENT_LOCAL_PTS  // timing experiment only: gathers hit 1024 cache-resident points
+    v &= 2047u;
+#endif
     Affine<Cv> p = load_affine(pts, v >> 1);
     p.y = fp_cneg(p.y, (v & 1) != 0);
     acc = xyzz_add_affine(acc, p);

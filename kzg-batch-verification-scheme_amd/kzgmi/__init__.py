@@ -19,7 +19,8 @@ from dataclasses import dataclass
 from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkzgmi.so")
+# KZGMI_LIB selects an alternative build (timing experiments); default: the in-tree library
+LIB_PATH = os.environ.get("KZGMI_LIB") or os.path.join(_HERE, "libkzgmi.so")
 
 CURVES = {"bls12_381": 0, "bn254": 1}
 FP_BYTES = {"bls12_381": 48, "bn254": 32}

@@ -1,0 +1,96 @@
+"""Parity at BASELINE.json's full sizes, HIP path vs the C oracle.
+
+The oracle (OpenMP, the GPU box's host cores) finishes these in seconds, so the check is the
+strongest one available: bit-exact combined points A and B (or the MSM result) plus the
+verdict, and the size-independent property that one corrupted evaluation flips the verdict.
+Inputs are generated on the device (kzgmi_gen_tuples / kzgmi_gen_g1; their host restatement
+is checked in test_gpu_parity.py) and copied to the host for the oracle.
+"""
+import hashlib
+
+import pytest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+from oracle import oracle as O  # noqa: E402  (checker only)
+from oracle.pyspec import curves as pc  # noqa: E402
+from oracle.pyspec import kzg as pk  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import kzgmi
+    c = kzgmi.Context(0, 1)
+    yield c
+    c.close()
+
+
+def _host(t):
+    return t.cpu().numpy().tobytes()
+
+
+def _gen_batch(ctx, curve, n, tau, seed):
+    import torch
+    g1b = 2 * pc.CURVES[curve].fp_bytes
+    Cm = torch.empty(n * g1b, dtype=torch.uint8, device="cuda")
+    P = torch.empty(n * g1b, dtype=torch.uint8, device="cuda")
+    z = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    y = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    ctx.gen_tuples(curve, tau, seed, n, Cm, z, y, P)
+    return Cm, z, y, P
+
+
+@pytest.mark.parametrize("curve,log_n,seed_no", [("bls12_381", 20, 4), ("bn254", 22, 5)])
+def test_full_batch_vs_oracle(ctx, curve, log_n, seed_no):
+    """cfg 3 (BLS12-381, n = 2^20) and cfg 5 (BN254, n = 2^22): A, B, verdict bit-exact."""
+    C = pc.CURVES[curve]
+    n, tau = 1 << log_n, 0xC0FFEE + seed_no
+    Cm, z, y, P = _gen_batch(ctx, curve, n, tau, hashlib.sha256(b"cfg%d" % seed_no).digest())
+    g2 = pk.g2_to_bytes(C.g2, C)
+    tg2 = O.g2_mul(curve, g2, tau)
+    srs = ctx.load_srs(curve, g2, tg2)
+    vseed = hashlib.sha256(b"cfg%d-verify" % seed_no).digest()
+    assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n) is True
+    A, B = ctx.last_combination(curve)
+    hb = [_host(t) for t in (Cm, z, y, P)]
+    ok, Ao, Bo = O.batch_verify(curve, hb[0], hb[1], hb[2], hb[3], n, g2, tg2, vseed, want_ab=True)
+    assert ok is True and A == Ao and B == Bo
+    # negative run (cfg 3 "plus one negative run with a corrupted y"): last tuple's y
+    y[32 * (n - 1) + 31] ^= 1
+    assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n) is False
+
+
+def test_full_msm_vs_oracle(ctx):
+    """cfg 2: BLS12-381 MSM, n = 2^20, points k_i G1 with k_i uniform in Fr, uniform scalars."""
+    import random
+    import torch
+    curve = "bls12_381"
+    C = pc.CURVES[curve]
+    n = 1 << 20
+    rng = random.Random(2)
+    ks = b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(n))
+    rng = random.Random(3)
+    sc = b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(n))
+    d_k = torch.frombuffer(bytearray(ks), dtype=torch.uint8).cuda()
+    pts = torch.empty(n * 2 * C.fp_bytes, dtype=torch.uint8, device="cuda")
+    ctx.gen_g1(curve, d_k, n, pts)
+    d_sc = torch.frombuffer(bytearray(sc), dtype=torch.uint8).cuda()
+    got = ctx.msm_g1(curve, pts, d_sc, n=n)
+    assert got == O.msm_g1(curve, _host(pts), sc, n)
+
+
+def test_sharded_msm_cfg4_shape(ctx):
+    """cfg 4 shape on one device: two 2^21-point shards (msm_partial) + combine == one MSM."""
+    import torch
+    curve = "bls12_381"
+    C = pc.CURVES[curve]
+    n = 1 << 22
+    Cm, z, _, _ = _gen_batch(ctx, curve, n, 77, hashlib.sha256(b"cfg4").digest())
+    g1b = 2 * C.fp_bytes
+    pb = ctx.partial_bytes(curve)
+    parts = torch.empty(2 * pb, dtype=torch.uint8, device="cuda")
+    h = n // 2
+    ctx.msm_partial(curve, Cm[: h * g1b], z[: h * 32], h, parts[:pb])
+    ctx.msm_partial(curve, Cm[h * g1b:], z[h * 32:], h, parts[pb:])
+    got = ctx.msm_combine(curve, parts, 2)
+    assert got == O.msm_g1(curve, _host(Cm), _host(z), n)

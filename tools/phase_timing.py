@@ -1,0 +1,40 @@
+"""Single-batch phase timing (no verdict assertion: used with timing-experiment builds).
+
+python tools/phase_timing.py [--n N] [--reps R] [--lib path/to/libkzgmi.so]
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kzg-batch-verification-scheme_amd"))
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=1 << 20)
+ap.add_argument("--reps", type=int, default=4)
+ap.add_argument("--lib", default=None)
+ap.add_argument("--curve", default="bls12_381")
+args = ap.parse_args()
+if args.lib:
+    os.environ["KZGMI_LIB"] = args.lib
+import torch  # noqa: E402
+import kzgmi  # noqa: E402
+
+ctx = kzgmi.Context(0, 1)
+curve, n = args.curve, args.n
+g2 = kzgmi.G2_GENERATOR[curve]
+tau = 0x1234567
+srs = ctx.load_srs(curve, g2, ctx.g2_mul(curve, g2, tau))
+g1b = 2 * kzgmi.FP_BYTES[curve]
+C = torch.empty(n * g1b, dtype=torch.uint8, device="cuda")
+P = torch.empty(n * g1b, dtype=torch.uint8, device="cuda")
+z = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+y = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+ctx.gen_tuples(curve, tau, hashlib.sha256(b"t").digest(), n, C, z, y, P)
+seed = hashlib.sha256(b"v").digest()
+ok = ctx.batch_verify(srs, C, z, y, P, seed=seed, n=n)
+ctx.set_profiling(True)
+for _ in range(args.reps):
+    ok = ctx.batch_verify(srs, C, z, y, P, seed=seed, n=n)
+print(json.dumps({"ok": ok, "lib": kzgmi.LIB_PATH, "phases": ctx.phase_ms()}))
