@@ -134,6 +134,8 @@ def main():
     ap.add_argument("--msm-steps", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--compressed-steps", type=int, default=16,
+                    help="secondary: pipelined batches with compressed inputs + subgroup checks (0 = skip)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU pipeline (RCCL all-gather per batch) even at world size 1")
     args = ap.parse_args()
@@ -243,6 +245,44 @@ def main():
         phases_single = ctx.phase_ms()
         ctx.set_profiling(False)
 
+    # ---- secondary: compressed inputs + subgroup checks, single GPU
+    comp = None
+    if world == 1 and not sharded and args.compressed_steps > 0:
+        fb = kzgmi.FP_BYTES[curve]
+        cc = torch.empty(n * fb, dtype=torch.uint8, device="cuda")
+        pp = torch.empty(n * fb, dtype=torch.uint8, device="cuda")
+        ctx.g1_compress(curve, Cm, n, cc)
+        ctx.g1_compress(curve, P, n, pp)
+
+        def cstep(k):
+            s = k % slots
+            if pending[s]:
+                assert ctx.wait(s), "batch rejected"
+            ctx.batch_verify_async(srs, s, cc, z, y, pp, n, seed=vseed, compressed=True, subgroup_check=True)
+            pending[s] = True
+
+        for k in range(min(4, args.compressed_steps)):
+            cstep(k)
+        drain()
+        barrier()
+        ctx.set_profiling(True)
+        a = time.perf_counter()
+        for k in range(args.compressed_steps):
+            cstep(k)
+        drain()
+        barrier()
+        dt = time.perf_counter() - a
+        cph = ctx.phase_ms()
+        ctx.set_profiling(False)
+        ctx.set_profiling(True)
+        assert ctx.batch_verify(srs, cc, z, y, pp, seed=vseed, n=n, compressed=True, subgroup_check=True)
+        single = ctx.phase_ms()
+        ctx.set_profiling(False)
+        comp = {"batch_verifies_per_s": args.compressed_steps / dt, "steps": args.compressed_steps,
+                "input": "48 B compressed C and pi, decompressed + subgroup-checked on the GPU",
+                "phase_ms_single_batch": single, "phase_ms_avg_in_timed_region": cph}
+        del cc, pp
+
     # ---- secondary: G1 MSM pts/s at n points per GPU (commitments as points, z as scalars)
     msm_rate = None
     if args.msm_steps > 0:
@@ -340,6 +380,7 @@ def main():
             "single_batch_latency_ms": lat,
             "phase_ms_avg_in_timed_region": phases,
             "phase_ms_single_batch": phases_single,
+            "compressed_subgroup": comp,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu and "value" in cpu else None,
         },
     }

@@ -12,8 +12,11 @@
  *     G1: BLS12-381 96 B x||y, infinity = 0x40 || 95 zero bytes (ZCash uncompressed flags);
  *         BN254 64 B x||y, infinity = 64 zero bytes.
  *     G2: x.c1||x.c0||y.c1||y.c0 (192 B BLS12-381 / 128 B BN254), same infinity rules.
- *   - Points must be on the curve (checked: KZGMI_ERR_NOT_ON_CURVE); subgroup membership
- *     is the caller's responsibility (decompression/subgroup checks: SURVEY.md 8f item 1).
+ *   - Points must be on the curve (checked: KZGMI_ERR_NOT_ON_CURVE).  Subgroup membership is
+ *     checked only with KZGMI_FLAG_SUBGROUP_CHECK (the *_ex entry points, SURVEY.md 8f item
+ *     1), which also accept compressed G1 inputs (KZGMI_FLAG_COMPRESSED):
+ *       BLS12-381 48 B ZCash (0x80 compressed, 0x40 infinity, 0x20 larger y),
+ *       BN254 32 B gnark-crypto (top bits 0b10 smaller y, 0b11 larger y, 0b01 infinity).
  *   - Return value 0 = OK, negative = error (see KZGMI_ERR_*).  Invalid input is an error,
  *     never "ok = 0".  kzgmi_last_error() gives a thread-local message.
  *   - Threading: one ctx per host thread; calls on one ctx are serialised by the caller.
@@ -43,6 +46,12 @@ typedef enum { KZGMI_BLS12_381 = 0, KZGMI_BN254 = 1 } kzgmi_curve;
 #define KZGMI_ERR_SCALAR (-4)
 #define KZGMI_ERR_DEVICE (-5)
 #define KZGMI_ERR_OOM (-6)
+#define KZGMI_ERR_NOT_IN_SUBGROUP (-7)
+
+/* flags of the *_ex entry points */
+#define KZGMI_FLAG_COMPRESSED 1u     /* commitments/proofs are compressed G1 encodings */
+#define KZGMI_FLAG_SUBGROUP_CHECK 2u /* reject points outside the order-r subgroup (BLS12-381;
+                                        BN254 G1 has cofactor 1, the flag is a no-op there) */
 
 typedef struct kzgmi_ctx kzgmi_ctx; /* one GPU, its streams and workspaces */
 typedef struct kzgmi_srs kzgmi_srs; /* {G1, [1]_2, [tau]_2} + precomputed Miller lines */
@@ -85,6 +94,25 @@ int kzgmi_batch_verify_device_async(kzgmi_ctx* ctx, const kzgmi_srs* srs, int sl
                                     const void* d_proofs, size_t n, const uint8_t* seed32);
 int kzgmi_slot_wait(kzgmi_ctx* ctx, int slot, int* ok_out);
 
+/* batch_verify with input-format / validation flags (KZGMI_FLAG_*).
+ * flags = 0 is exactly kzgmi_batch_verify / kzgmi_batch_verify_device_async. */
+int kzgmi_batch_verify_ex(kzgmi_ctx* ctx, const kzgmi_srs* srs, const uint8_t* commitments,
+                          const uint8_t* zs, const uint8_t* ys, const uint8_t* proofs, size_t n,
+                          const uint8_t* seed32, uint32_t flags, int* ok_out);
+int kzgmi_batch_verify_device_ex_async(kzgmi_ctx* ctx, const kzgmi_srs* srs, int slot,
+                                       const void* d_commitments, const void* d_zs,
+                                       const void* d_ys, const void* d_proofs, size_t n,
+                                       const uint8_t* seed32, uint32_t flags);
+
+/* Validate n device-resident G1 encodings (flags: KZGMI_FLAG_COMPRESSED,
+ * KZGMI_FLAG_SUBGROUP_CHECK): 0 if all are valid, else the first error class found. */
+int kzgmi_g1_validate_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_points, size_t n,
+                             uint32_t flags);
+/* Compress n device-resident uncompressed G1 encodings into d_out (n x 48 B / 32 B).  Input
+ * utility for tests and benchmarks: no validation. */
+int kzgmi_g1_compress_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_points, size_t n,
+                             void* d_out);
+
 /* Diagnostics: the combined points A and B of the last synchronous batch_verify on slot 0
  * (G1 encodings, 2 x G1 bytes), for bit-exact parity tests against the oracle. */
 int kzgmi_last_combination(kzgmi_ctx* ctx, uint8_t* a_out, uint8_t* b_out);
@@ -112,7 +140,7 @@ int kzgmi_batch_combine_device(kzgmi_ctx* ctx, const kzgmi_srs* srs, const void*
 int kzgmi_batch_partial_device_async(kzgmi_ctx* ctx, const kzgmi_srs* srs, int slot,
                                      const void* d_commitments, const void* d_zs, const void* d_ys,
                                      const void* d_proofs, size_t n, uint64_t index_offset,
-                                     const uint8_t* seed32, void* d_partial_out);
+                                     const uint8_t* seed32, uint32_t flags, void* d_partial_out);
 int kzgmi_batch_combine_device_async(kzgmi_ctx* ctx, const kzgmi_srs* srs, int slot,
                                      const void* d_partials, int n_parts);
 int kzgmi_msm_partial_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_points,

@@ -146,6 +146,7 @@ int map_device_err(uint32_t e) {
     case DERR_ENCODING: return fail(KZGMI_ERR_ENCODING, "invalid point encoding");
     case DERR_NOT_ON_CURVE: return fail(KZGMI_ERR_NOT_ON_CURVE, "point not on curve");
     case DERR_SCALAR: return fail(KZGMI_ERR_SCALAR, "non-canonical scalar (>= r)");
+    case DERR_NOT_IN_SUBGROUP: return fail(KZGMI_ERR_NOT_IN_SUBGROUP, "point not in the order-r subgroup");
     default: return fail(KZGMI_ERR_DEVICE, "unknown device error");
   }
 }
@@ -193,7 +194,8 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl, uint32_t nsets, size
 // ------------------------------------------------------------------------------ batch
 template <class Cv>
 int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, const void* dz, const void* dy,
-                  const void* dpi, size_t n, const Seed& seed, uint64_t offset, void* d_partial_out) {
+                  const void* dpi, size_t n, const Seed& seed, uint64_t offset, void* d_partial_out,
+                  uint32_t flags) {
   using XY = Xyzz<Cv>;
   using FrF = Fp<typename Cv::FrP>;
   const size_t npts = 2 * n + 1;
@@ -211,8 +213,14 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   uint32_t* err = s.flags.template as<uint32_t>() + 1;
   Affine<Cv>* pts = s.pts.template as<Affine<Cv>>();
   uint8_t* inf = s.inf.template as<uint8_t>();
-  L::convert_points(st, (const uint8_t*)dpi, (uint32_t)n, pts, inf, err);
-  L::convert_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err);
+  if (flags & KZGMI_FLAG_COMPRESSED) {
+    L::decompress_points(st, (const uint8_t*)dpi, (uint32_t)n, pts, inf, err);
+    L::decompress_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err);
+  } else {
+    L::convert_points(st, (const uint8_t*)dpi, (uint32_t)n, pts, inf, err);
+    L::convert_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err);
+  }
+  if (flags & KZGMI_FLAG_SUBGROUP_CHECK) L::subgroup_check(st, pts, inf, (uint32_t)(2 * n), err);
   L::set_generator(st, pts + 2 * n, inf + 2 * n);
   mark(c, s, PH_CONVERT + 1);
   L::scalar_prep(st, seed, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n, s.scal_r.template as<uint32_t>(),
@@ -387,6 +395,13 @@ void kzgmi_srs_free(kzgmi_srs* srs) {
 
 int kzgmi_batch_verify_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const void* dC, const void* dz,
                                     const void* dy, const void* dpi, size_t n, const uint8_t* seed32) {
+  return kzgmi_batch_verify_device_ex_async(c, srs, slot, dC, dz, dy, dpi, n, seed32, 0);
+}
+
+int kzgmi_batch_verify_device_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const void* dC, const void* dz,
+                                       const void* dy, const void* dpi, size_t n, const uint8_t* seed32,
+                                       uint32_t flags) {
+  if (flags & ~(KZGMI_FLAG_COMPRESSED | KZGMI_FLAG_SUBGROUP_CHECK)) return fail(KZGMI_ERR_ARG, "unknown flags");
   CHK(check_ctx(c, slot));
   if (!srs || srs->ctx != c) return fail(KZGMI_ERR_ARG, "srs does not belong to this context");
   if (n && (!dC || !dz || !dy || !dpi)) return fail(KZGMI_ERR_ARG, "null input");
@@ -405,7 +420,7 @@ int kzgmi_batch_verify_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot
     return 0;
   }
   return dispatch(srs->curve, [&](auto cv) -> int {
-    return enqueue_batch<decltype(cv)>(c, s, srs, dC, dz, dy, dpi, n, seed, 0, nullptr);
+    return enqueue_batch<decltype(cv)>(c, s, srs, dC, dz, dy, dpi, n, seed, 0, nullptr, flags);
   });
 }
 
@@ -425,20 +440,32 @@ int kzgmi_batch_verify_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* dC
 
 int kzgmi_batch_verify(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commitments, const uint8_t* zs,
                        const uint8_t* ys, const uint8_t* proofs, size_t n, const uint8_t* seed32, int* ok_out) {
+  return kzgmi_batch_verify_ex(c, srs, commitments, zs, ys, proofs, n, seed32, 0, ok_out);
+}
+
+int kzgmi_batch_verify_ex(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commitments, const uint8_t* zs,
+                          const uint8_t* ys, const uint8_t* proofs, size_t n, const uint8_t* seed32, uint32_t flags,
+                          int* ok_out) {
   CHK(check_ctx(c));
   if (!srs || !ok_out) return fail(KZGMI_ERR_ARG, "null argument");
   if (n && (!commitments || !zs || !ys || !proofs)) return fail(KZGMI_ERR_ARG, "null input");
-  if (n == 0) return kzgmi_batch_verify_device(c, srs, nullptr, nullptr, nullptr, nullptr, 0, seed32, ok_out);
   Slot& s = c->slots[0];
-  const size_t gb = g1_bytes(srs->curve);
-  CHK(s.stage.ensure(n * (2 * gb + 64)));
-  uint8_t* base = s.stage.template as<uint8_t>();
-  uint8_t *dC = base, *dpi = base + n * gb, *dz = base + 2 * n * gb, *dy = dz + 32 * n;
-  HIPCHK(hipMemcpyAsync(dC, commitments, n * gb, hipMemcpyHostToDevice, s.stream));
-  HIPCHK(hipMemcpyAsync(dpi, proofs, n * gb, hipMemcpyHostToDevice, s.stream));
-  HIPCHK(hipMemcpyAsync(dz, zs, n * 32, hipMemcpyHostToDevice, s.stream));
-  HIPCHK(hipMemcpyAsync(dy, ys, n * 32, hipMemcpyHostToDevice, s.stream));
-  return kzgmi_batch_verify_device(c, srs, dC, dz, dy, dpi, n, seed32, ok_out);
+  uint8_t *dC = nullptr, *dpi = nullptr, *dz = nullptr, *dy = nullptr;
+  if (n) {
+    const size_t gb = (flags & KZGMI_FLAG_COMPRESSED) ? g1_bytes(srs->curve) / 2 : g1_bytes(srs->curve);
+    CHK(s.stage.ensure(n * (2 * gb + 64)));
+    uint8_t* base = s.stage.template as<uint8_t>();
+    dC = base;
+    dpi = base + n * gb;
+    dz = base + 2 * n * gb;
+    dy = dz + 32 * n;
+    HIPCHK(hipMemcpyAsync(dC, commitments, n * gb, hipMemcpyHostToDevice, s.stream));
+    HIPCHK(hipMemcpyAsync(dpi, proofs, n * gb, hipMemcpyHostToDevice, s.stream));
+    HIPCHK(hipMemcpyAsync(dz, zs, n * 32, hipMemcpyHostToDevice, s.stream));
+    HIPCHK(hipMemcpyAsync(dy, ys, n * 32, hipMemcpyHostToDevice, s.stream));
+  }
+  CHK(kzgmi_batch_verify_device_ex_async(c, srs, 0, dC, dz, dy, dpi, n, seed32, flags));
+  return kzgmi_slot_wait(c, 0, ok_out);
 }
 
 int kzgmi_last_combination(kzgmi_ctx* c, uint8_t* a_out, uint8_t* b_out) {
@@ -544,7 +571,8 @@ size_t kzgmi_partial_bytes(kzgmi_curve curve) {
 
 int kzgmi_batch_partial_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const void* dC, const void* dz,
                                      const void* dy, const void* dpi, size_t n, uint64_t index_offset,
-                                     const uint8_t* seed32, void* d_partial_out) {
+                                     const uint8_t* seed32, uint32_t flags, void* d_partial_out) {
+  if (flags & ~(KZGMI_FLAG_COMPRESSED | KZGMI_FLAG_SUBGROUP_CHECK)) return fail(KZGMI_ERR_ARG, "unknown flags");
   CHK(check_ctx(c, slot));
   if (!srs || srs->ctx != c || !d_partial_out) return fail(KZGMI_ERR_ARG, "bad argument");
   if (!seed32) return fail(KZGMI_ERR_ARG, "sharded verification needs an explicit shared seed");
@@ -565,14 +593,14 @@ int kzgmi_batch_partial_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slo
       s.partial_job = true;
       return 0;
     }
-    return enqueue_batch<Cv>(c, s, srs, dC, dz, dy, dpi, n, seed, index_offset, d_partial_out);
+    return enqueue_batch<Cv>(c, s, srs, dC, dz, dy, dpi, n, seed, index_offset, d_partial_out, flags);
   });
 }
 
 int kzgmi_batch_partial_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* dC, const void* dz, const void* dy,
                                const void* dpi, size_t n, uint64_t index_offset, const uint8_t* seed32,
                                void* d_partial_out) {
-  CHK(kzgmi_batch_partial_device_async(c, srs, 0, dC, dz, dy, dpi, n, index_offset, seed32, d_partial_out));
+  CHK(kzgmi_batch_partial_device_async(c, srs, 0, dC, dz, dy, dpi, n, index_offset, seed32, 0, d_partial_out));
   return kzgmi_slot_wait(c, 0, nullptr);
 }
 
@@ -607,6 +635,52 @@ int kzgmi_batch_combine_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* d
   if (!ok_out) return fail(KZGMI_ERR_ARG, "null ok_out");
   CHK(kzgmi_batch_combine_device_async(c, srs, 0, d_partials, n_parts));
   return kzgmi_slot_wait(c, 0, ok_out);
+}
+
+int kzgmi_g1_validate_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_points, size_t n, uint32_t flags) {
+  CHK(check_ctx(c));
+  if (flags & ~(KZGMI_FLAG_COMPRESSED | KZGMI_FLAG_SUBGROUP_CHECK)) return fail(KZGMI_ERR_ARG, "unknown flags");
+  if (n && !d_points) return fail(KZGMI_ERR_ARG, "null input");
+  if (n > (1u << 27)) return fail(KZGMI_ERR_ARG, "too many points (max 2^27 per call)");
+  if (n == 0) return 0;
+  Slot& s = c->slots[0];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot 0 busy: call kzgmi_slot_wait first");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    using L = Launch<Cv>;
+    CHK(s.pts.ensure(n * sizeof(Affine<Cv>)));
+    CHK(s.inf.ensure(n));
+    CHK(s.flags.ensure(16));
+    hipStream_t st = s.stream;
+    HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
+    uint32_t* err = s.flags.template as<uint32_t>() + 1;
+    if (flags & KZGMI_FLAG_COMPRESSED)
+      L::decompress_points(st, (const uint8_t*)d_points, (uint32_t)n, s.pts.template as<Affine<Cv>>(),
+                           s.inf.template as<uint8_t>(), err);
+    else
+      L::convert_points(st, (const uint8_t*)d_points, (uint32_t)n, s.pts.template as<Affine<Cv>>(),
+                        s.inf.template as<uint8_t>(), err);
+    if (flags & KZGMI_FLAG_SUBGROUP_CHECK)
+      L::subgroup_check(st, s.pts.template as<Affine<Cv>>(), s.inf.template as<uint8_t>(), (uint32_t)n, err);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
+    s.pending = true;
+    s.partial_job = true;
+    return finish_slot(c, s, nullptr);
+  });
+}
+
+int kzgmi_g1_compress_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_points, size_t n, void* d_out) {
+  CHK(check_ctx(c));
+  if (n && (!d_points || !d_out)) return fail(KZGMI_ERR_ARG, "null argument");
+  if (n > (1u << 27)) return fail(KZGMI_ERR_ARG, "too many points (max 2^27 per call)");
+  Slot& s = c->slots[0];
+  return dispatch(curve, [&](auto cv) -> int {
+    Launch<decltype(cv)>::compress_points(s.stream, (const uint8_t*)d_points, (uint32_t)n, (uint8_t*)d_out);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s.stream));
+    return 0;
+  });
 }
 
 int kzgmi_msm_partial_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dpts, const void* dsc, size_t n,

@@ -9,7 +9,7 @@
 namespace kzgmi {
 
 // device-side error codes (atomicMax into the context's error word; host maps to KZGMI_ERR_*)
-enum : uint32_t { DERR_NONE = 0, DERR_ENCODING = 1, DERR_NOT_ON_CURVE = 2, DERR_SCALAR = 3 };
+enum : uint32_t { DERR_NONE = 0, DERR_ENCODING = 1, DERR_NOT_ON_CURVE = 2, DERR_SCALAR = 3, DERR_NOT_IN_SUBGROUP = 4 };
 
 KZ_DEV void raise_err(uint32_t* err, uint32_t code) { atomicMax(err, code); }
 

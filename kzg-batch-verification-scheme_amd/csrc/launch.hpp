@@ -23,6 +23,10 @@ struct Launch {
   // ---- I/O and scalars (launch_io.hip)
   static void convert_points(hipStream_t st, const uint8_t* bytes, uint32_t n, AF* pts, uint8_t* inf, uint32_t* err);
   static void set_generator(hipStream_t st, AF* pt, uint8_t* inf);
+  static void decompress_points(hipStream_t st, const uint8_t* bytes, uint32_t n, AF* pts, uint8_t* inf,
+                                uint32_t* err);
+  static void compress_points(hipStream_t st, const uint8_t* in, uint32_t n, uint8_t* out);
+  static void subgroup_check(hipStream_t st, const AF* pts, const uint8_t* inf, uint32_t n, uint32_t* err);
   static void convert_scalars(hipStream_t st, const uint8_t* bytes, uint32_t n, uint32_t* out, uint32_t* err);
   static void convert_g2(hipStream_t st, const uint8_t* bytes, uint32_t n, G2Aff<Cv>* out, uint8_t* inf,
                          uint32_t* err);

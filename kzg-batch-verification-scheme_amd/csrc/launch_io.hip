@@ -1,5 +1,6 @@
 // Decoding / scalar-prep / encoding launchers (compiled once per curve).  Kernels: kernels.hpp.
 #include "launch.hpp"
+#include "points.hpp"
 
 namespace kzgmi {
 
@@ -10,6 +11,21 @@ void Launch<Cv>::convert_points(hipStream_t st, const uint8_t* bytes, uint32_t n
 template <class Cv>
 void Launch<Cv>::set_generator(hipStream_t st, AF* pt, uint8_t* inf) {
   k_set_generator<Cv><<<1, 1, 0, st>>>(pt, inf);
+}
+template <class Cv>
+void Launch<Cv>::decompress_points(hipStream_t st, const uint8_t* bytes, uint32_t n, AF* pts, uint8_t* inf,
+                                   uint32_t* err) {
+  if (n) k_decompress_points<Cv><<<grid_for(n, 256), 256, 0, st>>>(bytes, n, pts, inf, err);
+}
+template <class Cv>
+void Launch<Cv>::compress_points(hipStream_t st, const uint8_t* in, uint32_t n, uint8_t* out) {
+  if (n) k_compress_points<Cv><<<grid_for(n, 256), 256, 0, st>>>(in, n, out);
+}
+template <class Cv>
+void Launch<Cv>::subgroup_check(hipStream_t st, const AF* pts, const uint8_t* inf, uint32_t n, uint32_t* err) {
+  if constexpr (Cv::ID == 0) {  // BN254: cofactor 1, every curve point is in G1
+    if (n) k_subgroup_check<Cv><<<grid_for(n, 256), 256, 0, st>>>(pts, inf, n, err);
+  }
 }
 template <class Cv>
 void Launch<Cv>::convert_scalars(hipStream_t st, const uint8_t* bytes, uint32_t n, uint32_t* out, uint32_t* err) {
@@ -45,6 +61,9 @@ void Launch<Cv>::sum_partials(hipStream_t st, const XY* parts, uint32_t nparts, 
 using C_ = KZ_CURVE_T;
 template void Launch<C_>::convert_points(hipStream_t, const uint8_t*, uint32_t, Affine<C_>*, uint8_t*, uint32_t*);
 template void Launch<C_>::set_generator(hipStream_t, Affine<C_>*, uint8_t*);
+template void Launch<C_>::decompress_points(hipStream_t, const uint8_t*, uint32_t, Affine<C_>*, uint8_t*, uint32_t*);
+template void Launch<C_>::compress_points(hipStream_t, const uint8_t*, uint32_t, uint8_t*);
+template void Launch<C_>::subgroup_check(hipStream_t, const Affine<C_>*, const uint8_t*, uint32_t, uint32_t*);
 template void Launch<C_>::convert_scalars(hipStream_t, const uint8_t*, uint32_t, uint32_t*, uint32_t*);
 template void Launch<C_>::convert_g2(hipStream_t, const uint8_t*, uint32_t, G2Aff<C_>*, uint8_t*, uint32_t*);
 template size_t Launch<C_>::tpart_bytes(uint32_t);

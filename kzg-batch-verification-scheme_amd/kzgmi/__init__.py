@@ -66,6 +66,10 @@ def lib():
         "kzgmi_batch_verify": ([vp, vp, u8p, u8p, u8p, u8p, sz, u8p, ip], c.c_int),
         "kzgmi_batch_verify_device": ([vp, vp, vp, vp, vp, vp, sz, u8p, ip], c.c_int),
         "kzgmi_batch_verify_device_async": ([vp, vp, c.c_int, vp, vp, vp, vp, sz, u8p], c.c_int),
+        "kzgmi_batch_verify_ex": ([vp, vp, u8p, u8p, u8p, u8p, sz, u8p, c.c_uint32, ip], c.c_int),
+        "kzgmi_batch_verify_device_ex_async": ([vp, vp, c.c_int, vp, vp, vp, vp, sz, u8p, c.c_uint32], c.c_int),
+        "kzgmi_g1_validate_device": ([vp, c.c_int, vp, sz, c.c_uint32], c.c_int),
+        "kzgmi_g1_compress_device": ([vp, c.c_int, vp, sz, vp], c.c_int),
         "kzgmi_slot_wait": ([vp, c.c_int, ip], c.c_int),
         "kzgmi_last_combination": ([vp, u8p, u8p], c.c_int),
         "kzgmi_msm_g1": ([vp, c.c_int, u8p, u8p, sz, u8p], c.c_int),
@@ -73,7 +77,8 @@ def lib():
         "kzgmi_partial_bytes": ([c.c_int], sz),
         "kzgmi_batch_partial_device": ([vp, vp, vp, vp, vp, vp, sz, c.c_uint64, u8p, vp], c.c_int),
         "kzgmi_batch_combine_device": ([vp, vp, vp, c.c_int, ip], c.c_int),
-        "kzgmi_batch_partial_device_async": ([vp, vp, c.c_int, vp, vp, vp, vp, sz, c.c_uint64, u8p, vp], c.c_int),
+        "kzgmi_batch_partial_device_async": ([vp, vp, c.c_int, vp, vp, vp, vp, sz, c.c_uint64, u8p, c.c_uint32, vp],
+                                             c.c_int),
         "kzgmi_batch_combine_device_async": ([vp, vp, c.c_int, vp, c.c_int], c.c_int),
         "kzgmi_msm_partial_device": ([vp, c.c_int, vp, vp, sz, vp], c.c_int),
         "kzgmi_msm_combine_device": ([vp, c.c_int, vp, c.c_int, u8p], c.c_int),
@@ -98,12 +103,23 @@ def exported_symbols():
         "kzgmi_version", "kzgmi_last_error", "kzgmi_phase_names", "kzgmi_ctx_create",
         "kzgmi_ctx_destroy", "kzgmi_srs_load", "kzgmi_srs_free", "kzgmi_batch_verify",
         "kzgmi_batch_verify_device", "kzgmi_batch_verify_device_async", "kzgmi_slot_wait",
+        "kzgmi_batch_verify_ex", "kzgmi_batch_verify_device_ex_async", "kzgmi_g1_validate_device",
+        "kzgmi_g1_compress_device",
         "kzgmi_last_combination", "kzgmi_msm_g1", "kzgmi_msm_g1_device", "kzgmi_partial_bytes",
         "kzgmi_batch_partial_device", "kzgmi_batch_combine_device", "kzgmi_batch_partial_device_async",
         "kzgmi_batch_combine_device_async", "kzgmi_msm_partial_device",
         "kzgmi_msm_combine_device", "kzgmi_pairing", "kzgmi_gen_g1", "kzgmi_gen_tuples",
         "kzgmi_g2_mul", "kzgmi_probe_fpmul", "kzgmi_set_profiling", "kzgmi_get_phase_ms",
     ]
+
+
+FLAG_COMPRESSED = 1
+FLAG_SUBGROUP_CHECK = 2
+ERR_NOT_IN_SUBGROUP = -7
+
+
+def _flags(compressed: bool, subgroup_check: bool) -> int:
+    return (FLAG_COMPRESSED if compressed else 0) | (FLAG_SUBGROUP_CHECK if subgroup_check else 0)
 
 
 def _check(rc: int):
@@ -179,8 +195,11 @@ class Context:
 
     # ------------------------------------------------------------------ batch verify
     def batch_verify(self, srs: Srs, commitments, zs, ys, proofs, seed: Optional[bytes] = None,
-                     n: Optional[int] = None) -> bool:
-        g1b = 2 * FP_BYTES[srs.curve]
+                     n: Optional[int] = None, compressed: bool = False, subgroup_check: bool = False) -> bool:
+        """BASELINE.json:5 batch_verify.  compressed: C/pi are compressed G1 encodings;
+        subgroup_check: reject points outside G1 (KZGMI_ERR_NOT_IN_SUBGROUP)."""
+        flags = _flags(compressed, subgroup_check)
+        g1b = (1 if compressed else 2) * FP_BYTES[srs.curve]
         ok = ctypes.c_int(-1)
         sd = None if seed is None else bytes(seed)
         if seed is not None and len(sd) != 32:
@@ -188,6 +207,10 @@ class Context:
         if _is_device_tensor(commitments):
             if n is None:
                 n = commitments.numel() // g1b
+            if flags:
+                _check(lib().kzgmi_batch_verify_device_ex_async(self.handle, srs.handle, 0, _dptr(commitments),
+                                                                _dptr(zs), _dptr(ys), _dptr(proofs), n, sd, flags))
+                return self.wait(0)
             _check(lib().kzgmi_batch_verify_device(self.handle, srs.handle, _dptr(commitments), _dptr(zs),
                                                    _dptr(ys), _dptr(proofs), n, sd, ctypes.byref(ok)))
         else:
@@ -196,14 +219,25 @@ class Context:
                 n = len(cb) // g1b
             if len(cb) < n * g1b or len(pb) < n * g1b or len(zb) < 32 * n or len(yb) < 32 * n:
                 raise ValueError("input buffers shorter than n tuples")
-            _check(lib().kzgmi_batch_verify(self.handle, srs.handle, cb, zb, yb, pb, n, sd, ctypes.byref(ok)))
+            _check(lib().kzgmi_batch_verify_ex(self.handle, srs.handle, cb, zb, yb, pb, n, sd, flags,
+                                               ctypes.byref(ok)))
         return bool(ok.value)
 
     def batch_verify_async(self, srs: Srs, slot: int, commitments, zs, ys, proofs, n: int,
-                           seed: Optional[bytes] = None):
+                           seed: Optional[bytes] = None, compressed: bool = False, subgroup_check: bool = False):
         sd = None if seed is None else bytes(seed)
-        _check(lib().kzgmi_batch_verify_device_async(self.handle, srs.handle, int(slot), _dptr(commitments),
-                                                     _dptr(zs), _dptr(ys), _dptr(proofs), n, sd))
+        _check(lib().kzgmi_batch_verify_device_ex_async(self.handle, srs.handle, int(slot), _dptr(commitments),
+                                                        _dptr(zs), _dptr(ys), _dptr(proofs), n, sd,
+                                                        _flags(compressed, subgroup_check)))
+
+    def g1_validate(self, curve: str, points, n: int, compressed: bool = False, subgroup_check: bool = False):
+        """Raise KzgmiError unless all n device-resident G1 encodings are valid."""
+        _check(lib().kzgmi_g1_validate_device(self.handle, CURVES[curve], _dptr(points), n,
+                                              _flags(compressed, subgroup_check)))
+
+    def g1_compress(self, curve: str, points, n: int, out):
+        """Device utility: uncompressed G1 encodings -> compressed (no validation)."""
+        _check(lib().kzgmi_g1_compress_device(self.handle, CURVES[curve], _dptr(points), n, _dptr(out)))
 
     def wait(self, slot: int) -> bool:
         ok = ctypes.c_int(-1)
@@ -251,11 +285,11 @@ class Context:
         return bool(ok.value)
 
     def batch_partial_async(self, srs: Srs, slot: int, commitments, zs, ys, proofs, n: int, index_offset: int,
-                            seed: bytes, out):
+                            seed: bytes, out, compressed: bool = False, subgroup_check: bool = False):
         """Enqueue this shard's partial (A_k, B_k) on `slot`; complete with wait(slot)."""
         _check(lib().kzgmi_batch_partial_device_async(self.handle, srs.handle, int(slot), _dptr(commitments),
                                                       _dptr(zs), _dptr(ys), _dptr(proofs), n, int(index_offset),
-                                                      bytes(seed), _dptr(out)))
+                                                      bytes(seed), _flags(compressed, subgroup_check), _dptr(out)))
 
     def batch_combine_async(self, srs: Srs, slot: int, partials, n_parts: int):
         """Enqueue sum-of-partials + pairing check on `slot`; wait(slot) returns the verdict."""
@@ -337,9 +371,11 @@ def load_srs(curve: str, g2: bytes, tau_g2: bytes, ctx: Optional[Context] = None
     return (ctx or default_context()).load_srs(curve, g2, tau_g2)
 
 
-def batch_verify(commitments, zs, ys, proofs, srs: Srs, seed: Optional[bytes] = None) -> bool:
+def batch_verify(commitments, zs, ys, proofs, srs: Srs, seed: Optional[bytes] = None, compressed: bool = False,
+                 subgroup_check: bool = False) -> bool:
     """BASELINE.json:5 batch_verify(commitments, zs, ys, proofs, srs) on the GPU."""
-    return srs.ctx.batch_verify(srs, commitments, zs, ys, proofs, seed=seed)
+    return srs.ctx.batch_verify(srs, commitments, zs, ys, proofs, seed=seed, compressed=compressed,
+                                subgroup_check=subgroup_check)
 
 
 def msm_g1(curve: str, points, scalars, ctx: Optional[Context] = None) -> bytes:

@@ -180,6 +180,65 @@ static int C_(fr_decode_raw)(uint64_t* raw, const uint8_t* b) {
   return FR_(geq_mod)(raw) ? KZGO_ERR_SCALAR : 0;
 }
 
+/* ------------------------------------------------------------------ compressed G1 */
+/* BLS12-381: 48 B ZCash flags (0x80 compressed, 0x40 infinity, 0x20 larger y);
+ * BN254: 32 B gnark-crypto (top bits 0b10 smaller y, 0b11 larger y, 0b01 infinity). */
+static int C_(y_is_larger)(const FP* y) {  /* raw y > (p-1)/2 <=> 2y > p - 1 <=> 2y >= p */
+  uint64_t raw[sizeof(FP) / 8]; FP_(from_mont)(raw, y);
+  uint64_t dbl[sizeof(FP) / 8 + 1]; uint64_t c = 0;
+  for (size_t i = 0; i < sizeof(FP) / 8; ++i) { dbl[i] = (raw[i] << 1) | c; c = raw[i] >> 63; }
+  if (c) return 1;
+  for (int i = (int)(sizeof(FP) / 8) - 1; i >= 0; --i) {
+    if (dbl[i] != PRAW[i]) return dbl[i] > PRAW[i];
+  }
+  return 1;  /* 2y == p impossible (p odd) */
+}
+static int C_(g1_decode_compressed)(C_(aff)* r, const uint8_t* b) {
+  memset(r, 0, sizeof(*r));
+  uint8_t xb[FPB]; memcpy(xb, b, FPB);
+  int larger;
+  int rest = 0;
+  for (int i = 1; i < FPB; ++i) rest |= b[i];
+#if IS_BLS
+  if (!(b[0] & 0x80)) return KZGO_ERR_ENCODING;
+  if (b[0] & 0x40) { if (b[0] != 0xC0 || rest) return KZGO_ERR_ENCODING; r->inf = 1; return 0; }
+  larger = (b[0] & 0x20) != 0;
+  xb[0] &= 0x1F;
+#else
+  uint8_t m = b[0] & 0xC0;
+  if (m == 0x40) { if (b[0] != 0x40 || rest) return KZGO_ERR_ENCODING; r->inf = 1; return 0; }
+  if (m == 0x00) return KZGO_ERR_ENCODING;
+  larger = m == 0xC0;
+  xb[0] &= 0x3F;
+#endif
+  if (FP_(from_be)(&r->x, xb, FPB)) return KZGO_ERR_ENCODING;
+  FP rhs, bb, y, y2; uint64_t raw[sizeof(FP) / 8];
+  memset(raw, 0, sizeof(raw)); raw[0] = B_SMALL; FP_(to_mont)(&bb, raw);
+  FP_(sqr)(&rhs, &r->x); FP_(mul)(&rhs, &rhs, &r->x); FP_(add)(&rhs, &rhs, &bb);
+  uint64_t e[sizeof(FP) / 8]; uint64_t c = 1;  /* e = (p + 1) / 4 */
+  for (size_t i = 0; i < sizeof(FP) / 8; ++i) { uint64_t t = PRAW[i] + c; c = t < c; e[i] = t; }
+  for (size_t i = 0; i < sizeof(FP) / 8; ++i) e[i] = (e[i] >> 2) | (i + 1 < sizeof(FP) / 8 ? e[i + 1] << 62 : 0);
+  FP_(pow)(&y, &rhs, e, (int)(sizeof(FP) * 8));
+  FP_(sqr)(&y2, &y);
+  if (!FP_(eq)(&y2, &rhs)) return KZGO_ERR_NOT_ON_CURVE;
+  if (FP_(is_zero)(&y) && larger) return KZGO_ERR_ENCODING;
+  if (C_(y_is_larger)(&y) != larger) FP_(neg)(&y, &y);
+  r->y = y;
+  return 0;
+}
+static void C_(g1_encode_compressed)(uint8_t* b, const C_(aff)* a) {
+  memset(b, 0, FPB);
+#if IS_BLS
+  if (a->inf) { b[0] = 0xC0; return; }
+  FP_(to_be)(b, &a->x, FPB);
+  b[0] |= 0x80 | (C_(y_is_larger)(&a->y) ? 0x20 : 0);
+#else
+  if (a->inf) { b[0] = 0x40; return; }
+  FP_(to_be)(b, &a->x, FPB);
+  b[0] |= C_(y_is_larger)(&a->y) ? 0xC0 : 0x80;
+#endif
+}
+
 /* ------------------------------------------------------------------ scalar mul */
 static inline int C_(bit)(const uint64_t* k, int i) { return (int)((k[i >> 6] >> (i & 63)) & 1); }
 
@@ -190,6 +249,13 @@ static void C_(mul_raw)(C_(jac)* r, const C_(aff)* p, const uint64_t* k) {
     if (C_(bit)(k, i)) C_(jac_add_aff)(&acc, &acc, p);
   }
   *r = acc;
+}
+
+/* subgroup membership by definition: [r]P == O */
+static int C_(in_subgroup)(const C_(aff)* p) {
+  if (p->inf) return 1;
+  C_(jac) q; C_(mul_raw)(&q, p, RRAW);
+  return C_(jac_is_inf)(&q);
 }
 
 /* ------------------------------------------------------------------ Pippenger */

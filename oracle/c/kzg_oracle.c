@@ -151,7 +151,11 @@ static const uint64_t BLS_LOOPW[2] = {BLS_LOOP, 0};
 #define FROB_GY1 BLS_FROB_GY1
 #define B2_0 BLS_B2_0
 #define B2_1 BLS_B2_1
+#define PRAW BLS_P_MOD
+#define RRAW BLS_FR_MOD
 #include "curve_tmpl.h"
+#undef PRAW
+#undef RRAW
 #undef FP
 #undef FP_
 #undef FR
@@ -231,6 +235,8 @@ static const uint64_t BLS_LOOPW[2] = {BLS_LOOP, 0};
 #define FROB_GY1 BN_FROB_GY1
 #define B2_0 BN_B2_0
 #define B2_1 BN_B2_1
+#define PRAW BN_P_MOD
+#define RRAW BN_FR_MOD
 #include "curve_tmpl.h"
 
 /* ================================================================== C API (ctypes) */
@@ -312,6 +318,52 @@ int kzgo_msm_g1(int curve, const uint8_t* pts, const uint8_t* scalars, size_t n,
   }
 DEF_MULGEN(bls, fr_bls)
 DEF_MULGEN(bn, fr_bn)
+
+/* Compressed encodings and the subgroup definition (SURVEY.md 8f item 1 oracle). */
+#define DEF_COMPRESSED(C)                                                                    \
+  static int C##_decompress_api(const uint8_t* in, size_t n, uint8_t* out) {                \
+    int err = 0;                                                                             \
+    for (size_t i = 0; i < n; ++i) {                                                         \
+      C##_aff a; int e = C##_g1_decode_compressed(&a, in + i * (C##_FPB_));                  \
+      if (e) { if (!err) err = e; memset(&a, 0, sizeof(a)); a.inf = 1; }                     \
+      C##_g1_encode(out + i * 2 * (C##_FPB_), &a);                                           \
+    }                                                                                        \
+    return err;                                                                              \
+  }                                                                                          \
+  static int C##_compress_api(const uint8_t* in, size_t n, uint8_t* out) {                  \
+    for (size_t i = 0; i < n; ++i) {                                                         \
+      C##_aff a; int e = C##_g1_decode(&a, in + i * 2 * (C##_FPB_));                         \
+      if (e) return e;                                                                       \
+      C##_g1_encode_compressed(out + i * (C##_FPB_), &a);                                    \
+    }                                                                                        \
+    return 0;                                                                                \
+  }                                                                                          \
+  static int C##_subgroup_api(const uint8_t* in, size_t n, int* ok) {                       \
+    int err = 0, good = 1;                                                                   \
+    _Pragma("omp parallel for num_threads(kzgo_threads()) schedule(dynamic, 4) reduction(&:good)") \
+    for (size_t i = 0; i < n; ++i) {                                                         \
+      C##_aff a; int e = C##_g1_decode(&a, in + i * 2 * (C##_FPB_));                         \
+      if (e) { err = e; continue; }                                                          \
+      good &= C##_in_subgroup(&a);                                                           \
+    }                                                                                        \
+    *ok = good;                                                                              \
+    return err;                                                                              \
+  }
+DEF_COMPRESSED(bls)
+DEF_COMPRESSED(bn)
+
+int kzgo_g1_decompress(int curve, const uint8_t* in, size_t n, uint8_t* out) {
+  if (n && (!in || !out)) return KZGO_ERR_ARG;
+  return CURVE_DISPATCH(curve, bls_decompress_api(in, n, out), bn_decompress_api(in, n, out));
+}
+int kzgo_g1_compress(int curve, const uint8_t* in, size_t n, uint8_t* out) {
+  if (n && (!in || !out)) return KZGO_ERR_ARG;
+  return CURVE_DISPATCH(curve, bls_compress_api(in, n, out), bn_compress_api(in, n, out));
+}
+int kzgo_g1_subgroup_check(int curve, const uint8_t* in, size_t n, int* ok) {
+  if (!ok || (n && !in)) return KZGO_ERR_ARG;
+  return CURVE_DISPATCH(curve, bls_subgroup_api(in, n, ok), bn_subgroup_api(in, n, ok));
+}
 
 int kzgo_g1_mul_gen(int curve, const uint8_t* scalars, size_t n, uint8_t* out) {
   if (n && (!scalars || !out)) return KZGO_ERR_ARG;

@@ -37,6 +37,9 @@ def lib():
         L.kzgo_pairing_check.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p, c.POINTER(c.c_int)]
         L.kzgo_msm_g1.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_size_t, c.c_char_p]
         L.kzgo_g1_mul_gen.argtypes = [c.c_int, c.c_char_p, c.c_size_t, c.c_char_p]
+        L.kzgo_g1_decompress.argtypes = [c.c_int, c.c_char_p, c.c_size_t, c.c_char_p]
+        L.kzgo_g1_compress.argtypes = [c.c_int, c.c_char_p, c.c_size_t, c.c_char_p]
+        L.kzgo_g1_subgroup_check.argtypes = [c.c_int, c.c_char_p, c.c_size_t, c.POINTER(c.c_int)]
         L.kzgo_pairing.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p]
         L.kzgo_g2_mul.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p]
         L.kzgo_randomizer_bytes.argtypes = [c.c_char_p, c.c_uint64, c.c_char_p]
@@ -92,6 +95,26 @@ def batch_combination(curve, commitments, zs, ys, proofs, n, offset, g2, tau_g2,
 def pairing_check(curve, A: bytes, B: bytes, g2: bytes, tau_g2: bytes) -> bool:
     ok = ctypes.c_int(-1)
     _check(lib().kzgo_pairing_check(CURVE_IDS[curve], A, B, g2, tau_g2, ctypes.byref(ok)))
+    return bool(ok.value)
+
+
+def g1_decompress(curve, data: bytes, n: int):
+    """(error code of the first invalid encoding or 0, n uncompressed encodings)."""
+    out = ctypes.create_string_buffer(n * 2 * FP_BYTES[curve])
+    rc = lib().kzgo_g1_decompress(CURVE_IDS[curve], data, n, out)
+    return rc, out.raw
+
+
+def g1_compress(curve, points: bytes, n: int) -> bytes:
+    out = ctypes.create_string_buffer(n * FP_BYTES[curve])
+    _check(lib().kzgo_g1_compress(CURVE_IDS[curve], points, n, out))
+    return out.raw
+
+
+def g1_subgroup_check(curve, points: bytes, n: int) -> bool:
+    """True iff every (uncompressed, valid) point satisfies [r]P == O."""
+    ok = ctypes.c_int(-1)
+    _check(lib().kzgo_g1_subgroup_check(CURVE_IDS[curve], points, n, ctypes.byref(ok)))
     return bool(ok.value)
 
 

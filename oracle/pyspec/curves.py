@@ -232,6 +232,24 @@ def g1_mul(P: G1Point, k: int, C: CurveParams) -> G1Point:
     return _jac_to_affine(R, p)
 
 
+def g1_mul_unreduced(P: G1Point, k: int, C: CurveParams) -> G1Point:
+    """[k]P without reducing k mod r (for points that may lie outside the order-r subgroup)."""
+    if P is None or k == 0:
+        return None
+    p = C.p
+    R = (1, 1, 0)
+    for bit in bin(k)[2:]:
+        R = _jac_dbl(R, p)
+        if bit == "1":
+            R = _jac_add_affine(R, P, p)
+    return _jac_to_affine(R, p)
+
+
+def g1_in_subgroup(P: G1Point, C: CurveParams) -> bool:
+    """Definition: [r]P == O (the fast endomorphism test on the GPU is checked against this)."""
+    return g1_mul_unreduced(P, C.r, C) is None
+
+
 def g1_msm(points, scalars, C: CurveParams) -> G1Point:
     """Naive sum of k_i * P_i (definition of the MSM)."""
     acc = None

@@ -89,6 +89,62 @@ def g1_from_bytes(b: bytes, C: CurveParams) -> G1Point:
     return P
 
 
+def g1_to_bytes_compressed(P: G1Point, C: CurveParams) -> bytes:
+    """BLS12-381: 48 B ZCash (0x80 compressed | 0x40 infinity | 0x20 larger y).
+    BN254: 32 B gnark-crypto (top bits 0b10 smaller y, 0b11 larger y, 0b01 infinity)."""
+    n = C.fp_bytes
+    if C.name == "bls12_381":
+        if P is None:
+            return bytes([0xC0]) + bytes(n - 1)
+        b = bytearray(P[0].to_bytes(n, "big"))
+        b[0] |= 0x80 | (0x20 if P[1] > (C.p - 1) // 2 else 0)
+        return bytes(b)
+    if P is None:
+        return bytes([0x40]) + bytes(n - 1)
+    b = bytearray(P[0].to_bytes(n, "big"))
+    b[0] |= 0xC0 if P[1] > (C.p - 1) // 2 else 0x80
+    return bytes(b)
+
+
+def g1_from_bytes_compressed(b: bytes, C: CurveParams) -> G1Point:
+    """Inverse of g1_to_bytes_compressed; ValueError on any invalid encoding, 'not on curve'
+    when x^3 + b has no square root."""
+    n = C.fp_bytes
+    if len(b) != n:
+        raise ValueError("bad length")
+    b0 = b[0]
+    if C.name == "bls12_381":
+        if not b0 & 0x80:
+            raise ValueError("compression flag missing")
+        if b0 & 0x40:
+            if b0 != 0xC0 or any(b[1:]):
+                raise ValueError("bad infinity encoding")
+            return None
+        larger = bool(b0 & 0x20)
+        x = int.from_bytes(bytes([b0 & 0x1F]) + b[1:], "big")
+    else:
+        m = b0 & 0xC0
+        if m == 0x40:
+            if b0 != 0x40 or any(b[1:]):
+                raise ValueError("bad infinity encoding")
+            return None
+        if m == 0x00:
+            raise ValueError("not a compressed encoding")
+        larger = m == 0xC0
+        x = int.from_bytes(bytes([b0 & 0x3F]) + b[1:], "big")
+    if x >= C.p:
+        raise ValueError("non-canonical coordinate")
+    rhs = (x * x * x + C.b) % C.p
+    y = pow(rhs, (C.p + 1) // 4, C.p)
+    if y * y % C.p != rhs:
+        raise ValueError("point not on curve")
+    if y == 0 and larger:
+        raise ValueError("bad sign flag")
+    if (y > (C.p - 1) // 2) != larger:
+        y = C.p - y
+    return (x, y)
+
+
 def g2_to_bytes(Q: G2Point, C: CurveParams) -> bytes:
     n = C.fp_bytes
     if Q is None:

@@ -118,3 +118,43 @@ def test_sharded_msm_equals_unsharded():
         part = O.msm_g1(curve, pts[lo * 96:hi * 96], scs[lo * 32:hi * 32], hi - lo)
         acc = pc.g1_add(acc, pk.g1_from_bytes(part, C), C)
     assert acc == full
+
+
+# ---------------------------------------------------------------- SURVEY.md 8f item 1
+@pytest.mark.parametrize("curve", CURVES)
+def test_compressed_roundtrip_oracle_vs_spec(curve, golden):
+    """Compressed encodings: C oracle == Python spec, both directions, on golden points."""
+    C = pc.CURVES[curve]
+    g = golden("%s_batch_n16.json" % curve)
+    pts = bytes.fromhex(g["commitments"]) + bytes.fromhex(g["proofs"])
+    n = len(pts) // (2 * C.fp_bytes)
+    comp = O.g1_compress(curve, pts, n)
+    g1b, fb = 2 * C.fp_bytes, C.fp_bytes
+    assert comp == b"".join(pk.g1_to_bytes_compressed(pk.g1_from_bytes(pts[i * g1b:(i + 1) * g1b], C), C)
+                            for i in range(n))
+    rc, back = O.g1_decompress(curve, comp, n)
+    assert rc == 0 and back == pts
+    for i in range(n):
+        assert pk.g1_from_bytes_compressed(comp[i * fb:(i + 1) * fb], C) == pk.g1_from_bytes(pts[i * g1b:(i + 1) * g1b], C)
+    inf = pk.g1_to_bytes_compressed(None, C)
+    assert O.g1_decompress(curve, inf, 1) == (0, pk.g1_to_bytes(None, C))
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_invalid_compressed(curve):
+    from pointcases import invalid_compressed
+    C = pc.CURVES[curve]
+    for enc, want in invalid_compressed(C):
+        rc, _ = O.g1_decompress(curve, enc, 1)
+        assert rc == want, (enc.hex(), rc, want)
+        with pytest.raises(ValueError):
+            pk.g1_from_bytes_compressed(enc, C)
+
+
+def test_subgroup_definition():
+    """Oracle subgroup check ([r]P == O) on members, random non-members and small-order points."""
+    from pointcases import subgroup_cases
+    C = pc.BLS12_381
+    for P, member in subgroup_cases():
+        assert O.g1_subgroup_check("bls12_381", pk.g1_to_bytes(P, C), 1) is member
+        assert pc.g1_in_subgroup(P, C) is member
