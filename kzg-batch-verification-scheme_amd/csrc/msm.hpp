@@ -22,7 +22,7 @@ namespace kzgmi {
 
 constexpr int WBITS = 16;                      // window width c
 constexpr int NBUCKETS = 1 << (WBITS - 1);     // signed digits: |d| in [1, 2^15]
-constexpr int ACC_CHUNK = 32;                  // entries per accumulation thread
+constexpr int ACC_CHUNK = 64;                  // entries per accumulation thread
 constexpr int SEG = 16;                        // buckets per reduction segment
 constexpr int MAX_CLASSES = 4;
 
