@@ -52,6 +52,14 @@ typedef enum { KZGMI_BLS12_381 = 0, KZGMI_BN254 = 1 } kzgmi_curve;
 #define KZGMI_FLAG_COMPRESSED 1u     /* commitments/proofs are compressed G1 encodings */
 #define KZGMI_FLAG_SUBGROUP_CHECK 2u /* reject points outside the order-r subgroup (BLS12-381;
                                         BN254 G1 has cofactor 1, the flag is a no-op there) */
+#define KZGMI_FLAG_POWERS 4u         /* r_i = r^i with r = int_be(seed32) < r supplied by the caller
+                                        (e.g. the EIP-4844 verify_kzg_proof_batch challenge) */
+#define KZGMI_FLAG_FIAT_SHAMIR 8u    /* r_i = r^i with r derived on the GPU from the inputs:
+                                        leaf_i = SHA256("KZGMI_FS_LEAF_V1" || be64(i) || C_i || pi_i
+                                        || z_i || y_i) (points compressed), binary Merkle root over
+                                        max(4096, next_pow2(n)) zero-padded leaf slots,
+                                        r = int_be(SHA256("KZGMI_FS_ROOT_V1" || be64(n) || root))
+                                        mod r (1 if 0); seed32 is ignored */
 
 typedef struct kzgmi_ctx kzgmi_ctx; /* one GPU, its streams and workspaces */
 typedef struct kzgmi_srs kzgmi_srs; /* {G1, [1]_2, [tau]_2} + precomputed Miller lines */
@@ -103,6 +111,21 @@ int kzgmi_batch_verify_device_ex_async(kzgmi_ctx* ctx, const kzgmi_srs* srs, int
                                        const void* d_commitments, const void* d_zs,
                                        const void* d_ys, const void* d_proofs, size_t n,
                                        const uint8_t* seed32, uint32_t flags);
+
+/* Fiat-Shamir challenge of KZGMI_FLAG_FIAT_SHAMIR for a device-resident batch (flags:
+ * KZGMI_FLAG_COMPRESSED): r as 32 big-endian bytes. */
+int kzgmi_fs_challenge_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_commitments,
+                              const void* d_zs, const void* d_ys, const void* d_proofs, size_t n,
+                              uint32_t flags, uint8_t* r_out);
+/* Multi-GPU form: a shard [index_offset, index_offset + n) with index_offset % 4096 == 0
+ * writes its ceil(n / 4096) subtree roots (32 B each) to d_out; gather all shards' roots in
+ * order and derive r with kzgmi_fs_challenge_from_digests_device, then verify each shard
+ * with kzgmi_batch_partial_device_async(..., KZGMI_FLAG_POWERS, seed32 = r). */
+int kzgmi_fs_chunk_digests_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_commitments,
+                                  const void* d_zs, const void* d_ys, const void* d_proofs, size_t n,
+                                  uint64_t index_offset, uint32_t flags, void* d_out);
+int kzgmi_fs_challenge_from_digests_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_digests,
+                                           size_t nchunks, uint64_t n_total, uint8_t* r_out);
 
 /* Validate n device-resident G1 encodings (flags: KZGMI_FLAG_COMPRESSED,
  * KZGMI_FLAG_SUBGROUP_CHECK): 0 if all are valid, else the first error class found. */

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <algorithm>
 #include <vector>
 
 using namespace kzgmi;
@@ -66,6 +67,7 @@ struct Slot {
   hipStream_t stream = nullptr;
   DevBuf pts, inf, scal_r, scal_s, scal_t, tpart, cnt, off, coarse, ent, total, sval, skey;
   DevBuf buckets, pfirst, plast, R, U, scratch, winsum, res, flags, stage, outb;
+  DevBuf fs_leaves, fs_tmp, fs_top, pow, chal;  // Fiat-Shamir / powers-of-r randomisers
   int* host_flags = nullptr;  // pinned: [ok, err]
   hipEvent_t ev[kNumPhases + 1] = {};
   bool ev_used[kNumPhases + 1] = {};
@@ -85,6 +87,7 @@ struct kzgmi_ctx {
   DevBuf table[2], table_base[2];
   bool table_ready[2] = {false, false};
   DevBuf lines_tmp, tmp;
+  std::vector<kzgmi_srs*> srs_list;  // live SRS objects: detached (device memory freed) on destroy
 };
 
 struct kzgmi_srs {
@@ -191,6 +194,49 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl, uint32_t nsets, size
   return 0;
 }
 
+// ------------------------------------------------------------------------------ Fiat-Shamir
+constexpr uint32_t kAllFlags = KZGMI_FLAG_COMPRESSED | KZGMI_FLAG_SUBGROUP_CHECK | KZGMI_FLAG_POWERS |
+                               KZGMI_FLAG_FIAT_SHAMIR;
+
+uint32_t next_pow2(uint32_t x) {
+  uint32_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// 4096-leaf subtree roots of tuples [0, n) (global indices offset + i) -> returned device pointer
+template <class Cv>
+int enqueue_fs_digests(Slot& s, const void* dC, const void* dpi, const void* dz, const void* dy, size_t n,
+                       uint64_t offset, bool compressed, const uint32_t** digests_out) {
+  using L = Launch<Cv>;
+  const uint32_t nch = (uint32_t)((n + FS_CHUNK - 1) / FS_CHUNK);
+  const size_t slots = (size_t)nch * FS_CHUNK;
+  CHK(s.fs_leaves.ensure(slots * 32));
+  CHK(s.fs_tmp.ensure(slots * 24 + 64));
+  HIPCHK(hipMemsetAsync(s.fs_leaves.p, 0, slots * 32, s.stream));
+  L::fs_leaves(s.stream, (const uint8_t*)dC, (const uint8_t*)dpi, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n,
+               offset, compressed, s.fs_leaves.template as<uint32_t>());
+  *digests_out = L::fs_reduce(s.stream, s.fs_leaves.template as<uint32_t>(), (uint32_t)slots, nch,
+                              s.fs_tmp.template as<uint32_t>());
+  return 0;
+}
+
+// chunk digests (device) -> root -> r and its power table in s.pow, r (BE words) in s.chal
+template <class Cv>
+int enqueue_fs_challenge(Slot& s, const uint32_t* digests, uint32_t nch, uint64_t n_total) {
+  using L = Launch<Cv>;
+  const uint32_t p2 = next_pow2(nch);
+  CHK(s.fs_top.ensure((size_t)p2 * 32 * 2 + 64));
+  CHK(s.pow.ensure(FS_POW_BITS * sizeof(Fp<typename Cv::FrP>)));
+  CHK(s.chal.ensure(32));
+  uint32_t* top = s.fs_top.template as<uint32_t>();
+  HIPCHK(hipMemcpyAsync(top, digests, (size_t)nch * 32, hipMemcpyDeviceToDevice, s.stream));
+  L::fs_pad(s.stream, top, nch, p2);
+  const uint32_t* root = L::fs_reduce(s.stream, top, p2, 1, top + 8 * (size_t)p2);
+  L::fs_challenge(s.stream, root, n_total, s.pow.p, s.chal.template as<uint32_t>());
+  return 0;
+}
+
 // ------------------------------------------------------------------------------ batch
 template <class Cv>
 int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, const void* dz, const void* dy,
@@ -202,7 +248,8 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   using L = Launch<Cv>;
   CHK(s.pts.ensure(npts * sizeof(Affine<Cv>)));
   CHK(s.inf.ensure(npts));
-  CHK(s.scal_r.ensure(n * 16));
+  const bool powers = (flags & (KZGMI_FLAG_POWERS | KZGMI_FLAG_FIAT_SHAMIR)) != 0;
+  CHK(s.scal_r.ensure(n * (powers ? 32 : 16)));
   CHK(s.scal_s.ensure(n * 32));
   CHK(s.scal_t.ensure(32));
   CHK(s.tpart.ensure(L::tpart_bytes((uint32_t)n)));
@@ -223,19 +270,40 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   if (flags & KZGMI_FLAG_SUBGROUP_CHECK) L::subgroup_check(st, pts, inf, (uint32_t)(2 * n), err);
   L::set_generator(st, pts + 2 * n, inf + 2 * n);
   mark(c, s, PH_CONVERT + 1);
-  L::scalar_prep(st, seed, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n, s.scal_r.template as<uint32_t>(),
-                 s.scal_s.template as<uint32_t>(), s.tpart.p, s.scal_t.template as<uint32_t>(), err);
+  if (flags & KZGMI_FLAG_FIAT_SHAMIR) {  // r from the transcript of this (whole) batch
+    const uint32_t* digests = nullptr;
+    CHK(enqueue_fs_digests<Cv>(s, dC, dpi, dz, dy, n, 0, (flags & KZGMI_FLAG_COMPRESSED) != 0, &digests));
+    CHK(enqueue_fs_challenge<Cv>(s, digests, (uint32_t)((n + FS_CHUNK - 1) / FS_CHUNK), n));
+  } else if (flags & KZGMI_FLAG_POWERS) {  // r supplied by the caller in place of the seed
+    CHK(s.pow.ensure(FS_POW_BITS * sizeof(FrF)));
+    L::pow_table(st, seed, s.pow.p, err);
+  }
+  if (powers)
+    L::scalar_prep_pow(st, s.pow.p, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n,
+                       s.scal_r.template as<uint32_t>(), s.scal_s.template as<uint32_t>(), s.tpart.p,
+                       s.scal_t.template as<uint32_t>(), err);
+  else
+    L::scalar_prep(st, seed, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n,
+                   s.scal_r.template as<uint32_t>(), s.scal_s.template as<uint32_t>(), s.tpart.p,
+                   s.scal_t.template as<uint32_t>(), err);
   mark(c, s, PH_SCALARS + 1);
   TermList tl{};
   const uint32_t nn = (uint32_t)n;
-  tl.c[0] = {nn, 0, 4, 8, 0, 4, s.scal_r.template as<uint32_t>()};           // MSM#0: r_i pi_i
-  tl.c[1] = {nn, nn, 4, 8, 8, 4, s.scal_r.template as<uint32_t>()};          // MSM#1: r_i C_i
-  tl.c[2] = {nn, 0, 8, 16, 8, 8, s.scal_s.template as<uint32_t>()};          //        s_i pi_i
-  tl.c[3] = {1, 2 * nn, 8, 16, 8, 0, s.scal_t.template as<uint32_t>()};      //        -t G1
+  if (!powers) {  // 127-bit r_i: MSM#0 in 8 windows (sets 0..7), MSM#1 in 16 (sets 8..23)
+    tl.c[0] = {nn, 0, 4, 8, 0, 4, s.scal_r.template as<uint32_t>()};          // MSM#0: r_i pi_i
+    tl.c[1] = {nn, nn, 4, 8, 8, 4, s.scal_r.template as<uint32_t>()};         // MSM#1: r_i C_i
+    tl.c[2] = {nn, 0, 8, 16, 8, 8, s.scal_s.template as<uint32_t>()};         //        s_i pi_i
+    tl.c[3] = {1, 2 * nn, 8, 16, 8, 0, s.scal_t.template as<uint32_t>()};     //        -t G1
+  } else {        // r_i = r^i, full Fr: both MSMs in 16 windows (sets 0..15, 16..31)
+    tl.c[0] = {nn, 0, 8, 16, 0, 8, s.scal_r.template as<uint32_t>()};
+    tl.c[1] = {nn, nn, 8, 16, 16, 8, s.scal_r.template as<uint32_t>()};
+    tl.c[2] = {nn, 0, 8, 16, 16, 8, s.scal_s.template as<uint32_t>()};
+    tl.c[3] = {1, 2 * nn, 8, 16, 16, 0, s.scal_t.template as<uint32_t>()};
+  }
   tl.nclass = 4;
   tl.total = 3 * nn + 1;
-  MsmWindows mw{2, {0, 8}, {8, 16}};
-  CHK(run_msm_core<Cv>(c, s, tl, 24, (size_t)32 * n + 16, mw));
+  const MsmWindows mw = powers ? MsmWindows{2, {0, 16}, {16, 16}} : MsmWindows{2, {0, 8}, {8, 16}};
+  CHK(run_msm_core<Cv>(c, s, tl, powers ? 32 : 24, (size_t)(powers ? 48 : 32) * n + 16, mw));
   if (d_partial_out) {
     HIPCHK(hipMemcpyAsync(d_partial_out, s.res.p, 2 * sizeof(XY), hipMemcpyDeviceToDevice, st));
   } else {
@@ -326,7 +394,8 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     DevBuf* bufs[] = {&s.pts, &s.inf, &s.scal_r, &s.scal_s, &s.scal_t, &s.tpart, &s.cnt, &s.off, &s.coarse, &s.ent,
                       &s.total, &s.sval, &s.skey, &s.buckets, &s.pfirst, &s.plast, &s.R, &s.U, &s.scratch,
-                      &s.winsum, &s.res, &s.flags, &s.stage, &s.outb};
+                      &s.winsum, &s.res, &s.flags, &s.stage, &s.outb, &s.fs_leaves, &s.fs_tmp,
+                      &s.fs_top, &s.pow, &s.chal};
     for (DevBuf* b : bufs) b->release();
     for (auto& e : s.ev)
       if (e) (void)hipEventDestroy(e);
@@ -336,6 +405,12 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
   for (int k = 0; k < 2; ++k) { c->table[k].release(); c->table_base[k].release(); }
   c->lines_tmp.release();
   c->tmp.release();
+  for (kzgmi_srs* srs : c->srs_list) {  // detach: later kzgmi_srs_free() only deletes the struct
+    srs->lines.release();
+    srs->q.release();
+    srs->q_inf.release();
+    srs->ctx = nullptr;
+  }
   delete c;
 }
 
@@ -379,6 +454,7 @@ int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g2, const uin
       kzgmi_srs_free(srs);
       return e;
     }
+    c->srs_list.push_back(srs);
     *out = srs;
     return 0;
   });
@@ -386,11 +462,15 @@ int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g2, const uin
 
 void kzgmi_srs_free(kzgmi_srs* srs) {
   if (!srs) return;
-  if (srs->ctx) (void)hipSetDevice(srs->ctx->device);
-  srs->lines.release();
-  srs->q.release();
-  srs->q_inf.release();
-  delete srs;
+  if (kzgmi_ctx* c = srs->ctx) {  // still attached: free its device memory on its device
+    (void)hipSetDevice(c->device);
+    auto& v = c->srs_list;
+    v.erase(std::remove(v.begin(), v.end(), srs), v.end());
+    srs->lines.release();
+    srs->q.release();
+    srs->q_inf.release();
+  }
+  delete srs;  // a detached SRS (its context already destroyed) owns no device memory
 }
 
 int kzgmi_batch_verify_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const void* dC, const void* dz,
@@ -401,7 +481,10 @@ int kzgmi_batch_verify_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot
 int kzgmi_batch_verify_device_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const void* dC, const void* dz,
                                        const void* dy, const void* dpi, size_t n, const uint8_t* seed32,
                                        uint32_t flags) {
-  if (flags & ~(KZGMI_FLAG_COMPRESSED | KZGMI_FLAG_SUBGROUP_CHECK)) return fail(KZGMI_ERR_ARG, "unknown flags");
+  if (flags & ~kAllFlags) return fail(KZGMI_ERR_ARG, "unknown flags");
+  if ((flags & KZGMI_FLAG_POWERS) && (flags & KZGMI_FLAG_FIAT_SHAMIR))
+    return fail(KZGMI_ERR_ARG, "KZGMI_FLAG_POWERS and KZGMI_FLAG_FIAT_SHAMIR are exclusive");
+  if ((flags & KZGMI_FLAG_POWERS) && !seed32) return fail(KZGMI_ERR_ARG, "KZGMI_FLAG_POWERS needs r in seed32");
   CHK(check_ctx(c, slot));
   if (!srs || srs->ctx != c) return fail(KZGMI_ERR_ARG, "srs does not belong to this context");
   if (n && (!dC || !dz || !dy || !dpi)) return fail(KZGMI_ERR_ARG, "null input");
@@ -572,7 +655,9 @@ size_t kzgmi_partial_bytes(kzgmi_curve curve) {
 int kzgmi_batch_partial_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const void* dC, const void* dz,
                                      const void* dy, const void* dpi, size_t n, uint64_t index_offset,
                                      const uint8_t* seed32, uint32_t flags, void* d_partial_out) {
-  if (flags & ~(KZGMI_FLAG_COMPRESSED | KZGMI_FLAG_SUBGROUP_CHECK)) return fail(KZGMI_ERR_ARG, "unknown flags");
+  if (flags & ~kAllFlags) return fail(KZGMI_ERR_ARG, "unknown flags");
+  if (flags & KZGMI_FLAG_FIAT_SHAMIR)
+    return fail(KZGMI_ERR_ARG, "shards take r via KZGMI_FLAG_POWERS (see kzgmi_fs_challenge_from_digests_device)");
   CHK(check_ctx(c, slot));
   if (!srs || srs->ctx != c || !d_partial_out) return fail(KZGMI_ERR_ARG, "bad argument");
   if (!seed32) return fail(KZGMI_ERR_ARG, "sharded verification needs an explicit shared seed");
@@ -667,6 +752,68 @@ int kzgmi_g1_validate_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_poin
     s.pending = true;
     s.partial_job = true;
     return finish_slot(c, s, nullptr);
+  });
+}
+
+int kzgmi_fs_chunk_digests_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dC, const void* dz, const void* dy,
+                                  const void* dpi, size_t n, uint64_t index_offset, uint32_t flags, void* d_out) {
+  CHK(check_ctx(c));
+  if (!d_out || (n && (!dC || !dz || !dy || !dpi)) || n == 0) return fail(KZGMI_ERR_ARG, "bad argument");
+  if (index_offset % FS_CHUNK) return fail(KZGMI_ERR_ARG, "index_offset must be a multiple of 4096");
+  if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "too many tuples (max 2^26 per call)");
+  Slot& s = c->slots[0];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot 0 busy: call kzgmi_slot_wait first");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    const uint32_t* dg = nullptr;
+    CHK(enqueue_fs_digests<Cv>(s, dC, dpi, dz, dy, n, index_offset, (flags & KZGMI_FLAG_COMPRESSED) != 0, &dg));
+    const size_t nch = (n + FS_CHUNK - 1) / FS_CHUNK;
+    HIPCHK(hipMemcpyAsync(d_out, dg, nch * 32, hipMemcpyDeviceToDevice, s.stream));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s.stream));
+    return 0;
+  });
+}
+
+int kzgmi_fs_challenge_from_digests_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_digests, size_t nchunks,
+                                           uint64_t n_total, uint8_t* r_out) {
+  CHK(check_ctx(c));
+  if (!d_digests || !r_out || nchunks == 0 || nchunks > (1u << 22)) return fail(KZGMI_ERR_ARG, "bad argument");
+  if ((n_total + FS_CHUNK - 1) / FS_CHUNK != nchunks) return fail(KZGMI_ERR_ARG, "nchunks != ceil(n_total / 4096)");
+  Slot& s = c->slots[0];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot 0 busy: call kzgmi_slot_wait first");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    CHK(enqueue_fs_challenge<Cv>(s, (const uint32_t*)d_digests, (uint32_t)nchunks, n_total));
+    uint32_t w[8];
+    HIPCHK(hipMemcpyAsync(w, s.chal.p, 32, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s.stream));
+    for (int k = 0; k < 8; ++k)
+      for (int b = 0; b < 4; ++b) r_out[4 * k + b] = (uint8_t)(w[k] >> (24 - 8 * b));
+    return 0;
+  });
+}
+
+int kzgmi_fs_challenge_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dC, const void* dz, const void* dy,
+                              const void* dpi, size_t n, uint32_t flags, uint8_t* r_out) {
+  CHK(check_ctx(c));
+  if (!r_out || n == 0 || !dC || !dz || !dy || !dpi) return fail(KZGMI_ERR_ARG, "bad argument");
+  if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "too many tuples (max 2^26 per call)");
+  Slot& s = c->slots[0];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot 0 busy: call kzgmi_slot_wait first");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    const uint32_t* dg = nullptr;
+    CHK(enqueue_fs_digests<Cv>(s, dC, dpi, dz, dy, n, 0, (flags & KZGMI_FLAG_COMPRESSED) != 0, &dg));
+    CHK(enqueue_fs_challenge<Cv>(s, dg, (uint32_t)((n + FS_CHUNK - 1) / FS_CHUNK), n));
+    uint32_t w[8];
+    HIPCHK(hipMemcpyAsync(w, s.chal.p, 32, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s.stream));
+    for (int k = 0; k < 8; ++k)
+      for (int b = 0; b < 4; ++b) r_out[4 * k + b] = (uint8_t)(w[k] >> (24 - 8 * b));
+    return 0;
   });
 }
 

@@ -13,6 +13,10 @@ enum : uint32_t { DERR_NONE = 0, DERR_ENCODING = 1, DERR_NOT_ON_CURVE = 2, DERR_
 
 KZ_DEV void raise_err(uint32_t* err, uint32_t code) { atomicMax(err, code); }
 
+// Fiat-Shamir transcript geometry (fs.hpp)
+constexpr uint32_t FS_CHUNK = 4096;  // leaves per shard-alignment subtree
+constexpr int FS_POW_BITS = 32;      // r^(2^k), k < 32: any global index < 2^32
+
 // ---------------------------------------------------------------------------- SHA-256
 __constant__ static const uint32_t kSha256K[64] = {
     0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
@@ -26,13 +30,18 @@ __constant__ static const uint32_t kSha256K[64] = {
 
 KZ_DEV uint32_t ror32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
-// One compression of a single padded block given as 16 big-endian words.
-KZ_DEV void sha256_one_block(const uint32_t (&blk)[16], uint32_t (&h)[8]) {
+KZ_DEV void sha256_init(uint32_t (&h)[8]) {
+  h[0] = 0x6a09e667; h[1] = 0xbb67ae85; h[2] = 0x3c6ef372; h[3] = 0xa54ff53a;
+  h[4] = 0x510e527f; h[5] = 0x9b05688c; h[6] = 0x1f83d9ab; h[7] = 0x5be0cd19;
+}
+
+// One compression of a block given as 16 big-endian words into the chaining state h.
+KZ_DEV void sha256_compress(const uint32_t (&blk)[16], uint32_t (&h)[8]) {
   uint32_t w[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) w[i] = blk[i];
-  uint32_t a = 0x6a09e667, b = 0xbb67ae85, c = 0x3c6ef372, d = 0xa54ff53a;
-  uint32_t e = 0x510e527f, f = 0x9b05688c, g = 0x1f83d9ab, hh = 0x5be0cd19;
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
+  uint32_t e = h[4], f = h[5], g = h[6], hh = h[7];
 #pragma unroll
   for (int i = 0; i < 64; ++i) {
     uint32_t wi;
@@ -53,8 +62,33 @@ KZ_DEV void sha256_one_block(const uint32_t (&blk)[16], uint32_t (&h)[8]) {
     uint32_t t2 = S0 + mj;
     hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
   }
-  h[0] = a + 0x6a09e667; h[1] = b + 0xbb67ae85; h[2] = c + 0x3c6ef372; h[3] = d + 0xa54ff53a;
-  h[4] = e + 0x510e527f; h[5] = f + 0x9b05688c; h[6] = g + 0x1f83d9ab; h[7] = hh + 0x5be0cd19;
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d;
+  h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+// One compression of a single padded block (the whole message fits one block).
+KZ_DEV void sha256_one_block(const uint32_t (&blk)[16], uint32_t (&h)[8]) {
+  sha256_init(h);
+  sha256_compress(blk, h);
+}
+
+// SHA-256 of a message given as NW big-endian words (4 NW bytes), padding included.
+template <int NW>
+KZ_DEV void sha256_words(const uint32_t (&m)[NW], uint32_t (&h)[8]) {
+  constexpr int BYTES = 4 * NW;
+  constexpr int NB = (BYTES + 9 + 63) / 64;  // padded blocks
+  sha256_init(h);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    uint32_t blk[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int wi = 16 * b + k;
+      blk[k] = wi < NW ? m[wi] : wi == NW ? 0x80000000u : 0u;
+    }
+    if (b == NB - 1) blk[15] = (uint32_t)(BYTES * 8);  // length < 2^32 bits
+    sha256_compress(blk, h);
+  }
 }
 
 // SHA256(seed[32] || le64(i) [|| tag]) for messages of 40 or 41 bytes (one block).

@@ -34,6 +34,19 @@ struct Launch {
                           const uint8_t* ys, uint32_t n, uint32_t* r_out, uint32_t* s_out, void* tpart,
                           uint32_t* negt, uint32_t* err);
   static size_t tpart_bytes(uint32_t n);
+  // ---- Fiat-Shamir / powers-of-r randomisers (fs.hpp)
+  static void fs_leaves(hipStream_t st, const uint8_t* dC, const uint8_t* dpi, const uint8_t* dz, const uint8_t* dy,
+                        uint32_t n, uint64_t offset, bool compressed, uint32_t* leaves);
+  // Merkle-reduce `count` 32-byte nodes to `target` (count / target a power of two; each
+  // result node covers count / target consecutive inputs); tmp holds 3 count / 4 nodes;
+  // returns the buffer holding the result
+  static const uint32_t* fs_reduce(hipStream_t st, const uint32_t* in, uint32_t count, uint32_t target, uint32_t* tmp);
+  static void fs_pad(hipStream_t st, uint32_t* digests, uint32_t nchunks, uint32_t p2);
+  static void fs_challenge(hipStream_t st, const uint32_t* root, uint64_t n, void* pow, uint32_t* chal_out);
+  static void pow_table(hipStream_t st, const Seed& r_be, void* pow, uint32_t* err);
+  static void scalar_prep_pow(hipStream_t st, const void* pow, uint64_t index_offset, const uint8_t* zs,
+                              const uint8_t* ys, uint32_t n, uint32_t* r_out, uint32_t* s_out, void* tpart,
+                              uint32_t* negt, uint32_t* err);
   static void encode_points(hipStream_t st, const XY* res, uint32_t count, uint8_t* out);
   static void sum_partials(hipStream_t st, const XY* parts, uint32_t nparts, uint32_t stride, uint32_t nout, XY* out);
   // ---- pairing (launch_pairing.hip)

@@ -1,6 +1,7 @@
 // Decoding / scalar-prep / encoding launchers (compiled once per curve).  Kernels: kernels.hpp.
 #include "launch.hpp"
 #include "points.hpp"
+#include "fs.hpp"
 
 namespace kzgmi {
 
@@ -50,6 +51,51 @@ void Launch<Cv>::scalar_prep(hipStream_t st, const Seed& seed, uint64_t index_of
   k_tsum<Cv><<<1, 256, 0, st>>>((const FrF*)tpart, nblk, negt);
 }
 template <class Cv>
+void Launch<Cv>::fs_leaves(hipStream_t st, const uint8_t* dC, const uint8_t* dpi, const uint8_t* dz, const uint8_t* dy,
+                           uint32_t n, uint64_t offset, bool compressed, uint32_t* leaves) {
+  if (n) k_fs_leaves<Cv><<<grid_for(n, 256), 256, 0, st>>>(dC, dpi, dz, dy, n, offset, compressed ? 1 : 0, leaves);
+}
+template <class Cv>
+const uint32_t* Launch<Cv>::fs_reduce(hipStream_t st, const uint32_t* in, uint32_t count, uint32_t target,
+                                      uint32_t* tmp) {
+  // ping-pong inside tmp (3 count / 4 nodes): pass outputs alternate between
+  // [0, count/2) and [count/2, 3 count/4)
+  uint32_t* bufs[2] = {tmp, tmp + 8 * (size_t)(count / 2)};
+  int which = 0;
+  while (count > target) {
+    uint32_t group = count / target < 512 ? count / target : 512;
+    uint32_t out_n = count / group;
+    uint32_t* out = bufs[which];
+    k_fs_merkle<<<out_n, 256, 0, st>>>(in, group, out);
+    in = out;
+    count = out_n;
+    which ^= 1;
+  }
+  return in;
+}
+template <class Cv>
+void Launch<Cv>::fs_pad(hipStream_t st, uint32_t* digests, uint32_t nchunks, uint32_t p2) {
+  if (p2 > nchunks) k_fs_pad<<<grid_for(p2 - nchunks, 256), 256, 0, st>>>(digests, nchunks, p2);
+}
+template <class Cv>
+void Launch<Cv>::fs_challenge(hipStream_t st, const uint32_t* root, uint64_t n, void* pow, uint32_t* chal_out) {
+  k_fs_challenge<Cv><<<1, 64, 0, st>>>(root, n, (Fp<typename Cv::FrP>*)pow, chal_out);
+}
+template <class Cv>
+void Launch<Cv>::pow_table(hipStream_t st, const Seed& r_be, void* pow, uint32_t* err) {
+  k_pow_table<Cv><<<1, 64, 0, st>>>(r_be, (Fp<typename Cv::FrP>*)pow, err);
+}
+template <class Cv>
+void Launch<Cv>::scalar_prep_pow(hipStream_t st, const void* pow, uint64_t index_offset, const uint8_t* zs,
+                                 const uint8_t* ys, uint32_t n, uint32_t* r_out, uint32_t* s_out, void* tpart,
+                                 uint32_t* negt, uint32_t* err) {
+  using FrF = Fp<typename Cv::FrP>;
+  const uint32_t nblk = grid_for(n, PREP_BLOCK);
+  k_scalar_prep_pow<Cv, PREP_BLOCK><<<nblk, PREP_BLOCK, 0, st>>>((const FrF*)pow, index_offset, zs, ys, n, r_out,
+                                                                  s_out, (FrF*)tpart, err);
+  k_tsum<Cv><<<1, 256, 0, st>>>((const FrF*)tpart, nblk, negt);
+}
+template <class Cv>
 void Launch<Cv>::encode_points(hipStream_t st, const XY* res, uint32_t count, uint8_t* out) {
   k_encode_points<Cv><<<grid_for(count, 64), 64, 0, st>>>(res, count, out);
 }
@@ -69,6 +115,14 @@ template void Launch<C_>::convert_g2(hipStream_t, const uint8_t*, uint32_t, G2Af
 template size_t Launch<C_>::tpart_bytes(uint32_t);
 template void Launch<C_>::scalar_prep(hipStream_t, const Seed&, uint64_t, const uint8_t*, const uint8_t*, uint32_t,
                                       uint32_t*, uint32_t*, void*, uint32_t*, uint32_t*);
+template void Launch<C_>::fs_leaves(hipStream_t, const uint8_t*, const uint8_t*, const uint8_t*, const uint8_t*,
+                                     uint32_t, uint64_t, bool, uint32_t*);
+template const uint32_t* Launch<C_>::fs_reduce(hipStream_t, const uint32_t*, uint32_t, uint32_t, uint32_t*);
+template void Launch<C_>::fs_pad(hipStream_t, uint32_t*, uint32_t, uint32_t);
+template void Launch<C_>::fs_challenge(hipStream_t, const uint32_t*, uint64_t, void*, uint32_t*);
+template void Launch<C_>::pow_table(hipStream_t, const Seed&, void*, uint32_t*);
+template void Launch<C_>::scalar_prep_pow(hipStream_t, const void*, uint64_t, const uint8_t*, const uint8_t*, uint32_t,
+                                          uint32_t*, uint32_t*, void*, uint32_t*, uint32_t*);
 template void Launch<C_>::encode_points(hipStream_t, const Xyzz<C_>*, uint32_t, uint8_t*);
 template void Launch<C_>::sum_partials(hipStream_t, const Xyzz<C_>*, uint32_t, uint32_t, uint32_t, Xyzz<C_>*);
 

@@ -91,20 +91,15 @@ __global__ void __launch_bounds__(256) k_decompress_points(const uint8_t* __rest
   inf[i] = is_inf ? 1 : 0;
 }
 
-// uncompressed G1 encodings -> compressed (no validation: a test/bench input utility)
+// one uncompressed G1 encoding (as loaded little-endian words) -> its compressed encoding
+// (same word layout; no validation)
 template <class Cv>
-__global__ void __launch_bounds__(256) k_compress_points(const uint8_t* __restrict__ in, uint32_t n,
-                                                         uint8_t* __restrict__ out) {
+KZ_DEV void compress_encoding(const uint32_t (&w)[2 * Cv::FpP::N], uint32_t (&o)[Cv::FpP::N]) {
   using P = typename Cv::FpP;
   constexpr int N = P::N;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t w[2 * N];
-  load_words(in + (size_t)i * 8 * N, w);
   uint32_t any = 0;
 #pragma unroll
   for (int k = 0; k < 2 * N; ++k) any |= w[k];
-  uint32_t o[N];
 #pragma unroll
   for (int k = 0; k < N; ++k) o[k] = w[k];
   const bool is_inf = Cv::ID == 0 ? (w[0] & 0x40u) != 0 : any == 0;
@@ -116,6 +111,18 @@ __global__ void __launch_bounds__(256) k_compress_points(const uint8_t* __restri
     const bool larger = fp_raw_gt(fp_from_be_words<P>(w, N), P::HALF);
     o[0] |= Cv::ID == 0 ? (0x80u | (larger ? 0x20u : 0u)) : (larger ? 0xc0u : 0x80u);
   }
+}
+
+// uncompressed G1 encodings -> compressed (no validation: a test/bench input utility)
+template <class Cv>
+__global__ void __launch_bounds__(256) k_compress_points(const uint8_t* __restrict__ in, uint32_t n,
+                                                         uint8_t* __restrict__ out) {
+  constexpr int N = Cv::FpP::N;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[2 * N], o[N];
+  load_words(in + (size_t)i * 8 * N, w);
+  compress_encoding<Cv>(w, o);
   store_words(out + (size_t)i * 4 * N, o);
 }
 

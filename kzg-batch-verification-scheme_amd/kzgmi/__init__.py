@@ -70,6 +70,9 @@ def lib():
         "kzgmi_batch_verify_device_ex_async": ([vp, vp, c.c_int, vp, vp, vp, vp, sz, u8p, c.c_uint32], c.c_int),
         "kzgmi_g1_validate_device": ([vp, c.c_int, vp, sz, c.c_uint32], c.c_int),
         "kzgmi_g1_compress_device": ([vp, c.c_int, vp, sz, vp], c.c_int),
+        "kzgmi_fs_challenge_device": ([vp, c.c_int, vp, vp, vp, vp, sz, c.c_uint32, u8p], c.c_int),
+        "kzgmi_fs_chunk_digests_device": ([vp, c.c_int, vp, vp, vp, vp, sz, c.c_uint64, c.c_uint32, vp], c.c_int),
+        "kzgmi_fs_challenge_from_digests_device": ([vp, c.c_int, vp, sz, c.c_uint64, u8p], c.c_int),
         "kzgmi_slot_wait": ([vp, c.c_int, ip], c.c_int),
         "kzgmi_last_combination": ([vp, u8p, u8p], c.c_int),
         "kzgmi_msm_g1": ([vp, c.c_int, u8p, u8p, sz, u8p], c.c_int),
@@ -104,7 +107,8 @@ def exported_symbols():
         "kzgmi_ctx_destroy", "kzgmi_srs_load", "kzgmi_srs_free", "kzgmi_batch_verify",
         "kzgmi_batch_verify_device", "kzgmi_batch_verify_device_async", "kzgmi_slot_wait",
         "kzgmi_batch_verify_ex", "kzgmi_batch_verify_device_ex_async", "kzgmi_g1_validate_device",
-        "kzgmi_g1_compress_device",
+        "kzgmi_g1_compress_device", "kzgmi_fs_challenge_device", "kzgmi_fs_chunk_digests_device",
+        "kzgmi_fs_challenge_from_digests_device",
         "kzgmi_last_combination", "kzgmi_msm_g1", "kzgmi_msm_g1_device", "kzgmi_partial_bytes",
         "kzgmi_batch_partial_device", "kzgmi_batch_combine_device", "kzgmi_batch_partial_device_async",
         "kzgmi_batch_combine_device_async", "kzgmi_msm_partial_device",
@@ -115,11 +119,25 @@ def exported_symbols():
 
 FLAG_COMPRESSED = 1
 FLAG_SUBGROUP_CHECK = 2
+FLAG_POWERS = 4
+FLAG_FIAT_SHAMIR = 8
 ERR_NOT_IN_SUBGROUP = -7
+FS_CHUNK = 4096
 
 
-def _flags(compressed: bool, subgroup_check: bool) -> int:
-    return (FLAG_COMPRESSED if compressed else 0) | (FLAG_SUBGROUP_CHECK if subgroup_check else 0)
+def _flags(compressed: bool = False, subgroup_check: bool = False, fiat_shamir: bool = False,
+           challenge=None) -> int:
+    return ((FLAG_COMPRESSED if compressed else 0) | (FLAG_SUBGROUP_CHECK if subgroup_check else 0)
+            | (FLAG_FIAT_SHAMIR if fiat_shamir else 0) | (FLAG_POWERS if challenge is not None else 0))
+
+
+def _challenge_seed(seed, challenge):
+    """KZGMI_FLAG_POWERS passes r (int or 32 big-endian bytes) in the seed argument."""
+    if challenge is None:
+        return None if seed is None else bytes(seed)
+    if seed is not None:
+        raise ValueError("pass either seed or challenge")
+    return int(challenge).to_bytes(32, "big") if isinstance(challenge, int) else bytes(challenge)
 
 
 def _check(rc: int):
@@ -195,13 +213,16 @@ class Context:
 
     # ------------------------------------------------------------------ batch verify
     def batch_verify(self, srs: Srs, commitments, zs, ys, proofs, seed: Optional[bytes] = None,
-                     n: Optional[int] = None, compressed: bool = False, subgroup_check: bool = False) -> bool:
+                     n: Optional[int] = None, compressed: bool = False, subgroup_check: bool = False,
+                     fiat_shamir: bool = False, challenge=None) -> bool:
         """BASELINE.json:5 batch_verify.  compressed: C/pi are compressed G1 encodings;
-        subgroup_check: reject points outside G1 (KZGMI_ERR_NOT_IN_SUBGROUP)."""
-        flags = _flags(compressed, subgroup_check)
+        subgroup_check: reject points outside G1 (KZGMI_ERR_NOT_IN_SUBGROUP); fiat_shamir:
+        r_i = r^i with r hashed from the inputs on the GPU; challenge: r_i = r^i for a
+        caller-supplied r (e.g. the EIP-4844 transcript's)."""
+        flags = _flags(compressed, subgroup_check, fiat_shamir, challenge)
         g1b = (1 if compressed else 2) * FP_BYTES[srs.curve]
         ok = ctypes.c_int(-1)
-        sd = None if seed is None else bytes(seed)
+        sd = _challenge_seed(seed, challenge)
         if seed is not None and len(sd) != 32:
             raise ValueError("seed must be 32 bytes")
         if _is_device_tensor(commitments):
@@ -224,11 +245,33 @@ class Context:
         return bool(ok.value)
 
     def batch_verify_async(self, srs: Srs, slot: int, commitments, zs, ys, proofs, n: int,
-                           seed: Optional[bytes] = None, compressed: bool = False, subgroup_check: bool = False):
-        sd = None if seed is None else bytes(seed)
+                           seed: Optional[bytes] = None, compressed: bool = False, subgroup_check: bool = False,
+                           fiat_shamir: bool = False, challenge=None):
         _check(lib().kzgmi_batch_verify_device_ex_async(self.handle, srs.handle, int(slot), _dptr(commitments),
-                                                        _dptr(zs), _dptr(ys), _dptr(proofs), n, sd,
-                                                        _flags(compressed, subgroup_check)))
+                                                        _dptr(zs), _dptr(ys), _dptr(proofs), n,
+                                                        _challenge_seed(seed, challenge),
+                                                        _flags(compressed, subgroup_check, fiat_shamir, challenge)))
+
+    # ------------------------------------------------------------------ Fiat-Shamir
+    def fs_challenge(self, curve: str, commitments, zs, ys, proofs, n: int, compressed: bool = False) -> int:
+        """r of KZGMI_FLAG_FIAT_SHAMIR for device-resident inputs."""
+        out = ctypes.create_string_buffer(32)
+        _check(lib().kzgmi_fs_challenge_device(self.handle, CURVES[curve], _dptr(commitments), _dptr(zs), _dptr(ys),
+                                               _dptr(proofs), n, _flags(compressed), out))
+        return int.from_bytes(out.raw, "big")
+
+    def fs_chunk_digests(self, curve: str, commitments, zs, ys, proofs, n: int, index_offset: int, out,
+                         compressed: bool = False):
+        """Shard's 4096-leaf subtree roots (ceil(n / 4096) x 32 B) into device tensor `out`."""
+        _check(lib().kzgmi_fs_chunk_digests_device(self.handle, CURVES[curve], _dptr(commitments), _dptr(zs),
+                                                   _dptr(ys), _dptr(proofs), n, int(index_offset),
+                                                   _flags(compressed), _dptr(out)))
+
+    def fs_challenge_from_digests(self, curve: str, digests, nchunks: int, n_total: int) -> int:
+        out = ctypes.create_string_buffer(32)
+        _check(lib().kzgmi_fs_challenge_from_digests_device(self.handle, CURVES[curve], _dptr(digests), nchunks,
+                                                            int(n_total), out))
+        return int.from_bytes(out.raw, "big")
 
     def g1_validate(self, curve: str, points, n: int, compressed: bool = False, subgroup_check: bool = False):
         """Raise KzgmiError unless all n device-resident G1 encodings are valid."""
@@ -285,11 +328,14 @@ class Context:
         return bool(ok.value)
 
     def batch_partial_async(self, srs: Srs, slot: int, commitments, zs, ys, proofs, n: int, index_offset: int,
-                            seed: bytes, out, compressed: bool = False, subgroup_check: bool = False):
-        """Enqueue this shard's partial (A_k, B_k) on `slot`; complete with wait(slot)."""
+                            seed, out, compressed: bool = False, subgroup_check: bool = False, challenge=None):
+        """Enqueue this shard's partial (A_k, B_k) on `slot`; complete with wait(slot).
+        challenge: r_i = r^(index_offset + i) (pass seed=None)."""
         _check(lib().kzgmi_batch_partial_device_async(self.handle, srs.handle, int(slot), _dptr(commitments),
                                                       _dptr(zs), _dptr(ys), _dptr(proofs), n, int(index_offset),
-                                                      bytes(seed), _flags(compressed, subgroup_check), _dptr(out)))
+                                                      _challenge_seed(seed, challenge),
+                                                      _flags(compressed, subgroup_check, False, challenge),
+                                                      _dptr(out)))
 
     def batch_combine_async(self, srs: Srs, slot: int, partials, n_parts: int):
         """Enqueue sum-of-partials + pairing check on `slot`; wait(slot) returns the verdict."""
@@ -372,10 +418,10 @@ def load_srs(curve: str, g2: bytes, tau_g2: bytes, ctx: Optional[Context] = None
 
 
 def batch_verify(commitments, zs, ys, proofs, srs: Srs, seed: Optional[bytes] = None, compressed: bool = False,
-                 subgroup_check: bool = False) -> bool:
+                 subgroup_check: bool = False, fiat_shamir: bool = False, challenge=None) -> bool:
     """BASELINE.json:5 batch_verify(commitments, zs, ys, proofs, srs) on the GPU."""
     return srs.ctx.batch_verify(srs, commitments, zs, ys, proofs, seed=seed, compressed=compressed,
-                                subgroup_check=subgroup_check)
+                                subgroup_check=subgroup_check, fiat_shamir=fiat_shamir, challenge=challenge)
 
 
 def msm_g1(curve: str, points, scalars, ctx: Optional[Context] = None) -> bytes:

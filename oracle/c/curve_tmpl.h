@@ -414,9 +414,12 @@ static void C_(pairing_check)(const C_(aff)* A, const C_(aff)* B, const C_(aff2)
 }
 
 /* offset = global index of tuple 0 (shards); do_pairing = 0 only computes A, B */
+/* seed != NULL: r_i = randomizer(seed, offset + i) (127-bit); pow_r != NULL (32 B big-endian r < r):
+ * r_i = r^(offset + i) (Fiat-Shamir / powers mode). */
 static int C_(batch_verify)(const uint8_t* cm, const uint8_t* zs, const uint8_t* ys, const uint8_t* pf,
                             size_t n, const uint8_t* g2b, const uint8_t* tg2b, const uint8_t* seed,
-                            int* ok, uint8_t* a_out, uint8_t* b_out, uint64_t offset, int do_pairing) {
+                            int* ok, uint8_t* a_out, uint8_t* b_out, uint64_t offset, int do_pairing,
+                            const uint8_t* pow_r) {
   C_(aff2) g2, tg2;
   int e;
   if ((e = C_(g2_decode)(&g2, g2b))) return e;
@@ -432,11 +435,23 @@ static int C_(batch_verify)(const uint8_t* cm, const uint8_t* zs, const uint8_t*
   uint64_t* sc = (uint64_t*)malloc((2 * n + 1) * 4 * sizeof(uint64_t)); /* [r..., s..., -t] */
   int err = 0;
   FR tsum; FR_(zero)(&tsum);
+  FR rbase;  /* powers mode: r in Montgomery form */
+  if (pow_r) {
+    uint64_t raw[4];
+    if ((e = C_(fr_decode_raw)(raw, pow_r))) { free(pts); free(sc); return e; }
+    FR_(to_mont)(&rbase, raw);
+  }
   #pragma omp parallel num_threads(kzgo_threads())
   {
     FR tloc; FR_(zero)(&tloc);
-    #pragma omp for schedule(static)
-    for (size_t i = 0; i < n; ++i) {
+    const size_t nt = (size_t)omp_get_num_threads(), tid = (size_t)omp_get_thread_num();
+    const size_t lo = n * tid / nt, hi = n * (tid + 1) / nt;
+    FR rcur;  /* powers mode: r^(offset + i), stepped by r */
+    if (pow_r) {
+      uint64_t ex[1] = {offset + (uint64_t)lo};
+      FR_(pow)(&rcur, &rbase, ex, 64);
+    }
+    for (size_t i = lo; i < hi; ++i) {
       int le = C_(g1_decode)(&pts[i], cm + i * 2 * FPB);
       if (!le) le = C_(g1_decode)(&pts[n + i], pf + i * 2 * FPB);
       uint64_t z[4], y[4], ri[4];
@@ -447,10 +462,17 @@ static int C_(batch_verify)(const uint8_t* cm, const uint8_t* zs, const uint8_t*
         { if (!err) err = le; }
         continue;
       }
-      kzgo_randomizer(seed, offset + (uint64_t)i, ri);
-      memcpy(sc + 4 * i, ri, 32);
       FR rm, zm, ym, s;
-      FR_(to_mont)(&rm, ri); FR_(to_mont)(&zm, z); FR_(to_mont)(&ym, y);
+      if (pow_r) {
+        rm = rcur;
+        FR_(mul)(&rcur, &rcur, &rbase);
+        FR_(from_mont)(ri, &rm);
+      } else {
+        kzgo_randomizer(seed, offset + (uint64_t)i, ri);
+        FR_(to_mont)(&rm, ri);
+      }
+      memcpy(sc + 4 * i, ri, 32);
+      FR_(to_mont)(&zm, z); FR_(to_mont)(&ym, y);
       FR_(mul)(&s, &rm, &zm); FR_(from_mont)(sc + 4 * (n + i), &s);
       FR_(mul)(&s, &rm, &ym); FR_(add)(&tloc, &tloc, &s);
     }

@@ -256,8 +256,19 @@ int kzgo_batch_verify(int curve, const uint8_t* cm, const uint8_t* zs, const uin
                       size_t n, const uint8_t* g2, const uint8_t* tau_g2, const uint8_t* seed, int* ok,
                       uint8_t* a_out, uint8_t* b_out) {
   if (!ok || !seed || !g2 || !tau_g2 || (n && (!cm || !zs || !ys || !pf))) return KZGO_ERR_ARG;
-  return CURVE_DISPATCH(curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, 1),
-                        bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, 1));
+  return CURVE_DISPATCH(curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, 1, NULL),
+                        bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, 1, NULL));
+}
+
+/* Powers mode (Fiat-Shamir / caller-supplied challenge): r_i = r^(offset + i), r = int_be(r32) < r.
+ * do_pairing = 0 gives the shard partials (ok untouched). */
+int kzgo_batch_verify_powers(int curve, const uint8_t* cm, const uint8_t* zs, const uint8_t* ys, const uint8_t* pf,
+                             size_t n, uint64_t offset, const uint8_t* g2, const uint8_t* tau_g2, const uint8_t* r32,
+                             int do_pairing, int* ok, uint8_t* a_out, uint8_t* b_out) {
+  if (!ok || !r32 || !g2 || !tau_g2 || (n && (!cm || !zs || !ys || !pf))) return KZGO_ERR_ARG;
+  return CURVE_DISPATCH(
+      curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, NULL, ok, a_out, b_out, offset, do_pairing, r32),
+      bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, NULL, ok, a_out, b_out, offset, do_pairing, r32));
 }
 
 /* A, B of tuples [offset, offset+n) of a global batch (no pairing): the shard partials */
@@ -266,8 +277,8 @@ int kzgo_batch_combination(int curve, const uint8_t* cm, const uint8_t* zs, cons
                            uint8_t* a_out, uint8_t* b_out) {
   int ok = -1;
   if (!seed || !g2 || !tau_g2 || !a_out || !b_out || (n && (!cm || !zs || !ys || !pf))) return KZGO_ERR_ARG;
-  return CURVE_DISPATCH(curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, &ok, a_out, b_out, offset, 0),
-                        bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, &ok, a_out, b_out, offset, 0));
+  return CURVE_DISPATCH(curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, &ok, a_out, b_out, offset, 0, NULL),
+                        bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, &ok, a_out, b_out, offset, 0, NULL));
 }
 
 int kzgo_pairing_check(int curve, const uint8_t* a, const uint8_t* b, const uint8_t* g2, const uint8_t* tau_g2, int* ok) {

@@ -37,6 +37,9 @@ def lib():
         L.kzgo_pairing_check.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p, c.POINTER(c.c_int)]
         L.kzgo_msm_g1.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_size_t, c.c_char_p]
         L.kzgo_g1_mul_gen.argtypes = [c.c_int, c.c_char_p, c.c_size_t, c.c_char_p]
+        L.kzgo_batch_verify_powers.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p, c.c_size_t,
+                                               c.c_uint64, c.c_char_p, c.c_char_p, c.c_char_p, c.c_int,
+                                               c.POINTER(c.c_int), c.c_char_p, c.c_char_p]
         L.kzgo_g1_decompress.argtypes = [c.c_int, c.c_char_p, c.c_size_t, c.c_char_p]
         L.kzgo_g1_compress.argtypes = [c.c_int, c.c_char_p, c.c_size_t, c.c_char_p]
         L.kzgo_g1_subgroup_check.argtypes = [c.c_int, c.c_char_p, c.c_size_t, c.POINTER(c.c_int)]
@@ -96,6 +99,17 @@ def pairing_check(curve, A: bytes, B: bytes, g2: bytes, tau_g2: bytes) -> bool:
     ok = ctypes.c_int(-1)
     _check(lib().kzgo_pairing_check(CURVE_IDS[curve], A, B, g2, tau_g2, ctypes.byref(ok)))
     return bool(ok.value)
+
+
+def batch_verify_powers(curve, commitments, zs, ys, proofs, n, g2, tau_g2, r: int, offset=0, pairing=True):
+    """Powers mode: r_i = r^(offset + i).  Returns (ok or None, A, B)."""
+    g1b = 2 * FP_BYTES[curve]
+    ok = ctypes.c_int(-1)
+    a = ctypes.create_string_buffer(g1b)
+    b = ctypes.create_string_buffer(g1b)
+    _check(lib().kzgo_batch_verify_powers(CURVE_IDS[curve], commitments, zs, ys, proofs, n, offset, g2, tau_g2,
+                                          int(r).to_bytes(32, "big"), 1 if pairing else 0, ctypes.byref(ok), a, b))
+    return (bool(ok.value) if pairing else None), a.raw, b.raw
 
 
 def g1_decompress(curve, data: bytes, n: int):

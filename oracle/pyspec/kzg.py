@@ -189,13 +189,14 @@ def randomizer(seed: bytes, i: int) -> int:
 
 
 def batch_combination(commitments: Sequence[G1Point], zs, ys, proofs: Sequence[G1Point],
-                      seed: bytes, C: CurveParams, offset: int = 0):
-    """Return (A, B) as affine points.  `offset` = global index of tuple 0 (sharding)."""
+                      seed: bytes, C: CurveParams, offset: int = 0, powers_of=None):
+    """Return (A, B) as affine points.  `offset` = global index of tuple 0 (sharding).
+    powers_of = r: Fiat-Shamir / powers mode, r_i = r^(offset + i) instead of the seed rule."""
     A = None
     B = None
     t = 0
     for i, (Ci, z, y, Pi) in enumerate(zip(commitments, zs, ys, proofs)):
-        ri = randomizer(seed, offset + i)
+        ri = pow(powers_of, offset + i, C.r) if powers_of is not None else randomizer(seed, offset + i)
         A = g1_add(A, g1_mul(Pi, ri, C), C)
         B = g1_add(B, g1_mul(Ci, ri, C), C)
         B = g1_add(B, g1_mul(Pi, ri * z % C.r, C), C)
@@ -271,3 +272,42 @@ def poly_commit_and_open(coeffs: List[int], z: int, tau: int, C: CurveParams):
         for k in range(d - 1, 0, -1):
             q[k - 1] = (coeffs[k] + z * q[k]) % r
     return commit(coeffs), y, commit(q)
+
+
+# ------------------------------------------------------------------ Fiat-Shamir transcript
+# (device implementation csrc/fs.hpp, C-ABI KZGMI_FLAG_FIAT_SHAMIR)
+FS_LEAF_TAG = b"KZGMI_FS_LEAF_V1"
+FS_ROOT_TAG = b"KZGMI_FS_ROOT_V1"
+FS_CHUNK = 4096
+
+
+def fs_leaf(i: int, c_comp: bytes, p_comp: bytes, z: int, y: int) -> bytes:
+    return hashlib.sha256(FS_LEAF_TAG + i.to_bytes(8, "big") + c_comp + p_comp + z.to_bytes(32, "big")
+                          + y.to_bytes(32, "big")).digest()
+
+
+def merkle_root(nodes: List[bytes]) -> bytes:
+    """Binary Merkle root of a power-of-two list; node = SHA256(left || right)."""
+    assert nodes and len(nodes) & (len(nodes) - 1) == 0
+    while len(nodes) > 1:
+        nodes = [hashlib.sha256(nodes[k] + nodes[k + 1]).digest() for k in range(0, len(nodes), 2)]
+    return nodes[0]
+
+
+def fs_slots(n: int) -> int:
+    slots = FS_CHUNK
+    while slots < n:
+        slots *= 2
+    return slots
+
+
+def fs_challenge(commitments: Sequence[G1Point], zs, ys, proofs: Sequence[G1Point], C: CurveParams) -> int:
+    """r = int_be(SHA256(ROOT_TAG || be64(n) || merkle_root(leaves, zero-padded to
+    max(4096, next_pow2(n)) slots))) mod r, 1 if 0; leaves over compressed encodings."""
+    n = len(commitments)
+    leaves = [fs_leaf(i, g1_to_bytes_compressed(commitments[i], C), g1_to_bytes_compressed(proofs[i], C), zs[i], ys[i])
+              for i in range(n)]
+    leaves += [bytes(32)] * (fs_slots(n) - n)
+    h = hashlib.sha256(FS_ROOT_TAG + n.to_bytes(8, "big") + merkle_root(leaves)).digest()
+    r = int.from_bytes(h, "big") % C.r
+    return r if r else 1

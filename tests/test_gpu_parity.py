@@ -265,3 +265,25 @@ def test_sharded_pipeline_rccl_world1(ctx, torch_dev):
     finally:
         if created:
             dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_srs_outliving_context(torch_dev, golden):
+    """An Srs freed after its Context was closed must not touch the destroyed context (it used
+    to leave a sticky 'invalid device ordinal' in the HIP runtime)."""
+    import gc
+    import kzgmi
+    torch = torch_dev
+    g = golden("bls12_381_batch_n4.json")
+    c = kzgmi.Context(0, 1)
+    srs = c.load_srs("bls12_381", h(g["g2"]), h(g["tau_g2"]))
+    c.close()
+    del srs
+    gc.collect()
+    x = torch.ones(8, device="cuda") * 2
+    torch.cuda.synchronize()
+    assert x.sum().item() == 16
+    c2 = kzgmi.Context(0, 1)
+    srs2 = c2.load_srs("bls12_381", h(g["g2"]), h(g["tau_g2"]))
+    assert c2.batch_verify(srs2, h(g["commitments"]), h(g["zs"]), h(g["ys"]), h(g["proofs"]), seed=h(g["seed"]))
+    c2.close()
