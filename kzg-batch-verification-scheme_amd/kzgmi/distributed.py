@@ -23,20 +23,52 @@ from __future__ import annotations
 from typing import Tuple
 
 
-def shard_range(n_total: int, world: int, rank: int) -> Tuple[int, int]:
-    """Contiguous balanced split: (offset, count) of rank's tuples."""
+FS_CHUNK = 4096  # Fiat-Shamir transcript subtree (csrc/fs.hpp): shard offsets must align to it
+
+
+def shard_range(n_total: int, world: int, rank: int, align: int = 1) -> Tuple[int, int]:
+    """Contiguous balanced split: (offset, count) of rank's tuples; offsets are multiples of
+    `align` (the Fiat-Shamir mode needs align = 4096)."""
     if world <= 0 or not 0 <= rank < world:
         raise ValueError("bad world/rank")
-    base, extra = divmod(n_total, world)
-    offset = rank * base + min(rank, extra)
-    return offset, base + (1 if rank < extra else 0)
+    units = (n_total + align - 1) // align
+    base, extra = divmod(units, world)
+    u0 = rank * base + min(rank, extra)
+    u1 = u0 + base + (1 if rank < extra else 0)
+    lo, hi = min(n_total, u0 * align), min(n_total, u1 * align)
+    return lo, hi - lo
+
+
+def fs_challenge_sharded(backend, curve: str, commitments, zs, ys, proofs, n_local: int, offset: int,
+                         n_total: int, compressed: bool = False, group=None) -> int:
+    """The Fiat-Shamir r of the whole (sharded) batch: each rank hashes its 4096-leaf subtrees,
+    the subtree roots are all-gathered (one collective), every rank derives the same r.
+    Shards must come from shard_range(..., align=4096)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    dev = backend.tensor_device()
+    counts = [(shard_range(n_total, world, k, FS_CHUNK)[1] + FS_CHUNK - 1) // FS_CHUNK for k in range(world)]
+    width = max(1, max(counts))
+    local = torch.zeros(width * 32, dtype=torch.uint8, device=dev)
+    if n_local:
+        backend.fs_chunk_digests(curve, commitments, zs, ys, proofs, n_local, offset, local, compressed=compressed)
+    gathered = torch.empty(world * width * 32, dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(gathered, local, group=group)
+    parts = [gathered[k * width * 32:(k * width + counts[k]) * 32] for k in range(world) if counts[k]]
+    digests = torch.cat(parts)
+    return backend.fs_challenge_from_digests(curve, digests, sum(counts), n_total)
 
 
 def sharded_batch_verify(backend, srs, commitments, zs, ys, proofs, n_local: int, offset: int,
-                         seed: bytes, group=None) -> bool:
+                         seed: bytes, group=None, fiat_shamir: bool = False, n_total: int = 0,
+                         compressed: bool = False) -> bool:
     """Verify this rank's shard as part of a global batch; collective over `group`.
 
     commitments/zs/ys/proofs: this rank's shard (device tensors on the GPU path).
+    fiat_shamir: r_i = r^i with r from the whole batch's transcript (fs_challenge_sharded;
+    shards from shard_range(n_total, world, rank, align=4096)); seed is ignored.
     Returns the global verdict on every rank.
     """
     import torch
@@ -46,7 +78,14 @@ def sharded_batch_verify(backend, srs, commitments, zs, ys, proofs, n_local: int
     pb = backend.partial_bytes(srs.curve)
     dev = backend.tensor_device()
     local = torch.empty(2 * pb, dtype=torch.uint8, device=dev)
-    backend.batch_partial(srs, commitments, zs, ys, proofs, n_local, offset, seed, local)
+    if fiat_shamir:
+        r = fs_challenge_sharded(backend, srs.curve, commitments, zs, ys, proofs, n_local, offset, n_total,
+                                 compressed=compressed, group=group)
+        backend.batch_partial_async(srs, 0, commitments, zs, ys, proofs, n_local, offset, None, local,
+                                    compressed=compressed, challenge=r)
+        backend.wait(0)
+    else:
+        backend.batch_partial(srs, commitments, zs, ys, proofs, n_local, offset, seed, local)
     gathered = torch.empty(world * 2 * pb, dtype=torch.uint8, device=dev)
     dist.all_gather_into_tensor(gathered, local, group=group)
     return backend.batch_combine(srs, gathered, world)

@@ -55,3 +55,7 @@ def test_shard_range():
                 assert o == off
                 off += c
             assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
+            aligned = [shard_range(n, w, r, align=4096) for r in range(w)]
+            assert sum(c for _, c in aligned) == n
+            assert all(o % 4096 == 0 or c == 0 for o, c in aligned)
+            assert [o for o, c in aligned if c] == sorted(o for o, c in aligned if c)

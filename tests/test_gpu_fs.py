@@ -140,3 +140,36 @@ def test_fs_full_size(ctx):
     assert ok is True and ctx.last_combination(curve) == (A, B)
     y[5] ^= 1
     assert ctx.batch_verify(srs, Cm, z, y, P, n=n, fiat_shamir=True) is False
+
+
+def test_sharded_fs_rccl_world1(ctx):
+    """kzgmi.distributed Fiat-Shamir flow on the device over a world-1 RCCL group."""
+    import os
+    import socket
+    import torch
+    import torch.distributed as dist
+    from kzgmi.distributed import fs_challenge_sharded, sharded_batch_verify
+    curve = "bls12_381"
+    C = pc.CURVES[curve]
+    n, tau = 5000, 4711
+    Cm, z, y, P = _gen(ctx, curve, n, tau, b"fs-rccl")
+    g2 = pk.g2_to_bytes(C.g2, C)
+    srs = ctx.load_srs(curve, g2, O.g2_mul(curve, g2, tau))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    created = not dist.is_initialized()
+    if created:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        r = fs_challenge_sharded(ctx, curve, Cm, z, y, P, n, 0, n)
+        assert r == ctx.fs_challenge(curve, Cm, z, y, P, n)
+        assert sharded_batch_verify(ctx, srs, Cm, z, y, P, n, 0, None, fiat_shamir=True, n_total=n) is True
+        y[7] ^= 1
+        assert sharded_batch_verify(ctx, srs, Cm, z, y, P, n, 0, None, fiat_shamir=True, n_total=n) is False
+    finally:
+        if created:
+            dist.destroy_process_group()
