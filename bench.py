@@ -134,7 +134,9 @@ def main():
     ap.add_argument("--msm-steps", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--compressed-steps", type=int, default=16,
+    ap.add_argument("--fs-steps", type=int, default=36,
+                    help="secondary: pipelined batches in Fiat-Shamir mode (r_i = r^i, 0 = skip)")
+    ap.add_argument("--compressed-steps", type=int, default=36,
                     help="secondary: pipelined batches with compressed inputs + subgroup checks (0 = skip)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU pipeline (RCCL all-gather per batch) even at world size 1")
@@ -283,6 +285,33 @@ def main():
                 "phase_ms_single_batch": single, "phase_ms_avg_in_timed_region": cph}
         del cc, pp
 
+    # ---- secondary: Fiat-Shamir randomisers, single GPU
+    fsm = None
+    if world == 1 and not sharded and args.fs_steps > 0:
+        def fstep(k):
+            s = k % slots
+            if pending[s]:
+                assert ctx.wait(s), "batch rejected"
+            ctx.batch_verify_async(srs, s, Cm, z, y, P, n, fiat_shamir=True)
+            pending[s] = True
+
+        for k in range(min(4, args.fs_steps)):
+            fstep(k)
+        drain()
+        barrier()
+        a = time.perf_counter()
+        for k in range(args.fs_steps):
+            fstep(k)
+        drain()
+        barrier()
+        dt = time.perf_counter() - a
+        ctx.set_profiling(True)
+        assert ctx.batch_verify(srs, Cm, z, y, P, n=n, fiat_shamir=True)
+        fsm = {"batch_verifies_per_s": args.fs_steps / dt, "steps": args.fs_steps,
+               "randomisers": "r_i = r^i, r from the GPU Merkle transcript of the batch (255-bit scalars)",
+               "phase_ms_single_batch": ctx.phase_ms()}
+        ctx.set_profiling(False)
+
     # ---- secondary: G1 MSM pts/s at n points per GPU (commitments as points, z as scalars)
     msm_rate = None
     if args.msm_steps > 0:
@@ -381,6 +410,7 @@ def main():
             "phase_ms_avg_in_timed_region": phases,
             "phase_ms_single_batch": phases_single,
             "compressed_subgroup": comp,
+            "fiat_shamir": fsm,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu and "value" in cpu else None,
         },
     }
