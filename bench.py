@@ -345,13 +345,29 @@ def main():
     fpmul_peak = ctx.probe_fpmul(curve)
     # modelled Fp products in the accumulation: ~32 n window-terms x (8M + 2S) per mixed add
     acc_fpmuls = 32 * n * 10
+    # PMC traffic of the same kernel and config from the committed profile (tools/profile.sh:
+    # separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE x 2 as MI355X_MICROARCH.md prescribes)
+    traffic, traffic_src, rocprof_ms = None, None, None
+    pmc_path = os.path.join(ROOT, "profiles", "r01", "rocprof", "pmc_accumulate.json")
+    if curve == "bls12_381" and n == 1 << 20 and os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f)
+        traffic = pmc["traffic_bytes_per_launch"]
+        traffic_src = "profiles/r01/rocprof/pmc_accumulate.json (%s)" % pmc["command"]
+        rocprof_ms = pmc["rocprof_avg_duration_ns"] / 1e6
     roofline = {
         "bound": "hbm",
         "achieved": achieved / 1e9 if achieved else None,
         "peak": HBM_PEAK / 1e9,
         "unit": "GB/s",
         "frac": (achieved / HBM_PEAK) if achieved else None,
-        "traffic": None,
+        "traffic": traffic,
+        "traffic_source": traffic_src,
+        "rocprof_kernel_avg_ms": rocprof_ms,
+        "timing_note": "kernel_ms = HIP events on the kernel's stream around k_accumulate + k_fixup in the "
+                       "12-deep pipelined region: includes time the launch waits for CUs held by other "
+                       "batches; rocprof_kernel_avg_ms is k_accumulate begin-to-end in the same pipelined "
+                       "command; compute.single_batch_* time the kernel alone",
         "kernel": "k_accumulate+k_fixup (bucket accumulation)",
         "kernel_ms": acc_ms,
         "algorithmic_bytes": alg_bytes,
