@@ -136,6 +136,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fs-steps", type=int, default=36,
                     help="secondary: pipelined batches in Fiat-Shamir mode (r_i = r^i, 0 = skip)")
+    ap.add_argument("--commit-steps", type=int, default=5,
+                    help="secondary: fixed-base prover commits of n coefficients (0 = skip)")
     ap.add_argument("--compressed-steps", type=int, default=36,
                     help="secondary: pipelined batches with compressed inputs + subgroup checks (0 = skip)")
     ap.add_argument("--sharded", action="store_true",
@@ -312,6 +314,24 @@ def main():
                "phase_ms_single_batch": ctx.phase_ms()}
         ctx.set_profiling(False)
 
+    # ---- secondary: prover-side fixed-base commit, single GPU
+    commit = None
+    if world == 1 and not sharded and args.commit_steps > 0:
+        a = time.perf_counter()
+        ck = ctx.load_commit_key(curve, Cm.cpu().numpy().tobytes(), n)  # n points as a stand-in SRS
+        load_s = time.perf_counter() - a
+        ctx.commit(ck, z, n)
+        barrier()
+        a = time.perf_counter()
+        for _ in range(args.commit_steps):
+            ctx.commit(ck, z, n)
+        barrier()
+        dt = time.perf_counter() - a
+        commit = {"commits_per_s": args.commit_steps / dt, "pts_per_s": n * args.commit_steps / dt,
+                  "key_load_s": load_s, "n": n,
+                  "method": "16 resident rows of 2^(16w)-shifted SRS points, one bucket set, synchronous calls"}
+        del ck
+
     # ---- secondary: G1 MSM pts/s at n points per GPU (commitments as points, z as scalars)
     msm_rate = None
     if args.msm_steps > 0:
@@ -427,6 +447,7 @@ def main():
             "phase_ms_single_batch": phases_single,
             "compressed_subgroup": comp,
             "fiat_shamir": fsm,
+            "prover_commit": commit,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu and "value" in cpu else None,
         },
     }

@@ -63,6 +63,7 @@ typedef enum { KZGMI_BLS12_381 = 0, KZGMI_BN254 = 1 } kzgmi_curve;
 
 typedef struct kzgmi_ctx kzgmi_ctx; /* one GPU, its streams and workspaces */
 typedef struct kzgmi_srs kzgmi_srs; /* {G1, [1]_2, [tau]_2} + precomputed Miller lines */
+typedef struct kzgmi_ck kzgmi_ck;   /* prover commit key: [tau^i]_1 + fixed-base tables */
 
 /* Version string of the library build. */
 const char* kzgmi_version(void);
@@ -170,6 +171,18 @@ int kzgmi_msm_partial_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_po
                              const void* d_scalars, size_t n, void* d_partial_out);
 int kzgmi_msm_combine_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_partials,
                              int n_parts, uint8_t* out);
+
+/* prover-side commitments with a fixed SRS base.  kzgmi_ck_load uploads
+ * n G1 powers ([tau^i]_1, host encodings, validated) and precomputes 16 rows of 2^(16 w)-shifted
+ * copies on the device (16 n points resident); kzgmi_commit then computes
+ * sum_{i < m} coeff_i [tau^i]_1 (coefficients: m x 32 B canonical Fr, m <= n) as ONE bucket
+ * set of 16-bit signed digits -- no per-window reduction, no window combination.  The key
+ * must be freed before (or is detached by) kzgmi_ctx_destroy. */
+int kzgmi_ck_load(kzgmi_ctx* ctx, kzgmi_curve curve, const uint8_t* g1_powers, size_t n, kzgmi_ck** out);
+void kzgmi_ck_free(kzgmi_ck* ck);
+int kzgmi_commit(kzgmi_ctx* ctx, const kzgmi_ck* ck, const uint8_t* coeffs, size_t m, uint8_t* out);
+int kzgmi_commit_device(kzgmi_ctx* ctx, const kzgmi_ck* ck, const void* d_coeffs, size_t m,
+                        uint8_t* out);
 
 /* Optimal-ate pairing e(P, Q) (cubed for BLS12-381, as in the oracle), 12 Fp values in
  * tower order, big-endian: 576 B (BLS12-381) / 384 B (BN254).  Test/diagnostic utility. */

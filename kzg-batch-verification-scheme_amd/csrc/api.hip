@@ -88,7 +88,17 @@ struct kzgmi_ctx {
   bool table_ready[2] = {false, false};
   DevBuf lines_tmp, tmp;
   std::vector<kzgmi_srs*> srs_list;  // live SRS objects: detached (device memory freed) on destroy
+  std::vector<kzgmi_ck*> ck_list;    // live commit keys: same
 };
+
+// prover commit key: rows w = 0..15 of 2^(16 w)-shifted SRS points, [row][point] Montgomery affine
+struct kzgmi_ck {
+  int curve = 0;
+  size_t n = 0;
+  kzgmi_ctx* ctx = nullptr;
+  DevBuf pts, inf;
+};
+constexpr int CK_ROWS = 16;  // 16-bit windows of a 255-bit Fr scalar
 
 struct kzgmi_srs {
   int curve = 0;
@@ -156,8 +166,11 @@ int map_device_err(uint32_t e) {
 
 // ------------------------------------------------------------------------------ MSM core
 template <class Cv>
-int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl, uint32_t nsets, size_t emax, const MsmWindows& mw) {
+int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl, uint32_t nsets, size_t emax, const MsmWindows& mw,
+                 const Affine<Cv>* pts = nullptr, const uint8_t* inf = nullptr) {
   using XY = Xyzz<Cv>;
+  if (!pts) pts = s.pts.template as<Affine<Cv>>();  // default: the slot's converted points
+  if (!inf) inf = s.inf.template as<uint8_t>();
   const uint32_t NB = nsets * NBUCKETS;
   const size_t nchunks = (emax + ACC_CHUNK - 1) / ACC_CHUNK + 1;
   CHK(s.cnt.ensure((size_t)NB * 4));
@@ -177,12 +190,12 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl, uint32_t nsets, size
   CHK(s.res.ensure(2 * sizeof(XY)));
   hipStream_t st = s.stream;
   using L = Launch<Cv>;
-  L::sort(st, tl, nsets, s.inf.template as<uint8_t>(), s.coarse.template as<uint32_t>(), s.ent.template as<uint64_t>(),
+  L::sort(st, tl, nsets, inf, s.coarse.template as<uint32_t>(), s.ent.template as<uint64_t>(),
           s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.total.template as<uint32_t>(),
           s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>());
   mark(c, s, PH_SORT + 1);
   L::accumulate(st, nchunks, s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
-                s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.pts.template as<Affine<Cv>>(),
+                s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts,
                 s.buckets.template as<XY>(), s.pfirst.template as<XY>(), s.plast.template as<XY>());
   mark(c, s, PH_ACCUM + 1);
   L::reduce(st, nsets, s.cnt.template as<uint32_t>(), s.buckets.template as<XY>(), s.R.template as<XY>(),
@@ -405,6 +418,11 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
   for (int k = 0; k < 2; ++k) { c->table[k].release(); c->table_base[k].release(); }
   c->lines_tmp.release();
   c->tmp.release();
+  for (kzgmi_ck* ck : c->ck_list) {  // detach: later kzgmi_ck_free() only deletes the struct
+    ck->pts.release();
+    ck->inf.release();
+    ck->ctx = nullptr;
+  }
   for (kzgmi_srs* srs : c->srs_list) {  // detach: later kzgmi_srs_free() only deletes the struct
     srs->lines.release();
     srs->q.release();
@@ -607,6 +625,121 @@ int read_flags_sync(kzgmi_ctx* c, Slot& s) {
 }
 }  // namespace
 extern "C" {
+
+// ------------------------------------------------------------------------------ prover commit key
+int kzgmi_ck_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1_powers, size_t n, kzgmi_ck** out) {
+  CHK(check_ctx(c));
+  if (!g1_powers || !out || n == 0) return fail(KZGMI_ERR_ARG, "bad commit key argument");
+  if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "commit key too large (max 2^26 points)");
+  Slot& s = c->slots[0];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot 0 busy: call kzgmi_slot_wait first");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    using L = Launch<Cv>;
+    const size_t gb = g1_bytes(Cv::ID);
+    kzgmi_ck* ck = new kzgmi_ck();
+    ck->curve = Cv::ID;
+    ck->n = n;
+    ck->ctx = c;
+    int r = 0;
+    if ((r = ck->pts.ensure((size_t)CK_ROWS * n * sizeof(Affine<Cv>))) || (r = ck->inf.ensure((size_t)CK_ROWS * n)) ||
+        (r = s.stage.ensure(n * gb)) || (r = s.flags.ensure(16))) {
+      delete ck;
+      return r;
+    }
+    hipStream_t st = s.stream;
+    Affine<Cv>* pts = ck->pts.template as<Affine<Cv>>();
+    uint8_t* inf = ck->inf.template as<uint8_t>();
+    bool okk = hipMemcpyAsync(s.stage.p, g1_powers, n * gb, hipMemcpyHostToDevice, st) == hipSuccess &&
+               hipMemsetAsync(s.flags.p, 0, 16, st) == hipSuccess;
+    if (okk) {
+      L::convert_points(st, s.stage.template as<uint8_t>(), (uint32_t)n, pts, inf, s.flags.template as<uint32_t>() + 1);
+      for (int w = 1; w < CK_ROWS; ++w)
+        L::shift_points(st, pts + (size_t)(w - 1) * n, inf + (size_t)(w - 1) * n, (uint32_t)n, pts + (size_t)w * n,
+                        inf + (size_t)w * n);
+      okk = hipGetLastError() == hipSuccess &&
+            hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
+            hipStreamSynchronize(st) == hipSuccess;
+    }
+    if (!okk) {
+      delete ck;
+      return fail(KZGMI_ERR_DEVICE, "commit key upload/precompute failed");
+    }
+    if (int e = map_device_err((uint32_t)s.host_flags[1])) {
+      delete ck;
+      return e;
+    }
+    c->ck_list.push_back(ck);
+    *out = ck;
+    return 0;
+  });
+}
+
+void kzgmi_ck_free(kzgmi_ck* ck) {
+  if (!ck) return;
+  if (kzgmi_ctx* c = ck->ctx) {
+    (void)hipSetDevice(c->device);
+    auto& v = c->ck_list;
+    v.erase(std::remove(v.begin(), v.end(), ck), v.end());
+    ck->pts.release();
+    ck->inf.release();
+  }
+  delete ck;
+}
+
+int kzgmi_commit_device(kzgmi_ctx* c, const kzgmi_ck* ck, const void* d_coeffs, size_t m, uint8_t* out) {
+  CHK(check_ctx(c));
+  if (!ck || ck->ctx != c) return fail(KZGMI_ERR_ARG, "commit key does not belong to this context");
+  if (!out || (m && !d_coeffs)) return fail(KZGMI_ERR_ARG, "null argument");
+  if (m > ck->n) return fail(KZGMI_ERR_ARG, "more coefficients than commit-key points");
+  Slot& s = c->slots[0];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot 0 busy: call kzgmi_slot_wait first");
+  return dispatch(ck->curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    using L = Launch<Cv>;
+    const size_t gb = g1_bytes(Cv::ID);
+    hipStream_t st = s.stream;
+    CHK(s.flags.ensure(16));
+    CHK(s.outb.ensure(gb));
+    CHK(s.res.ensure(2 * sizeof(Xyzz<Cv>)));
+    HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
+    if (m == 0) {
+      HIPCHK(hipMemsetAsync(s.res.p, 0, sizeof(Xyzz<Cv>), st));  // zz = 0: infinity
+    } else {
+      CHK(s.scal_s.ensure(m * 32));
+      mark(c, s, 0);
+      L::convert_scalars(st, (const uint8_t*)d_coeffs, (uint32_t)m, s.scal_s.template as<uint32_t>(),
+                         s.flags.template as<uint32_t>() + 1);
+      mark(c, s, PH_SCALARS + 1);
+      // one class per 16-bit window w: the points of row w (2^(16 w) P_i) take digit w of the
+      // coefficient; every class feeds the same bucket set, so no per-window reduction and no
+      // window combination
+      TermList tl{};
+      for (int w = 0; w < CK_ROWS; ++w)
+        tl.c[w] = {(uint32_t)m, (uint32_t)(w * ck->n), 8, 1, 0, 8, s.scal_s.template as<uint32_t>(), (uint32_t)w};
+      tl.nclass = CK_ROWS;
+      tl.total = (uint32_t)(CK_ROWS * m);
+      MsmWindows mw{1, {0, 0}, {1, 0}};
+      CHK(run_msm_core<Cv>(c, s, tl, 1, (size_t)CK_ROWS * m + 16, mw, ck->pts.template as<Affine<Cv>>(),
+                           ck->inf.template as<uint8_t>()));
+    }
+    Launch<Cv>::encode_points(st, s.res.template as<Xyzz<Cv>>(), 1, s.outb.template as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    CHK(read_flags_sync(c, s));
+    HIPCHK(hipMemcpy(out, s.outb.p, gb, hipMemcpyDeviceToHost));
+    return 0;
+  });
+}
+
+int kzgmi_commit(kzgmi_ctx* c, const kzgmi_ck* ck, const uint8_t* coeffs, size_t m, uint8_t* out) {
+  CHK(check_ctx(c));
+  if (!ck || (m && !coeffs)) return fail(KZGMI_ERR_ARG, "null argument");
+  if (m == 0) return kzgmi_commit_device(c, ck, nullptr, 0, out);
+  Slot& s = c->slots[0];
+  CHK(s.stage.ensure(m * 32));
+  HIPCHK(hipMemcpyAsync(s.stage.p, coeffs, m * 32, hipMemcpyHostToDevice, s.stream));
+  return kzgmi_commit_device(c, ck, s.stage.p, m, out);
+}
 
 int kzgmi_msm_g1_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dpts, const void* dsc, size_t n, uint8_t* out) {
   CHK(check_ctx(c));

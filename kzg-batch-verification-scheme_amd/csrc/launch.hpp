@@ -55,6 +55,8 @@ struct Launch {
   static void pairing_check(hipStream_t st, const XY* res, const Line<Cv>* lines, const uint8_t* q_inf, int* ok);
   static void pairing_one(hipStream_t st, const AF* p, const uint8_t* p_inf, const Line<Cv>* lines,
                           const uint8_t* q_inf, uint8_t* out);
+  // ---- prover commit key (launch_gen.hip): row out = 2^16 * row in, affine
+  static void shift_points(hipStream_t st, const AF* in, const uint8_t* inf_in, uint32_t n, AF* out, uint8_t* inf_out);
   // ---- generators (launch_gen.hip)
   static void gen_table(hipStream_t st, XY* base, AF* table);
   static void gen_g1(hipStream_t st, const uint8_t* scalars, uint32_t n, const AF* table, uint8_t* out, uint32_t* err);

@@ -24,7 +24,7 @@ constexpr int WBITS = 16;                      // window width c
 constexpr int NBUCKETS = 1 << (WBITS - 1);     // signed digits: |d| in [1, 2^15]
 constexpr int ACC_CHUNK = 64;                  // entries per accumulation thread
 constexpr int SEG = 16;                        // buckets per reduction segment
-constexpr int MAX_CLASSES = 4;
+constexpr int MAX_CLASSES = 16;
 
 struct TermClass {
   uint32_t count;       // number of terms in the class
@@ -34,6 +34,8 @@ struct TermClass {
   uint32_t set_base;    // bucket set (= msm window) of window 0
   uint32_t scal_stride; // 0: one shared scalar for the whole class, else = scal_words
   const uint32_t* scal; // LE words, standard (non-Montgomery) form
+  uint32_t win_off;     // window of the scalar that local window 0 reads (fixed-base tables:
+                        // row w of 2^(16w)-shifted points reads digit w into one bucket set)
 };
 struct TermList {
   TermClass c[MAX_CLASSES];
@@ -110,7 +112,7 @@ static __global__ void __launch_bounds__(256) k_bin_count(TermList tl, const uin
   for (int j = 0; j < TILE_TERMS / 256; ++j) {
     uint32_t local = T.c * TILE_TERMS + j * 256 + threadIdx.x;
     if (local >= C.count || inf[C.pt_base + local]) continue;
-    int d = signed_digit(C, local, T.w);
+    int d = signed_digit(C, local, T.w + (int)C.win_off);
     if (d != 0) {
       uint32_t mag = (uint32_t)(d < 0 ? -d : d);
       atomicAdd(&hist[(mag - 1) >> COARSE_SHIFT], 1u);
@@ -170,7 +172,7 @@ static __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const u
     if (local >= C.count) continue;
     uint32_t pt = C.pt_base + local;
     if (inf[pt]) continue;
-    int d = signed_digit(C, local, T.w);
+    int d = signed_digit(C, local, T.w + (int)C.win_off);
     if (d == 0) continue;
     uint32_t mag = (uint32_t)(d < 0 ? -d : d);
     key[j] = set * NBUCKETS + (mag - 1);

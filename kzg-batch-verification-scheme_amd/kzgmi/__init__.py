@@ -70,6 +70,10 @@ def lib():
         "kzgmi_batch_verify_device_ex_async": ([vp, vp, c.c_int, vp, vp, vp, vp, sz, u8p, c.c_uint32], c.c_int),
         "kzgmi_g1_validate_device": ([vp, c.c_int, vp, sz, c.c_uint32], c.c_int),
         "kzgmi_g1_compress_device": ([vp, c.c_int, vp, sz, vp], c.c_int),
+        "kzgmi_ck_load": ([vp, c.c_int, u8p, sz, c.POINTER(c.c_void_p)], c.c_int),
+        "kzgmi_ck_free": ([vp], None),
+        "kzgmi_commit": ([vp, vp, u8p, sz, u8p], c.c_int),
+        "kzgmi_commit_device": ([vp, vp, vp, sz, u8p], c.c_int),
         "kzgmi_fs_challenge_device": ([vp, c.c_int, vp, vp, vp, vp, sz, c.c_uint32, u8p], c.c_int),
         "kzgmi_fs_chunk_digests_device": ([vp, c.c_int, vp, vp, vp, vp, sz, c.c_uint64, c.c_uint32, vp], c.c_int),
         "kzgmi_fs_challenge_from_digests_device": ([vp, c.c_int, vp, sz, c.c_uint64, u8p], c.c_int),
@@ -107,7 +111,8 @@ def exported_symbols():
         "kzgmi_ctx_destroy", "kzgmi_srs_load", "kzgmi_srs_free", "kzgmi_batch_verify",
         "kzgmi_batch_verify_device", "kzgmi_batch_verify_device_async", "kzgmi_slot_wait",
         "kzgmi_batch_verify_ex", "kzgmi_batch_verify_device_ex_async", "kzgmi_g1_validate_device",
-        "kzgmi_g1_compress_device", "kzgmi_fs_challenge_device", "kzgmi_fs_chunk_digests_device",
+        "kzgmi_g1_compress_device", "kzgmi_ck_load", "kzgmi_ck_free", "kzgmi_commit", "kzgmi_commit_device",
+        "kzgmi_fs_challenge_device", "kzgmi_fs_chunk_digests_device",
         "kzgmi_fs_challenge_from_digests_device",
         "kzgmi_last_combination", "kzgmi_msm_g1", "kzgmi_msm_g1_device", "kzgmi_partial_bytes",
         "kzgmi_batch_partial_device", "kzgmi_batch_combine_device", "kzgmi_batch_partial_device_async",
@@ -184,6 +189,22 @@ class Srs:
             pass
 
 
+class CommitKey:
+    """Prover commit key: [tau^i]_1 powers + fixed-base tables on the device."""
+    ctx: "Context"
+    curve: str
+    n: int
+    handle: ctypes.c_void_p
+
+    def __del__(self):
+        try:
+            if self.handle:
+                lib().kzgmi_ck_free(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
 class Context:
     """One GPU (device_id) with `slots` independent workspaces/streams."""
 
@@ -251,6 +272,32 @@ class Context:
                                                         _dptr(zs), _dptr(ys), _dptr(proofs), n,
                                                         _challenge_seed(seed, challenge),
                                                         _flags(compressed, subgroup_check, fiat_shamir, challenge)))
+
+    # ------------------------------------------------------------------ prover commit
+    def load_commit_key(self, curve: str, g1_powers: bytes, n: Optional[int] = None) -> CommitKey:
+        """g1_powers: n uncompressed G1 encodings [tau^i]_1 (host bytes)."""
+        pb = _host_bytes(g1_powers)
+        if n is None:
+            n = len(pb) // (2 * FP_BYTES[curve])
+        h = ctypes.c_void_p()
+        _check(lib().kzgmi_ck_load(self.handle, CURVES[curve], pb, n, ctypes.byref(h)))
+        ck = CommitKey()
+        ck.ctx, ck.curve, ck.n, ck.handle = self, curve, n, h
+        return ck
+
+    def commit(self, ck: CommitKey, coeffs, m: Optional[int] = None) -> bytes:
+        """sum_i coeff_i [tau^i]_1 for m <= ck.n coefficients (32 B canonical Fr each)."""
+        out = ctypes.create_string_buffer(2 * FP_BYTES[ck.curve])
+        if _is_device_tensor(coeffs):
+            if m is None:
+                m = coeffs.numel() // 32
+            _check(lib().kzgmi_commit_device(self.handle, ck.handle, _dptr(coeffs), m, out))
+        else:
+            cb = _host_bytes(coeffs)
+            if m is None:
+                m = len(cb) // 32
+            _check(lib().kzgmi_commit(self.handle, ck.handle, cb, m, out))
+        return out.raw
 
     # ------------------------------------------------------------------ Fiat-Shamir
     def fs_challenge(self, curve: str, commitments, zs, ys, proofs, n: int, compressed: bool = False) -> int:
