@@ -41,7 +41,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import kzgmi  # noqa: E402
-from kzgmi.distributed import ShardedPipeline, sharded_msm  # noqa: E402
+from kzgmi.distributed import ShardedMsmPipeline, ShardedPipeline  # noqa: E402
 
 METRIC = "batch-verifies/sec + G1 MSM pts/sec at n=2^20, BLS12-381; 1/2/4/8 GPU"
 HBM_PEAK = 8.0e12          # B/s, MI355X spec (MI355X_MICROARCH.md)
@@ -131,7 +131,7 @@ def main():
     ap.add_argument("--curve", default="bls12_381", choices=["bls12_381", "bn254"])
     ap.add_argument("--slots", type=int, default=0,
                     help="batches in flight (default 12 single-GPU; sharded 6 + 2 combine lanes)")
-    ap.add_argument("--msm-steps", type=int, default=5)
+    ap.add_argument("--msm-steps", type=int, default=24)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fs-steps", type=int, default=36,
@@ -332,21 +332,47 @@ def main():
                   "method": "16 resident rows of 2^(16w)-shifted SRS points, one bucket set, synchronous calls"}
         del ck
 
-    # ---- secondary: G1 MSM pts/s at n points per GPU (commitments as points, z as scalars)
-    msm_rate = None
+    # ---- secondary: G1 MSM pts/s at n points per GPU (commitments as points, z as scalars),
+    # pipelined over the same slots as the batch verifications (configs[1] throughput)
+    msm_rate, msm_latency_ms = None, None
     if args.msm_steps > 0:
-        def msm_step():
-            if world > 1:
-                sharded_msm(ctx, curve, Cm, z, n)
-            else:
-                ctx.msm_g1(curve, Cm, z, n=n)
-        msm_step()
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        msm_ref = ctx.msm_g1(curve, Cm, z, n=n)  # synchronous: single-MSM latency + reference
+        msm_latency_ms = (time.perf_counter() - a) * 1e3
+        msm_results = []
+        if world > 1:
+            mpipe = ShardedMsmPipeline(ctx, curve, slots, lanes)
+            submit = lambda: msm_results.extend(mpipe.submit(Cm, z, n))  # noqa: E731
+            mdrain = lambda: msm_results.extend(mpipe.drain())  # noqa: E731
+        else:
+            mk = [0]
+
+            def submit():
+                sl = mk[0] % slots
+                if mk[0] >= slots:
+                    msm_results.append(ctx.msm_wait(sl))
+                ctx.msm_g1_async(curve, sl, Cm, z, n)
+                mk[0] += 1
+
+            def mdrain():
+                for i in range(min(mk[0], slots)):
+                    msm_results.append(ctx.msm_wait((mk[0] + i) % slots))
+                mk[0] = 0
+        for _ in range(min(slots, args.msm_steps)):
+            submit()
+        mdrain()
         barrier()
         a = time.perf_counter()
         for _ in range(args.msm_steps):
-            msm_step()
+            submit()
+        mdrain()
         barrier()
         dt = time.perf_counter() - a
+        # every pipelined result equals the synchronous one (world 1) / the first global one
+        want = msm_ref if world == 1 else msm_results[0]
+        assert len(msm_results) == args.msm_steps + min(slots, args.msm_steps), len(msm_results)
+        assert all(r == want for r in msm_results), "pipelined MSM result differs"
         if world > 1:
             t = torch.tensor([dt], dtype=torch.float64, device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -442,6 +468,8 @@ def main():
             "tuples_per_s": value * n,
             "msm_pts_per_s": msm_rate,
             "msm_n_per_gpu": n,
+            "msm_single_latency_ms": msm_latency_ms,
+            "msm_method": "pipelined over the batch slots (kzgmi_msm_g1_device_async), 255-bit scalars",
             "single_batch_latency_ms": lat,
             "phase_ms_avg_in_timed_region": phases,
             "phase_ms_single_batch": phases_single,

@@ -148,6 +148,14 @@ int kzgmi_msm_g1(kzgmi_ctx* ctx, kzgmi_curve curve, const uint8_t* points, const
 int kzgmi_msm_g1_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_points,
                         const void* d_scalars, size_t n, uint8_t* out);
 
+/* Pipelined MSM (configs[1] throughput): enqueue on workspace `slot` and return at once;
+ * kzgmi_msm_wait() blocks until that slot's result is ready and writes the G1 encoding.
+ * MSMs on different slots overlap on the GPU exactly like the async batch verifications
+ * (kzgmi_slot_wait also completes an MSM job, discarding the point). */
+int kzgmi_msm_g1_device_async(kzgmi_ctx* ctx, kzgmi_curve curve, int slot, const void* d_points,
+                              const void* d_scalars, size_t n);
+int kzgmi_msm_wait(kzgmi_ctx* ctx, int slot, uint8_t* out);
+
 /* ---- multi-GPU point-range sharding ----------------------------
  * A rank verifying tuples [index_offset, index_offset + n) of a global batch writes its
  * partial (A_k, B_k) as 2 opaque partial-point records (kzgmi_partial_bytes() each) to
@@ -171,6 +179,12 @@ int kzgmi_msm_partial_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_po
                              const void* d_scalars, size_t n, void* d_partial_out);
 int kzgmi_msm_combine_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_partials,
                              int n_parts, uint8_t* out);
+/* Pipelined forms: the partial completes with kzgmi_slot_wait, the combine (sum of the
+ * gathered records, encoded) with kzgmi_msm_wait. */
+int kzgmi_msm_partial_device_async(kzgmi_ctx* ctx, kzgmi_curve curve, int slot, const void* d_points,
+                                   const void* d_scalars, size_t n, void* d_partial_out);
+int kzgmi_msm_combine_device_async(kzgmi_ctx* ctx, kzgmi_curve curve, int slot,
+                                   const void* d_partials, int n_parts);
 
 /* prover-side commitments with a fixed SRS base.  kzgmi_ck_load uploads
  * n G1 powers ([tau^i]_1, host encodings, validated) and precomputes 16 rows of 2^(16 w)-shifted

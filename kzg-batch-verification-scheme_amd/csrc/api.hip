@@ -69,10 +69,12 @@ struct Slot {
   DevBuf buckets, pfirst, plast, R, U, scratch, winsum, res, flags, stage, outb;
   DevBuf fs_leaves, fs_tmp, fs_top, pow, chal;  // Fiat-Shamir / powers-of-r randomisers
   int* host_flags = nullptr;  // pinned: [ok, err]
+  uint8_t* host_out = nullptr;  // pinned: encoded MSM result of an async MSM job
   hipEvent_t ev[kNumPhases + 1] = {};
   bool ev_used[kNumPhases + 1] = {};
   bool pending = false;
   bool partial_job = false;  // pending job produces a partial record, not a verdict
+  bool msm_job = false;      // pending job is an MSM whose encoded result lands in host_out
   int curve = 0;
 };
 
@@ -328,6 +330,7 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
   s.pending = true;
   s.partial_job = d_partial_out != nullptr;
+  s.msm_job = false;
   s.curve = Cv::ID;
   return 0;
 }
@@ -338,7 +341,7 @@ int finish_slot(kzgmi_ctx* c, Slot& s, int* ok_out) {
   collect_phases(c, s);
   int e = map_device_err((uint32_t)s.host_flags[1]);
   if (e) return e;
-  if (ok_out) *ok_out = s.partial_job ? 1 : s.host_flags[0];
+  if (ok_out) *ok_out = (s.partial_job || s.msm_job) ? 1 : s.host_flags[0];
   return 0;
 }
 
@@ -391,7 +394,8 @@ int kzgmi_ctx_create(kzgmi_ctx** out, int device_id, int pipeline_slots) {
   c->slots.resize(pipeline_slots);
   for (auto& s : c->slots) {
     if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&s.host_flags, 16, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc((void**)&s.host_flags, 16, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&s.host_out, 128, hipHostMallocDefault) != hipSuccess) {
       kzgmi_ctx_destroy(c);
       return fail(KZGMI_ERR_DEVICE, "stream/pinned allocation failed");
     }
@@ -413,6 +417,7 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
     for (auto& e : s.ev)
       if (e) (void)hipEventDestroy(e);
     if (s.host_flags) (void)hipHostFree(s.host_flags);
+    if (s.host_out) (void)hipHostFree(s.host_out);
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
   for (int k = 0; k < 2; ++k) { c->table[k].release(); c->table_base[k].release(); }
@@ -518,6 +523,7 @@ int kzgmi_batch_verify_device_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int s
     s.host_flags[1] = 0;
     s.pending = true;
     s.partial_job = false;
+    s.msm_job = false;
     return 0;
   }
   return dispatch(srs->curve, [&](auto cv) -> int {
@@ -764,6 +770,48 @@ int kzgmi_msm_g1_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dpts, const
   });
 }
 
+int kzgmi_msm_g1_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, const void* dpts, const void* dsc,
+                              size_t n) {
+  CHK(check_ctx(c, slot));
+  if (n && (!dpts || !dsc)) return fail(KZGMI_ERR_ARG, "null argument");
+  if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "MSM too large (max 2^26 points per call)");
+  Slot& s = c->slots[slot];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_msm_wait first");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    const size_t gb = g1_bytes(Cv::ID);
+    if (n == 0) {
+      HIPCHK(hipStreamSynchronize(s.stream));  // host_out/host_flags may still be copy targets
+      memset(s.host_out, 0, gb);
+      if (Cv::ID == 0) s.host_out[0] = 0x40;
+      s.host_flags[0] = 1;
+      s.host_flags[1] = 0;
+    } else {
+      CHK(enqueue_msm<Cv>(c, s, dpts, dsc, n));
+      CHK(s.outb.ensure(gb));
+      Launch<Cv>::encode_points(s.stream, s.res.template as<Xyzz<Cv>>(), 1, s.outb.template as<uint8_t>());
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(s.host_out, s.outb.p, gb, hipMemcpyDeviceToHost, s.stream));
+      HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, s.stream));
+    }
+    s.pending = true;
+    s.partial_job = false;
+    s.msm_job = true;
+    s.curve = Cv::ID;
+    return 0;
+  });
+}
+
+int kzgmi_msm_wait(kzgmi_ctx* c, int slot, uint8_t* out) {
+  CHK(check_ctx(c, slot));
+  Slot& s = c->slots[slot];
+  if (!s.pending || !s.msm_job) return fail(KZGMI_ERR_ARG, "slot has no pending MSM");
+  int ok = 0;
+  CHK(finish_slot(c, s, &ok));
+  if (out) memcpy(out, s.host_out, g1_bytes(s.curve));
+  return 0;
+}
+
 int kzgmi_msm_g1(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* points, const uint8_t* scalars, size_t n,
                  uint8_t* out) {
   CHK(check_ctx(c));
@@ -809,6 +857,7 @@ int kzgmi_batch_partial_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slo
       s.host_flags[1] = 0;
       s.pending = true;
       s.partial_job = true;
+      s.msm_job = false;
       return 0;
     }
     return enqueue_batch<Cv>(c, s, srs, dC, dz, dy, dpi, n, seed, index_offset, d_partial_out, flags);
@@ -844,6 +893,7 @@ int kzgmi_batch_combine_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slo
     HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
     s.pending = true;
     s.partial_job = false;
+    s.msm_job = false;
     s.curve = Cv::ID;
     return 0;
   });
@@ -884,6 +934,7 @@ int kzgmi_g1_validate_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_poin
     HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
     s.pending = true;
     s.partial_job = true;
+    s.msm_job = false;
     return finish_slot(c, s, nullptr);
   });
 }
@@ -979,6 +1030,59 @@ int kzgmi_msm_partial_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dpts, 
     CHK(enqueue_msm<Cv>(c, s, dpts, dsc, n));
     HIPCHK(hipMemcpyAsync(d_partial_out, s.res.p, sizeof(Xyzz<Cv>), hipMemcpyDeviceToDevice, s.stream));
     return read_flags_sync(c, s);
+  });
+}
+
+int kzgmi_msm_partial_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, const void* dpts, const void* dsc,
+                                   size_t n, void* d_partial_out) {
+  CHK(check_ctx(c, slot));
+  if (!d_partial_out || (n && (!dpts || !dsc))) return fail(KZGMI_ERR_ARG, "bad argument");
+  if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "MSM too large (max 2^26 points per call)");
+  Slot& s = c->slots[slot];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_slot_wait first");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    if (n == 0) {
+      HIPCHK(hipStreamSynchronize(s.stream));
+      HIPCHK(hipMemsetAsync(d_partial_out, 0, sizeof(Xyzz<Cv>), s.stream));  // ZZ = 0: infinity
+      s.host_flags[0] = 1;
+      s.host_flags[1] = 0;
+    } else {
+      CHK(enqueue_msm<Cv>(c, s, dpts, dsc, n));
+      HIPCHK(hipMemcpyAsync(d_partial_out, s.res.p, sizeof(Xyzz<Cv>), hipMemcpyDeviceToDevice, s.stream));
+      HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, s.stream));
+    }
+    s.pending = true;
+    s.partial_job = true;
+    s.msm_job = false;
+    s.curve = Cv::ID;
+    return 0;
+  });
+}
+
+int kzgmi_msm_combine_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, const void* d_partials, int n_parts) {
+  CHK(check_ctx(c, slot));
+  if (!d_partials || n_parts < 1) return fail(KZGMI_ERR_ARG, "bad argument");
+  Slot& s = c->slots[slot];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_msm_wait first");
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    using XY = Xyzz<Cv>;
+    const size_t gb = g1_bytes(Cv::ID);
+    CHK(s.res.ensure(2 * sizeof(XY)));
+    CHK(s.outb.ensure(gb));
+    CHK(s.flags.ensure(16));
+    HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));
+    Launch<Cv>::sum_partials(s.stream, (const XY*)d_partials, (uint32_t)n_parts, 1, 1, s.res.template as<XY>());
+    Launch<Cv>::encode_points(s.stream, s.res.template as<XY>(), 1, s.outb.template as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(s.host_out, s.outb.p, gb, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, s.stream));
+    s.pending = true;
+    s.partial_job = false;
+    s.msm_job = true;
+    s.curve = Cv::ID;
+    return 0;
   });
 }
 

@@ -81,6 +81,10 @@ def lib():
         "kzgmi_last_combination": ([vp, u8p, u8p], c.c_int),
         "kzgmi_msm_g1": ([vp, c.c_int, u8p, u8p, sz, u8p], c.c_int),
         "kzgmi_msm_g1_device": ([vp, c.c_int, vp, vp, sz, u8p], c.c_int),
+        "kzgmi_msm_g1_device_async": ([vp, c.c_int, c.c_int, vp, vp, sz], c.c_int),
+        "kzgmi_msm_wait": ([vp, c.c_int, u8p], c.c_int),
+        "kzgmi_msm_partial_device_async": ([vp, c.c_int, c.c_int, vp, vp, sz, vp], c.c_int),
+        "kzgmi_msm_combine_device_async": ([vp, c.c_int, c.c_int, vp, c.c_int], c.c_int),
         "kzgmi_partial_bytes": ([c.c_int], sz),
         "kzgmi_batch_partial_device": ([vp, vp, vp, vp, vp, vp, sz, c.c_uint64, u8p, vp], c.c_int),
         "kzgmi_batch_combine_device": ([vp, vp, vp, c.c_int, ip], c.c_int),
@@ -114,7 +118,8 @@ def exported_symbols():
         "kzgmi_g1_compress_device", "kzgmi_ck_load", "kzgmi_ck_free", "kzgmi_commit", "kzgmi_commit_device",
         "kzgmi_fs_challenge_device", "kzgmi_fs_chunk_digests_device",
         "kzgmi_fs_challenge_from_digests_device",
-        "kzgmi_last_combination", "kzgmi_msm_g1", "kzgmi_msm_g1_device", "kzgmi_partial_bytes",
+        "kzgmi_last_combination", "kzgmi_msm_g1", "kzgmi_msm_g1_device", "kzgmi_msm_g1_device_async",
+        "kzgmi_msm_wait", "kzgmi_msm_partial_device_async", "kzgmi_msm_combine_device_async", "kzgmi_partial_bytes",
         "kzgmi_batch_partial_device", "kzgmi_batch_combine_device", "kzgmi_batch_partial_device_async",
         "kzgmi_batch_combine_device_async", "kzgmi_msm_partial_device",
         "kzgmi_msm_combine_device", "kzgmi_pairing", "kzgmi_gen_g1", "kzgmi_gen_tuples",
@@ -356,6 +361,19 @@ class Context:
             _check(lib().kzgmi_msm_g1(self.handle, CURVES[curve], pb, sb, n, out))
         return out.raw
 
+    def msm_g1_async(self, curve: str, slot: int, points, scalars, n: int):
+        """Enqueue sum k_i P_i (device tensors) on workspace `slot`; msm_wait(slot) returns it."""
+        self._msm_curve = getattr(self, "_msm_curve", {})
+        self._msm_curve[slot] = curve
+        _check(lib().kzgmi_msm_g1_device_async(self.handle, CURVES[curve], int(slot), _dptr(points),
+                                               _dptr(scalars), int(n)))
+
+    def msm_wait(self, slot: int) -> bytes:
+        g1b = 2 * FP_BYTES[self._msm_curve[slot]]
+        out = ctypes.create_string_buffer(g1b)
+        _check(lib().kzgmi_msm_wait(self.handle, int(slot), out))
+        return out.raw
+
     # ------------------------------------------------------------------ multi-GPU pieces
     def tensor_device(self):
         import torch
@@ -392,6 +410,16 @@ class Context:
     def msm_partial(self, curve: str, points, scalars, n: int, out):
         _check(lib().kzgmi_msm_partial_device(self.handle, CURVES[curve], _dptr(points), _dptr(scalars), n,
                                               _dptr(out)))
+
+    def msm_partial_async(self, curve: str, slot: int, points, scalars, n: int, out):
+        _check(lib().kzgmi_msm_partial_device_async(self.handle, CURVES[curve], int(slot), _dptr(points),
+                                                    _dptr(scalars), int(n), _dptr(out)))
+
+    def msm_combine_async(self, curve: str, slot: int, partials, n_parts: int):
+        self._msm_curve = getattr(self, "_msm_curve", {})
+        self._msm_curve[slot] = curve
+        _check(lib().kzgmi_msm_combine_device_async(self.handle, CURVES[curve], int(slot), _dptr(partials),
+                                                    int(n_parts)))
 
     def msm_combine(self, curve: str, partials, n_parts: int) -> bytes:
         out = ctypes.create_string_buffer(2 * FP_BYTES[curve])

@@ -175,3 +175,65 @@ def sharded_msm(backend, curve: str, points, scalars, n_local: int, group=None) 
     gathered = torch.empty(world * pb, dtype=torch.uint8, device=dev)
     dist.all_gather_into_tensor(gathered, local, group=group)
     return backend.msm_combine(curve, gathered, world)
+
+
+class ShardedMsmPipeline:
+    """Several global MSMs in flight per rank (the MSM counterpart of ShardedPipeline): the
+    shard partial of MSM k runs on slot k % slots; when the slot comes round its partial
+    record is all-gathered and summed + encoded on combine lane j % lanes (context slots
+    slots .. slots+lanes-1), collected when the lane is reused.  Results (G1 encodings, the
+    same on every rank) come back in submission order."""
+
+    def __init__(self, backend, curve: str, slots: int = 3, lanes: int = 2, group=None):
+        import torch
+        import torch.distributed as dist
+        self.backend, self.curve, self.group = backend, curve, group
+        self.slots, self.lanes = slots, lanes
+        self.world = dist.get_world_size(group)
+        pb = backend.partial_bytes(curve)
+        self.dev = backend.tensor_device()
+        self.local = [torch.empty(pb, dtype=torch.uint8, device=self.dev) for _ in range(slots)]
+        self.gathered = [torch.empty(self.world * pb, dtype=torch.uint8, device=self.dev) for _ in range(lanes)]
+        self.pending = [False] * slots
+        self.lane_pending = [False] * lanes
+        self.k = 0
+        self.j = 0
+
+    def _collect_lane(self, lane: int, out):
+        if self.lane_pending[lane]:
+            out.append(self.backend.msm_wait(self.slots + lane))
+            self.lane_pending[lane] = False
+
+    def _gather_and_combine(self, s: int, out):
+        import torch
+        import torch.distributed as dist
+        self.backend.wait(s)
+        self.pending[s] = False
+        lane = self.j % self.lanes
+        self.j += 1
+        self._collect_lane(lane, out)
+        dist.all_gather_into_tensor(self.gathered[lane], self.local[s], group=self.group)
+        if str(self.dev).startswith("cuda"):
+            torch.cuda.current_stream().synchronize()
+        self.backend.msm_combine_async(self.curve, self.slots + lane, self.gathered[lane], self.world)
+        self.lane_pending[lane] = True
+
+    def submit(self, points, scalars, n_local: int):
+        s = self.k % self.slots
+        self.k += 1
+        done = []
+        if self.pending[s]:
+            self._gather_and_combine(s, done)
+        self.backend.msm_partial_async(self.curve, s, points, scalars, n_local, self.local[s])
+        self.pending[s] = True
+        return done
+
+    def drain(self):
+        out = []
+        for i in range(self.slots):
+            s = (self.k + i) % self.slots
+            if self.pending[s]:
+                self._gather_and_combine(s, out)
+        for i in range(self.lanes):
+            self._collect_lane((self.j + i) % self.lanes, out)
+        return out

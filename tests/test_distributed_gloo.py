@@ -102,6 +102,30 @@ class OracleBackend:
                                self.g2, self.tau_g2)
 
 
+    # MSM pieces (kzgmi.distributed.ShardedMsmPipeline): one G1 encoding per partial record
+    def msm_partial_async(self, curve, slot, points, scalars, n, out):
+        import torch
+        from oracle import oracle as O
+        g1b = 2 * self.C.fp_bytes
+        P = O.msm_g1(curve, bytes(points.numpy().tobytes()[:n * g1b]), bytes(scalars.numpy().tobytes()[:n * 32]), n)
+        out.copy_(torch.frombuffer(bytearray(P), dtype=torch.uint8))
+        self._slot_result = getattr(self, "_slot_result", {})
+        self._slot_result[slot] = True
+
+    def msm_combine_async(self, curve, slot, gathered, n_parts):
+        from oracle.pyspec import curves as pc
+        from oracle.pyspec import kzg as pk
+        raw = gathered.numpy().tobytes()
+        g1b = 2 * self.C.fp_bytes
+        S = None
+        for k in range(n_parts):
+            S = pc.g1_add(S, pk.g1_from_bytes(raw[k * g1b:(k + 1) * g1b], self.C), self.C)
+        self._slot_result[slot] = pk.g1_to_bytes(S, self.C)
+
+    def msm_wait(self, slot):
+        return self._slot_result.pop(slot)
+
+
 class FakeSrs:
     def __init__(self, curve):
         self.curve = curve
@@ -219,6 +243,40 @@ def _fs_worker(rank, world, port, curve, n_total, tau, corrupt, result_q):
     dist.destroy_process_group()
 
 
+def _msm_worker(rank, world, port, curve, n_total, result_q):
+    import random
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "kzg-batch-verification-scheme_amd"))
+    import torch
+    import torch.distributed as dist
+    from kzgmi.distributed import ShardedMsmPipeline, shard_range
+    from oracle import oracle as O
+    from oracle.pyspec import curves as pc
+    from oracle.pyspec import kzg as pk
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    C = pc.CURVES[curve]
+    rng = random.Random(9)  # same global inputs on every rank
+    pts = O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(n_total)), n_total)
+    scs = [b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(n_total)) for _ in range(2)]
+    want = [O.msm_g1(curve, pts, sc, n_total) for sc in scs]
+    off, cnt = shard_range(n_total, world, rank)
+    g1b = 2 * C.fp_bytes
+    t = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8)  # noqa: E731
+    lp = t(pts[off * g1b:(off + cnt) * g1b] or bytes(1))
+    ls = [t(sc[off * 32:(off + cnt) * 32] or bytes(1)) for sc in scs]
+    pipe = ShardedMsmPipeline(OracleBackend(curve, None, None), curve, slots=2, lanes=2)
+    order = [0, 1, 1, 0, 0]
+    out = []
+    for b in order:
+        out += pipe.submit(lp, ls[b], cnt)
+    out += pipe.drain()
+    dist.destroy_process_group()
+    result_q.put((rank, out == [want[b] for b in order]))
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -280,3 +338,20 @@ def test_sharded_fiat_shamir_world2(n_total, corrupt, expect):
         assert p.exitcode == 0
     res = sorted(q.get() for _ in range(2))
     assert [(same, ok) for _, same, ok in res] == [(True, expect)] * 2
+
+
+def test_sharded_msm_pipeline_world2():
+    """ShardedMsmPipeline across 2 gloo ranks: shard partials, all-gather, combine lanes;
+    every rank gets the global MSM of every submission, in order."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_msm_worker, args=(r, 2, port, "bls12_381", 37, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    res = sorted(q.get() for _ in range(2))
+    assert [ok for _, ok in res] == [True, True]

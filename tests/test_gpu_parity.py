@@ -201,6 +201,32 @@ def test_async_slots(ctx, curve, torch_dev):
     assert ctx.wait(1) is False
 
 
+@pytest.mark.parametrize("curve", CURVES)
+def test_async_msm_slots(ctx, curve, torch_dev):
+    """Pipelined MSM: two different MSMs in flight on slots 0/1, each bit-exact vs the oracle;
+    the empty MSM and a slot reused after wait; misuse errors."""
+    import kzgmi
+    torch = torch_dev
+    C = pc.CURVES[curve]
+    rng = random.Random(71)
+    n = 1500
+    pts = O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(n)), n)
+    sc0 = b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(n))
+    sc1 = b"".join(pk.fr_to_bytes(rng.randrange(1 << 64)) for _ in range(n))
+    dev = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).cuda()  # noqa: E731
+    dp, d0, d1 = dev(pts), dev(sc0), dev(sc1)
+    ctx.msm_g1_async(curve, 0, dp, d0, n)
+    ctx.msm_g1_async(curve, 1, dp, d1, n - 7)
+    with pytest.raises(kzgmi.KzgmiError):
+        ctx.msm_g1_async(curve, 0, dp, d0, n)  # slot busy
+    assert ctx.msm_wait(1) == O.msm_g1(curve, pts[:(n - 7) * 2 * C.fp_bytes], sc1[:(n - 7) * 32], n - 7)
+    assert ctx.msm_wait(0) == O.msm_g1(curve, pts, sc0, n)
+    with pytest.raises(kzgmi.KzgmiError):
+        ctx.msm_wait(0)  # nothing pending
+    ctx.msm_g1_async(curve, 0, dp, d0, 0)
+    assert ctx.msm_wait(0) == O.msm_g1(curve, b"", b"", 0)
+
+
 def test_sharded_partials_equal_unsharded(ctx, torch_dev):
     """Multi-GPU decomposition on one device: 3 shards + combine == single batch."""
     torch = torch_dev
@@ -262,6 +288,44 @@ def test_sharded_pipeline_rccl_world1(ctx, torch_dev):
             out += pipe.submit(Cm, z, ybad if b in (1, 4) else y, P, n, 0, seed)
         out += pipe.drain()
         assert out == [True, False, True, True, False]
+    finally:
+        if created:
+            dist.destroy_process_group()
+
+
+def test_sharded_msm_pipeline_rccl_world1(ctx, torch_dev):
+    """kzgmi.distributed.ShardedMsmPipeline over a world-1 RCCL group: async shard partials,
+    all-gather, async combine; results in submission order, bit-exact vs the oracle."""
+    import socket
+    import torch.distributed as dist
+    from kzgmi.distributed import ShardedMsmPipeline
+    torch = torch_dev
+    curve = "bls12_381"
+    C = pc.CURVES[curve]
+    rng = random.Random(72)
+    n = 900
+    pts = O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(n)), n)
+    scs = [b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(n)) for _ in range(2)]
+    want = [O.msm_g1(curve, pts, sc, n) for sc in scs]
+    dev = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).cuda()  # noqa: E731
+    dp, dsc = dev(pts), [dev(sc) for sc in scs]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    created = not dist.is_initialized()
+    if created:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        pipe = ShardedMsmPipeline(ctx, curve, slots=1, lanes=1)
+        out = []
+        order = [0, 1, 1, 0, 1]
+        for b in order:
+            out += pipe.submit(dp, dsc[b], n)
+        out += pipe.drain()
+        assert out == [want[b] for b in order]
     finally:
         if created:
             dist.destroy_process_group()
