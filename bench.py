@@ -132,6 +132,8 @@ def main():
     ap.add_argument("--slots", type=int, default=0,
                     help="batches in flight (default 12 single-GPU; sharded 6 + 2 combine lanes)")
     ap.add_argument("--msm-steps", type=int, default=24)
+    ap.add_argument("--glv-batch", type=int, default=1,
+                    help="GLV split of s_i / t (/ r^i) in batch verification (MSMs always use GLV)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fs-steps", type=int, default=36,
@@ -163,6 +165,7 @@ def main():
     slots = args.slots if args.slots else (6 if sharded else 12)
     lanes = 2 if sharded else 0
     ctx = kzgmi.Context(local, slots + lanes)  # + the combine lanes
+    ctx.set_glv(msm=True, batch=bool(args.glv_batch))
     g2 = kzgmi.G2_GENERATOR[curve]
     tg2 = ctx.g2_mul(curve, g2, TAU)
     cpu_baseline.tg2 = tg2
@@ -460,6 +463,7 @@ def main():
             "tuples_per_gpu": n,
             "global_batch": world * n,
             "pipeline_slots": slots,
+            "glv": {"msm": True, "batch": bool(args.glv_batch)},
             "parallelism": "point-range shards" + (", RCCL all_gather of partial sums" if sharded else ""),
         },
         "roofline": roofline,

@@ -68,6 +68,7 @@ struct Slot {
   DevBuf pts, inf, scal_r, scal_s, scal_t, tpart, cnt, off, coarse, ent, total, sval, skey;
   DevBuf buckets, pfirst, plast, R, U, scratch, winsum, res, flags, stage, outb;
   DevBuf fs_leaves, fs_tmp, fs_top, pow, chal;  // Fiat-Shamir / powers-of-r randomisers
+  DevBuf glv_r, glv_s, glv_t;                    // GLV half scalars (glv.hpp): [h0 x n | h1 x n]
   int* host_flags = nullptr;  // pinned: [ok, err]
   uint8_t* host_out = nullptr;  // pinned: encoded MSM result of an async MSM job
   hipEvent_t ev[kNumPhases + 1] = {};
@@ -84,6 +85,8 @@ struct kzgmi_ctx {
   int device = 0;
   std::vector<Slot> slots;
   bool profiling = false;
+  bool glv_msm = true;     // GLV split of full Fr scalars in kzgmi_msm_g1* 
+  bool glv_batch = true;   // ... and of s_i, t (and r^i) in batch verification (kzgmi_set_glv)
   double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
   int phase_calls = 0;
   DevBuf table[2], table_base[2];
@@ -259,11 +262,18 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
                   uint32_t flags) {
   using XY = Xyzz<Cv>;
   using FrF = Fp<typename Cv::FrP>;
-  const size_t npts = 2 * n + 1;
+  const bool glv = c->glv_batch;
+  const size_t PH = 2 * n + 1;  // GLV: phi(pts[j]) at pts[PH + j]
+  const size_t npts = glv ? 2 * PH : PH;
   using L = Launch<Cv>;
   CHK(s.pts.ensure(npts * sizeof(Affine<Cv>)));
   CHK(s.inf.ensure(npts));
   const bool powers = (flags & (KZGMI_FLAG_POWERS | KZGMI_FLAG_FIAT_SHAMIR)) != 0;
+  if (glv) {
+    CHK(s.glv_s.ensure(n * 32));
+    CHK(s.glv_t.ensure(32));
+    if (powers) CHK(s.glv_r.ensure(n * 32));
+  }
   CHK(s.scal_r.ensure(n * (powers ? 32 : 16)));
   CHK(s.scal_s.ensure(n * 32));
   CHK(s.scal_t.ensure(32));
@@ -284,6 +294,7 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   }
   if (flags & KZGMI_FLAG_SUBGROUP_CHECK) L::subgroup_check(st, pts, inf, (uint32_t)(2 * n), err);
   L::set_generator(st, pts + 2 * n, inf + 2 * n);
+  if (glv) L::endo_points(st, pts, inf, (uint32_t)PH, pts + PH, inf + PH);
   mark(c, s, PH_CONVERT + 1);
   if (flags & KZGMI_FLAG_FIAT_SHAMIR) {  // r from the transcript of this (whole) batch
     const uint32_t* digests = nullptr;
@@ -301,24 +312,57 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
     L::scalar_prep(st, seed, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n,
                    s.scal_r.template as<uint32_t>(), s.scal_s.template as<uint32_t>(), s.tpart.p,
                    s.scal_t.template as<uint32_t>(), err);
+  const uint32_t nn = (uint32_t)n;
+  uint32_t* gs = s.glv_s.template as<uint32_t>();
+  uint32_t* gt = s.glv_t.template as<uint32_t>();
+  uint32_t* gr = s.glv_r.template as<uint32_t>();
+  if (glv) {
+    L::glv_split(st, s.scal_s.template as<uint32_t>(), 8, nn, gs, gs + 4 * (size_t)n);
+    L::glv_split(st, s.scal_t.template as<uint32_t>(), 8, 1, gt, gt + 4);
+    if (powers) L::glv_split(st, s.scal_r.template as<uint32_t>(), 8, nn, gr, gr + 4 * (size_t)n);
+  }
   mark(c, s, PH_SCALARS + 1);
   TermList tl{};
-  const uint32_t nn = (uint32_t)n;
-  if (!powers) {  // 127-bit r_i: MSM#0 in 8 windows (sets 0..7), MSM#1 in 16 (sets 8..23)
+  const uint32_t ph = (uint32_t)PH;
+  if (glv) {  // every MSM in 8 windows of half scalars: sets 0..7 (MSM#0), 8..15 (MSM#1)
+    const uint32_t* rr = s.scal_r.template as<uint32_t>();
+    uint32_t k = 0;
+    if (!powers) {
+      tl.c[k++] = {nn, 0, 4, 8, 0, 4, rr};                     // MSM#0: r_i pi_i
+      tl.c[k++] = {nn, nn, 4, 8, 8, 4, rr};                    // MSM#1: r_i C_i
+    } else {
+      tl.c[k++] = {nn, 0, 4, 8, 0, 4, gr};                     // MSM#0: r_i pi_i = h0 pi + h1 phi(pi)
+      tl.c[k++] = {nn, ph, 4, 8, 0, 4, gr + 4 * (size_t)n};
+      tl.c[k++] = {nn, nn, 4, 8, 8, 4, gr};                    // MSM#1: r_i C_i
+      tl.c[k++] = {nn, ph + nn, 4, 8, 8, 4, gr + 4 * (size_t)n};
+    }
+    tl.c[k++] = {nn, 0, 4, 8, 8, 4, gs};                       //        s_i pi_i
+    tl.c[k++] = {nn, ph, 4, 8, 8, 4, gs + 4 * (size_t)n};
+    tl.c[k++] = {1, 2 * nn, 4, 8, 8, 0, gt};                   //        -t G1
+    tl.c[k++] = {1, ph + 2 * nn, 4, 8, 8, 0, gt + 4};
+    tl.nclass = k;
+    tl.total = 0;
+    for (uint32_t j = 0; j < k; ++j) tl.total += tl.c[j].count;
+    const MsmWindows mw{2, {0, 8}, {8, 8}};
+    CHK(run_msm_core<Cv>(c, s, tl, 16, (size_t)(powers ? 48 : 32) * n + 16, mw));
+  } else if (!powers) {  // 127-bit r_i: MSM#0 in 8 windows (sets 0..7), MSM#1 in 16 (sets 8..23)
     tl.c[0] = {nn, 0, 4, 8, 0, 4, s.scal_r.template as<uint32_t>()};          // MSM#0: r_i pi_i
     tl.c[1] = {nn, nn, 4, 8, 8, 4, s.scal_r.template as<uint32_t>()};         // MSM#1: r_i C_i
     tl.c[2] = {nn, 0, 8, 16, 8, 8, s.scal_s.template as<uint32_t>()};         //        s_i pi_i
     tl.c[3] = {1, 2 * nn, 8, 16, 8, 0, s.scal_t.template as<uint32_t>()};     //        -t G1
-  } else {        // r_i = r^i, full Fr: both MSMs in 16 windows (sets 0..15, 16..31)
+  }
+  if (!glv && powers) {  // r_i = r^i, full Fr: both MSMs in 16 windows (sets 0..15, 16..31)
     tl.c[0] = {nn, 0, 8, 16, 0, 8, s.scal_r.template as<uint32_t>()};
     tl.c[1] = {nn, nn, 8, 16, 16, 8, s.scal_r.template as<uint32_t>()};
     tl.c[2] = {nn, 0, 8, 16, 16, 8, s.scal_s.template as<uint32_t>()};
     tl.c[3] = {1, 2 * nn, 8, 16, 16, 0, s.scal_t.template as<uint32_t>()};
   }
-  tl.nclass = 4;
-  tl.total = 3 * nn + 1;
-  const MsmWindows mw = powers ? MsmWindows{2, {0, 16}, {16, 16}} : MsmWindows{2, {0, 8}, {8, 16}};
-  CHK(run_msm_core<Cv>(c, s, tl, powers ? 32 : 24, (size_t)(powers ? 48 : 32) * n + 16, mw));
+  if (!glv) {
+    tl.nclass = 4;
+    tl.total = 3 * nn + 1;
+    const MsmWindows mw = powers ? MsmWindows{2, {0, 16}, {16, 16}} : MsmWindows{2, {0, 8}, {8, 16}};
+    CHK(run_msm_core<Cv>(c, s, tl, powers ? 32 : 24, (size_t)(powers ? 48 : 32) * n + 16, mw));
+  }
   if (d_partial_out) {
     HIPCHK(hipMemcpyAsync(d_partial_out, s.res.p, 2 * sizeof(XY), hipMemcpyDeviceToDevice, st));
   } else {
@@ -412,7 +456,7 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
     DevBuf* bufs[] = {&s.pts, &s.inf, &s.scal_r, &s.scal_s, &s.scal_t, &s.tpart, &s.cnt, &s.off, &s.coarse, &s.ent,
                       &s.total, &s.sval, &s.skey, &s.buckets, &s.pfirst, &s.plast, &s.R, &s.U, &s.scratch,
                       &s.winsum, &s.res, &s.flags, &s.stage, &s.outb, &s.fs_leaves, &s.fs_tmp,
-                      &s.fs_top, &s.pow, &s.chal};
+                      &s.fs_top, &s.pow, &s.chal, &s.glv_r, &s.glv_s, &s.glv_t};
     for (DevBuf* b : bufs) b->release();
     for (auto& e : s.ev)
       if (e) (void)hipEventDestroy(e);
@@ -600,25 +644,42 @@ int kzgmi_last_combination(kzgmi_ctx* c, uint8_t* a_out, uint8_t* b_out) {
 namespace {
 template <class Cv>
 int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t n) {
-  CHK(s.pts.ensure(n * sizeof(Affine<Cv>)));
-  CHK(s.inf.ensure(n));
+  const bool glv = c->glv_msm;
+  CHK(s.pts.ensure((glv ? 2 : 1) * n * sizeof(Affine<Cv>)));
+  CHK(s.inf.ensure((glv ? 2 : 1) * n));
   CHK(s.scal_s.ensure(n * 32));
+  if (glv) CHK(s.glv_s.ensure(n * 32));
   CHK(s.flags.ensure(16));
   hipStream_t st = s.stream;
   mark(c, s, 0);
   HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
   uint32_t* err = s.flags.template as<uint32_t>() + 1;
-  Launch<Cv>::convert_points(st, (const uint8_t*)dpts, (uint32_t)n, s.pts.template as<Affine<Cv>>(),
-                             s.inf.template as<uint8_t>(), err);
+  Affine<Cv>* pts = s.pts.template as<Affine<Cv>>();
+  uint8_t* inf = s.inf.template as<uint8_t>();
+  Launch<Cv>::convert_points(st, (const uint8_t*)dpts, (uint32_t)n, pts, inf, err);
+  if (glv) Launch<Cv>::endo_points(st, pts, inf, (uint32_t)n, pts + n, inf + n);
   mark(c, s, PH_CONVERT + 1);
-  Launch<Cv>::convert_scalars(st, (const uint8_t*)dsc, (uint32_t)n, s.scal_s.template as<uint32_t>(), err);
+  uint32_t* sc = s.scal_s.template as<uint32_t>();
+  Launch<Cv>::convert_scalars(st, (const uint8_t*)dsc, (uint32_t)n, sc, err);
+  uint32_t* gs = s.glv_s.template as<uint32_t>();
+  if (glv) Launch<Cv>::glv_split(st, sc, 8, (uint32_t)n, gs, gs + 4 * n);
   mark(c, s, PH_SCALARS + 1);
   TermList tl{};
-  tl.c[0] = {(uint32_t)n, 0, 8, 16, 0, 8, s.scal_s.template as<uint32_t>()};
-  tl.nclass = 1;
-  tl.total = (uint32_t)n;
-  MsmWindows mw{1, {0, 0}, {16, 0}};
-  CHK(run_msm_core<Cv>(c, s, tl, 16, (size_t)16 * n + 16, mw));
+  const uint32_t nn = (uint32_t)n;
+  if (glv) {  // sum k_i P_i = sum h0_i P_i + h1_i phi(P_i): 8 windows, 8 bucket sets
+    tl.c[0] = {nn, 0, 4, 8, 0, 4, gs};
+    tl.c[1] = {nn, nn, 4, 8, 0, 4, gs + 4 * n};
+    tl.nclass = 2;
+    tl.total = 2 * nn;
+    const MsmWindows mw{1, {0, 0}, {8, 0}};
+    CHK(run_msm_core<Cv>(c, s, tl, 8, (size_t)16 * n + 16, mw));
+  } else {
+    tl.c[0] = {nn, 0, 8, 16, 0, 8, sc};
+    tl.nclass = 1;
+    tl.total = nn;
+    const MsmWindows mw{1, {0, 0}, {16, 0}};
+    CHK(run_msm_core<Cv>(c, s, tl, 16, (size_t)16 * n + 16, mw));
+  }
   s.curve = Cv::ID;
   return 0;
 }
@@ -1249,6 +1310,15 @@ int kzgmi_probe_fpmul(kzgmi_ctx* c, kzgmi_curve curve, double* muls_per_s) {
 }
 
 // ------------------------------------------------------------------------------ profiling
+int kzgmi_set_glv(kzgmi_ctx* c, int msm, int batch) {
+  CHK(check_ctx(c));
+  for (auto& s : c->slots)
+    if (s.pending) return fail(KZGMI_ERR_ARG, "kzgmi_set_glv with jobs in flight");
+  c->glv_msm = msm != 0;
+  c->glv_batch = batch != 0;
+  return 0;
+}
+
 int kzgmi_set_profiling(kzgmi_ctx* c, int on) {
   if (!c) return fail(KZGMI_ERR_ARG, "null context");
   c->profiling = on != 0;

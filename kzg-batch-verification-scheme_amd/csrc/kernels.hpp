@@ -4,6 +4,7 @@
 // kernel are those of oracle/pyspec/kzg.py, checked bit-exactly against the C oracle.
 #pragma once
 #include "msm.hpp"
+#include "glv.hpp"
 #include "pairing.hpp"
 
 namespace kzgmi {

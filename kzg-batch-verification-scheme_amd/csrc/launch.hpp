@@ -28,6 +28,9 @@ struct Launch {
   static void compress_points(hipStream_t st, const uint8_t* in, uint32_t n, uint8_t* out);
   static void subgroup_check(hipStream_t st, const AF* pts, const uint8_t* inf, uint32_t n, uint32_t* err);
   static void convert_scalars(hipStream_t st, const uint8_t* bytes, uint32_t n, uint32_t* out, uint32_t* err);
+  // GLV (glv.hpp): n scalars of 8 words, `stride` words apart -> half scalars h0, h1 (4 words each)
+  static void glv_split(hipStream_t st, const uint32_t* scal, uint32_t stride, uint32_t n, uint32_t* h0, uint32_t* h1);
+  static void endo_points(hipStream_t st, const AF* src, const uint8_t* src_inf, uint32_t n, AF* dst, uint8_t* dst_inf);
   static void convert_g2(hipStream_t st, const uint8_t* bytes, uint32_t n, G2Aff<Cv>* out, uint8_t* inf,
                          uint32_t* err);
   static void scalar_prep(hipStream_t st, const Seed& seed, uint64_t index_offset, const uint8_t* zs,

@@ -33,6 +33,16 @@ void Launch<Cv>::convert_scalars(hipStream_t st, const uint8_t* bytes, uint32_t 
   if (n) k_convert_scalars<Cv><<<grid_for(n, 256), 256, 0, st>>>(bytes, n, out, err);
 }
 template <class Cv>
+void Launch<Cv>::glv_split(hipStream_t st, const uint32_t* scal, uint32_t stride, uint32_t n, uint32_t* h0,
+                           uint32_t* h1) {
+  if (n) k_glv_split<Cv><<<grid_for(n, 256), 256, 0, st>>>(scal, stride, n, h0, h1);
+}
+template <class Cv>
+void Launch<Cv>::endo_points(hipStream_t st, const AF* src, const uint8_t* src_inf, uint32_t n, AF* dst,
+                             uint8_t* dst_inf) {
+  if (n) k_endo_points<Cv><<<grid_for(n, 256), 256, 0, st>>>(src, src_inf, n, dst, dst_inf);
+}
+template <class Cv>
 void Launch<Cv>::convert_g2(hipStream_t st, const uint8_t* bytes, uint32_t n, G2Aff<Cv>* out, uint8_t* inf,
                             uint32_t* err) {
   k_convert_g2<Cv><<<1, 64, 0, st>>>(bytes, n, out, inf, err);
@@ -124,6 +134,8 @@ template void Launch<C_>::pow_table(hipStream_t, const Seed&, void*, uint32_t*);
 template void Launch<C_>::scalar_prep_pow(hipStream_t, const void*, uint64_t, const uint8_t*, const uint8_t*, uint32_t,
                                           uint32_t*, uint32_t*, void*, uint32_t*, uint32_t*);
 template void Launch<C_>::encode_points(hipStream_t, const Xyzz<C_>*, uint32_t, uint8_t*);
+template void Launch<C_>::glv_split(hipStream_t, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t*);
+template void Launch<C_>::endo_points(hipStream_t, const Affine<C_>*, const uint8_t*, uint32_t, Affine<C_>*, uint8_t*);
 template void Launch<C_>::sum_partials(hipStream_t, const Xyzz<C_>*, uint32_t, uint32_t, uint32_t, Xyzz<C_>*);
 
 }  // namespace kzgmi

@@ -76,13 +76,17 @@ KZ_DEV TileRef tile_decode(const TermList& tl, uint32_t t) {
   return {k, (int)(t / chunks), t % chunks};
 }
 
-// signed 16-bit digit of window w (recoding windows 0..w; carry-propagating)
-KZ_DEV int signed_digit(const TermClass& C, uint32_t local, int w) {
+// signed 16-bit digit of window w (recoding windows 0..w; carry-propagating).  4-word
+// scalars are half-size (< 2^127): bit 127 is a sign flag (GLV halves, glv.hpp) returned in
+// `neg` -- the term then uses -P.
+KZ_DEV int signed_digit(const TermClass& C, uint32_t local, int w, bool& neg) {
   const uint32_t* s = C.scal + (size_t)local * C.scal_stride;
   uint32_t w8[8];
+  neg = false;
   if (C.scal_words == 4) {
     uint4 q = *reinterpret_cast<const uint4*>(s);
-    w8[0] = q.x; w8[1] = q.y; w8[2] = q.z; w8[3] = q.w;
+    neg = (q.w >> 31) != 0;
+    w8[0] = q.x; w8[1] = q.y; w8[2] = q.z; w8[3] = q.w & 0x7fffffffu;
     w8[4] = w8[5] = w8[6] = w8[7] = 0;
   } else {
     uint4 q0 = *reinterpret_cast<const uint4*>(s);
@@ -112,7 +116,8 @@ static __global__ void __launch_bounds__(256) k_bin_count(TermList tl, const uin
   for (int j = 0; j < TILE_TERMS / 256; ++j) {
     uint32_t local = T.c * TILE_TERMS + j * 256 + threadIdx.x;
     if (local >= C.count || inf[C.pt_base + local]) continue;
-    int d = signed_digit(C, local, T.w + (int)C.win_off);
+    bool ng;
+    int d = signed_digit(C, local, T.w + (int)C.win_off, ng);
     if (d != 0) {
       uint32_t mag = (uint32_t)(d < 0 ? -d : d);
       atomicAdd(&hist[(mag - 1) >> COARSE_SHIFT], 1u);
@@ -172,11 +177,12 @@ static __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const u
     if (local >= C.count) continue;
     uint32_t pt = C.pt_base + local;
     if (inf[pt]) continue;
-    int d = signed_digit(C, local, T.w + (int)C.win_off);
+    bool ng;
+    int d = signed_digit(C, local, T.w + (int)C.win_off, ng);
     if (d == 0) continue;
     uint32_t mag = (uint32_t)(d < 0 ? -d : d);
     key[j] = set * NBUCKETS + (mag - 1);
-    ent[j] = (pt << 1) | (d < 0 ? 1u : 0u);
+    ent[j] = (pt << 1) | ((d < 0) != ng ? 1u : 0u);
     rank[j] = atomicAdd(&hist[(mag - 1) >> COARSE_SHIFT], 1u);
   }
   __syncthreads();

@@ -83,6 +83,7 @@ def lib():
         "kzgmi_msm_g1_device": ([vp, c.c_int, vp, vp, sz, u8p], c.c_int),
         "kzgmi_msm_g1_device_async": ([vp, c.c_int, c.c_int, vp, vp, sz], c.c_int),
         "kzgmi_msm_wait": ([vp, c.c_int, u8p], c.c_int),
+        "kzgmi_set_glv": ([vp, c.c_int, c.c_int], c.c_int),
         "kzgmi_msm_partial_device_async": ([vp, c.c_int, c.c_int, vp, vp, sz, vp], c.c_int),
         "kzgmi_msm_combine_device_async": ([vp, c.c_int, c.c_int, vp, c.c_int], c.c_int),
         "kzgmi_partial_bytes": ([c.c_int], sz),
@@ -119,7 +120,7 @@ def exported_symbols():
         "kzgmi_fs_challenge_device", "kzgmi_fs_chunk_digests_device",
         "kzgmi_fs_challenge_from_digests_device",
         "kzgmi_last_combination", "kzgmi_msm_g1", "kzgmi_msm_g1_device", "kzgmi_msm_g1_device_async",
-        "kzgmi_msm_wait", "kzgmi_msm_partial_device_async", "kzgmi_msm_combine_device_async", "kzgmi_partial_bytes",
+        "kzgmi_msm_wait", "kzgmi_set_glv", "kzgmi_msm_partial_device_async", "kzgmi_msm_combine_device_async", "kzgmi_partial_bytes",
         "kzgmi_batch_partial_device", "kzgmi_batch_combine_device", "kzgmi_batch_partial_device_async",
         "kzgmi_batch_combine_device_async", "kzgmi_msm_partial_device",
         "kzgmi_msm_combine_device", "kzgmi_pairing", "kzgmi_gen_g1", "kzgmi_gen_tuples",
@@ -453,6 +454,10 @@ class Context:
         v = ctypes.c_double()
         _check(lib().kzgmi_probe_fpmul(self.handle, CURVES[curve], ctypes.byref(v)))
         return v.value
+
+    def set_glv(self, msm: bool = True, batch: bool = True):
+        """GLV split of full Fr scalars for MSMs / batch verification."""
+        _check(lib().kzgmi_set_glv(self.handle, int(bool(msm)), int(bool(batch))))
 
     def set_profiling(self, on: bool):
         _check(lib().kzgmi_set_profiling(self.handle, 1 if on else 0))

@@ -87,6 +87,65 @@ def glv_beta(p, r, b, g1, x_abs):
     raise AssertionError("no cube root of unity matches -x^2")
 
 
+def glv_params(p, r, g1, lam=None):
+    """GLV endomorphism phi(x, y) = (beta x, y) = [lam] P on G1 and a reduced basis of the
+    lattice {(a, b) : a + b lam = 0 mod r} (extended Euclid on (r, lam), Guide to ECC
+    Algorithm 3.74).  `lam` pins the eigenvalue (BLS12-381: -x^2, the subgroup-test phi)."""
+    g = 2
+    while pow(g, (p - 1) // 3, p) == 1:
+        g += 1
+    betas = [pow(g, (p - 1) // 3, p), pow(g, 2 * (p - 1) // 3, p)]
+    h = 2
+    while pow(h, (r - 1) // 3, r) == 1:
+        h += 1
+    lams = [lam] if lam is not None else [pow(h, (r - 1) // 3, r), pow(h, 2 * (r - 1) // 3, r)]
+    pair = None
+    for be in betas:  # first matching pair (the order tests/test_glv.py's spec also uses)
+        for la in lams:
+            if pair is None and (be * g1[0] % p, g1[1]) == _aff_mul(g1, la, p):
+                pair = (be, la)
+    assert pair, "no (beta, lambda) pair"
+    beta, la = pair
+    rs, ts = [r, la], [0, 1]
+    while rs[-1] * rs[-1] >= r:
+        q = rs[-2] // rs[-1]
+        rs.append(rs[-2] - q * rs[-1])
+        ts.append(ts[-2] - q * ts[-1])
+    m = len(rs) - 1
+    v1 = (rs[m], -ts[m])
+    q = rs[m - 1] // rs[m]
+    cands = [(rs[m - 1], -ts[m - 1]), (rs[m - 1] - q * rs[m], -(ts[m - 1] - q * ts[m]))]
+    v2 = min(cands, key=lambda v: v[0] ** 2 + v[1] ** 2)
+    if v1[0] * v2[1] - v1[1] * v2[0] < 0:
+        v2 = (-v2[0], -v2[1])
+    assert v1[0] * v2[1] - v1[1] * v2[0] == r
+    for v in (v1, v2):
+        assert (v[0] + v[1] * la) % r == 0 and abs(v[0]) < 1 << 128 and abs(v[1]) < 1 << 128
+    # Babai multipliers c1 = round(k g1 / r), c2 = round(k g2 / r) must be >= 0
+    assert v2[1] > 0 and -v1[1] > 0
+    return beta, la, v1, v2
+
+
+def glv_lines(p, r, g1, n, M, lam=None):
+    beta, la, v1, v2 = glv_params(p, r, g1, lam)
+    m128 = (1 << 128) - 1
+    return [
+        "  // GLV: phi(x, y) = (GLV_BETA x, y) = [GLV_LAMBDA] P on G1; k = k0 + k1 lambda with",
+        "  // (k0, k1) = (k, 0) - c1 v1 - c2 v2, c1 = round(k G1 / r), c2 = round(k G2 / r),",
+        "  // |k0|, |k1| < 2^127 (tools/gen_params.py glv_params; tests/test_glv.py)",
+        "  static constexpr uint32_t GLV_BETA_M[%d] = %s;" % (n, arr(M(beta), n)),
+        "  static constexpr uint32_t GLV_LAMBDA[8] = %s;" % arr(la, 8),
+        "  static constexpr uint32_t GLV_G1[4] = %s;  // v2.b" % arr(v2[1], 4),
+        "  static constexpr uint32_t GLV_G2[4] = %s;  // -v1.b" % arr(-v1[1], 4),
+        "  static constexpr uint32_t GLV_A1[4] = %s;  // v1.a mod 2^128" % arr(v1[0] & m128, 4),
+        "  static constexpr uint32_t GLV_A2[4] = %s;  // v2.a mod 2^128" % arr(v2[0] & m128, 4),
+        "  static constexpr uint32_t GLV_B1[4] = %s;  // v1.b mod 2^128" % arr(v1[1] & m128, 4),
+        "  static constexpr uint32_t GLV_B2[4] = %s;  // v2.b mod 2^128" % arr(v2[1] & m128, 4),
+        "  static constexpr uint32_t GLV_HALF_R[8] = %s;  // (r - 1) / 2" % arr((r - 1) // 2, 8),
+        "  static constexpr uint32_t GLV_MU[9] = %s;  // floor(2^512 / r) (Barrett)" % arr((1 << 512) // r, 9),
+    ]
+
+
 def main():
     out = ["// GENERATED by tools/gen_params.py -- do not edit.",
            "// 32-bit little-endian limbs; *_M = Montgomery form (R = 2^(32*N)).",
@@ -146,6 +205,8 @@ def main():
             beta = glv_beta(p, r, c["b"], c["g1"], c["loop"])
             out.append("  // phi(x, y) = (BETA x, y) acts as [-x^2] on G1 (subgroup test, Scott 2021)")
             out.append("  static constexpr uint32_t BETA_M[%d] = %s;" % (n, arr(M(beta), n)))
+        x2 = c["loop"] ** 2 if "u" not in c else None
+        out += glv_lines(p, r, c["g1"], n, M, lam=(-x2) % r if x2 else None)
         out.append("};")
         out.append("")
     out.append("}  // namespace kzgmi")
