@@ -132,8 +132,8 @@ def main():
     ap.add_argument("--slots", type=int, default=0,
                     help="batches in flight (default 12 single-GPU; sharded 6 + 2 combine lanes)")
     ap.add_argument("--msm-steps", type=int, default=24)
-    ap.add_argument("--glv-batch", type=int, default=1,
-                    help="GLV split of s_i / t (/ r^i) in batch verification (MSMs always use GLV)")
+    ap.add_argument("--trusted-steps", type=int, default=36,
+                    help="secondary: pipelined batches with KZGMI_FLAG_TRUSTED_G1 (GLV on BLS12-381; 0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fs-steps", type=int, default=36,
@@ -165,7 +165,6 @@ def main():
     slots = args.slots if args.slots else (6 if sharded else 12)
     lanes = 2 if sharded else 0
     ctx = kzgmi.Context(local, slots + lanes)  # + the combine lanes
-    ctx.set_glv(msm=True, batch=bool(args.glv_batch))
     g2 = kzgmi.G2_GENERATOR[curve]
     tg2 = ctx.g2_mul(curve, g2, TAU)
     cpu_baseline.tg2 = tg2
@@ -290,6 +289,34 @@ def main():
                 "phase_ms_single_batch": single, "phase_ms_avg_in_timed_region": cph}
         del cc, pp
 
+    # ---- secondary: inputs declared G1 members (KZGMI_FLAG_TRUSTED_G1): the GLV split of s_i, t
+    #  becomes exact on BLS12-381 and is used; single GPU
+    trusted = None
+    if world == 1 and not sharded and args.trusted_steps > 0:
+        def tstep(k):
+            s = k % slots
+            if pending[s]:
+                assert ctx.wait(s), "batch rejected"
+            ctx.batch_verify_async(srs, s, Cm, z, y, P, n, seed=vseed, trusted_g1=True)
+            pending[s] = True
+
+        for k in range(min(slots, args.trusted_steps)):
+            tstep(k)
+        drain()
+        barrier()
+        a = time.perf_counter()
+        for k in range(args.trusted_steps):
+            tstep(k)
+        drain()
+        barrier()
+        dt = time.perf_counter() - a
+        ctx.set_profiling(True)
+        assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n, trusted_g1=True)
+        trusted = {"batch_verifies_per_s": args.trusted_steps / dt, "steps": args.trusted_steps,
+                   "flags": "KZGMI_FLAG_TRUSTED_G1 (caller guarantees G1 membership; enables GLV)",
+                   "phase_ms_single_batch": ctx.phase_ms()}
+        ctx.set_profiling(False)
+
     # ---- secondary: Fiat-Shamir randomisers, single GPU
     fsm = None
     if world == 1 and not sharded and args.fs_steps > 0:
@@ -336,51 +363,59 @@ def main():
         del ck
 
     # ---- secondary: G1 MSM pts/s at n points per GPU (commitments as points, z as scalars),
-    # pipelined over the same slots as the batch verifications (configs[1] throughput)
-    msm_rate, msm_latency_ms = None, None
-    if args.msm_steps > 0:
+    # pipelined over the same slots as the batch verifications (configs[1] throughput); once as
+    # plain on-curve inputs and once declared G1 members (GLV on BLS12-381)
+    def msm_run(steps):
         torch.cuda.synchronize()
         a = time.perf_counter()
         msm_ref = ctx.msm_g1(curve, Cm, z, n=n)  # synchronous: single-MSM latency + reference
-        msm_latency_ms = (time.perf_counter() - a) * 1e3
-        msm_results = []
+        latency_ms = (time.perf_counter() - a) * 1e3
+        results = []
         if world > 1:
             mpipe = ShardedMsmPipeline(ctx, curve, slots, lanes)
-            submit = lambda: msm_results.extend(mpipe.submit(Cm, z, n))  # noqa: E731
-            mdrain = lambda: msm_results.extend(mpipe.drain())  # noqa: E731
+            submit = lambda: results.extend(mpipe.submit(Cm, z, n))  # noqa: E731
+            mdrain = lambda: results.extend(mpipe.drain())  # noqa: E731
         else:
             mk = [0]
 
             def submit():
                 sl = mk[0] % slots
                 if mk[0] >= slots:
-                    msm_results.append(ctx.msm_wait(sl))
+                    results.append(ctx.msm_wait(sl))
                 ctx.msm_g1_async(curve, sl, Cm, z, n)
                 mk[0] += 1
 
             def mdrain():
                 for i in range(min(mk[0], slots)):
-                    msm_results.append(ctx.msm_wait((mk[0] + i) % slots))
+                    results.append(ctx.msm_wait((mk[0] + i) % slots))
                 mk[0] = 0
-        for _ in range(min(slots, args.msm_steps)):
+        for _ in range(min(slots, steps)):
             submit()
         mdrain()
         barrier()
         a = time.perf_counter()
-        for _ in range(args.msm_steps):
+        for _ in range(steps):
             submit()
         mdrain()
         barrier()
         dt = time.perf_counter() - a
         # every pipelined result equals the synchronous one (world 1) / the first global one
-        want = msm_ref if world == 1 else msm_results[0]
-        assert len(msm_results) == args.msm_steps + min(slots, args.msm_steps), len(msm_results)
-        assert all(r == want for r in msm_results), "pipelined MSM result differs"
+        want = msm_ref if world == 1 else results[0]
+        assert len(results) == steps + min(slots, steps), len(results)
+        assert all(r == want for r in results), "pipelined MSM result differs"
         if world > 1:
             t = torch.tensor([dt], dtype=torch.float64, device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
-        msm_rate = world * n * args.msm_steps / dt
+        return world * n * steps / dt, latency_ms, msm_ref
+
+    msm_rate = msm_latency_ms = msm_rate_t = msm_latency_t = None
+    if args.msm_steps > 0:
+        msm_rate, msm_latency_ms, ref_u = msm_run(args.msm_steps)
+        ctx.set_trusted_g1(True)
+        msm_rate_t, msm_latency_t, ref_t = msm_run(args.msm_steps)
+        ctx.set_trusted_g1(False)
+        assert ref_u == ref_t, "GLV MSM differs from the plain MSM"
 
     if rank != 0:
         dist.barrier()
@@ -463,7 +498,6 @@ def main():
             "tuples_per_gpu": n,
             "global_batch": world * n,
             "pipeline_slots": slots,
-            "glv": {"msm": True, "batch": bool(args.glv_batch)},
             "parallelism": "point-range shards" + (", RCCL all_gather of partial sums" if sharded else ""),
         },
         "roofline": roofline,
@@ -474,6 +508,9 @@ def main():
             "msm_n_per_gpu": n,
             "msm_single_latency_ms": msm_latency_ms,
             "msm_method": "pipelined over the batch slots (kzgmi_msm_g1_device_async), 255-bit scalars",
+            "msm_trusted_g1_glv": {"pts_per_s": msm_rate_t, "single_latency_ms": msm_latency_t,
+                                   "note": "points declared G1 members (kzgmi_set_trusted_g1): GLV split"},
+            "trusted_g1": trusted,
             "single_batch_latency_ms": lat,
             "phase_ms_avg_in_timed_region": phases,
             "phase_ms_single_batch": phases_single,

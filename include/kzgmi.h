@@ -54,12 +54,17 @@ typedef enum { KZGMI_BLS12_381 = 0, KZGMI_BN254 = 1 } kzgmi_curve;
                                         BN254 G1 has cofactor 1, the flag is a no-op there) */
 #define KZGMI_FLAG_POWERS 4u         /* r_i = r^i with r = int_be(seed32) < r supplied by the caller
                                         (e.g. the EIP-4844 verify_kzg_proof_batch challenge) */
-#define KZGMI_FLAG_FIAT_SHAMIR 8u    /* r_i = r^i with r derived on the GPU from the inputs:
-                                        leaf_i = SHA256("KZGMI_FS_LEAF_V1" || be64(i) || C_i || pi_i
-                                        || z_i || y_i) (points compressed), binary Merkle root over
-                                        max(4096, next_pow2(n)) zero-padded leaf slots,
-                                        r = int_be(SHA256("KZGMI_FS_ROOT_V1" || be64(n) || root))
-                                        mod r (1 if 0); seed32 is ignored */
+#define KZGMI_FLAG_FIAT_SHAMIR 8u    /* deterministic randomisers from the inputs: a challenge r
+                                        derived on the GPU -- leaf_i = SHA256("KZGMI_FS_LEAF_V1" ||
+                                        be64(i) || C_i || pi_i || z_i || y_i) (points compressed),
+                                        binary Merkle root over max(4096, next_pow2(n)) zero-padded
+                                        leaf slots, r = int_be(SHA256("KZGMI_FS_ROOT_V1" || be64(n)
+                                        || root)) mod r (1 if 0) -- then the counter-mode 127-bit
+                                        r_i above with seed = be32(r); seed32 is ignored */
+#define KZGMI_FLAG_TRUSTED_G1 16u    /* the caller guarantees every C_i / pi_i is in G1 (e.g. it was
+                                        subgroup-checked when deserialised): lets BLS12-381 use the
+                                        GLV endomorphism, which is exact only on G1 (kzgmi_set_glv).
+                                        Results for inputs outside G1 are then unspecified. */
 
 typedef struct kzgmi_ctx kzgmi_ctx; /* one GPU, its streams and workspaces */
 typedef struct kzgmi_srs kzgmi_srs; /* {G1, [1]_2, [tau]_2} + precomputed Miller lines */
@@ -121,7 +126,7 @@ int kzgmi_fs_challenge_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_c
 /* Multi-GPU form: a shard [index_offset, index_offset + n) with index_offset % 4096 == 0
  * writes its ceil(n / 4096) subtree roots (32 B each) to d_out; gather all shards' roots in
  * order and derive r with kzgmi_fs_challenge_from_digests_device, then verify each shard
- * with kzgmi_batch_partial_device_async(..., KZGMI_FLAG_POWERS, seed32 = r). */
+ * with kzgmi_batch_partial_device_async(..., flags 0, seed32 = be32(r)). */
 int kzgmi_fs_chunk_digests_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_commitments,
                                   const void* d_zs, const void* d_ys, const void* d_proofs, size_t n,
                                   uint64_t index_offset, uint32_t flags, void* d_out);
@@ -224,11 +229,15 @@ int kzgmi_probe_fpmul(kzgmi_ctx* ctx, kzgmi_curve curve, double* muls_per_s);
 /* GLV endomorphism phi(x, y) = (beta x, y) = [lambda] P.  Full Fr
  * scalars k are split as k = k0 + k1 lambda (|k0|, |k1| < 2^127) so each MSM runs 8 windows
  * over P and phi(P) instead of 16 over P: the same bucket additions, half the bucket sets to
- * reduce and half the window-combination doublings.  Results are identical either way.
- * msm: kzgmi_msm_g1* (default on); batch: s_i, t (and r^i in the powers / Fiat-Shamir modes)
- * of batch verification (default on; measured 108 -> 113 batch-verifies/s).
- * Not allowed while jobs are in flight. */
+ * reduce and half the window-combination doublings.  phi acts as [lambda] only on G1, so the
+ * split is used where the points are G1 members: always on BN254 (cofactor 1); on BLS12-381
+ * for batch calls with KZGMI_FLAG_SUBGROUP_CHECK or KZGMI_FLAG_TRUSTED_G1 and for MSMs after
+ * kzgmi_set_trusted_g1(ctx, 1).  On G1 the results are identical either way.
+ * kzgmi_set_glv switches the split off/on (msm: kzgmi_msm_g1*, batch: s_i, t and r^i of batch
+ * verification; default both on) for A/B measurements.  Not allowed while jobs are in flight. */
 int kzgmi_set_glv(kzgmi_ctx* ctx, int msm, int batch);
+/* Declare that every point passed to kzgmi_msm_g1* on this context is in G1 (default 0). */
+int kzgmi_set_trusted_g1(kzgmi_ctx* ctx, int on);
 
 /* ---- profiling -----------------------------------------------------------------------
  * When enabled, every batch / MSM call records HIP events around each phase on the stream

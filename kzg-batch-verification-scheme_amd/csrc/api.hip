@@ -85,8 +85,13 @@ struct kzgmi_ctx {
   int device = 0;
   std::vector<Slot> slots;
   bool profiling = false;
-  bool glv_msm = true;     // GLV split of full Fr scalars in kzgmi_msm_g1* 
-  bool glv_batch = true;   // ... and of s_i, t (and r^i) in batch verification (kzgmi_set_glv)
+  // GLV split of full Fr scalars.  phi(P) = [lambda] P holds only on
+  // G1, so BLS12-381 (cofactor > 1) uses it only for points known to be in G1: batch calls
+  // with KZGMI_FLAG_SUBGROUP_CHECK or KZGMI_FLAG_TRUSTED_G1, MSMs after kzgmi_set_trusted_g1.
+  // BN254 G1 is the whole curve (cofactor 1): always.
+  bool glv_msm = true;      // enable knobs (kzgmi_set_glv; A/B measurements)
+  bool glv_batch = true;
+  bool msm_trusted_g1 = false;
   double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
   int phase_calls = 0;
   DevBuf table[2], table_base[2];
@@ -214,7 +219,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl, uint32_t nsets, size
 
 // ------------------------------------------------------------------------------ Fiat-Shamir
 constexpr uint32_t kAllFlags = KZGMI_FLAG_COMPRESSED | KZGMI_FLAG_SUBGROUP_CHECK | KZGMI_FLAG_POWERS |
-                               KZGMI_FLAG_FIAT_SHAMIR;
+                               KZGMI_FLAG_FIAT_SHAMIR | KZGMI_FLAG_TRUSTED_G1;
 
 uint32_t next_pow2(uint32_t x) {
   uint32_t p = 1;
@@ -262,13 +267,16 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
                   uint32_t flags) {
   using XY = Xyzz<Cv>;
   using FrF = Fp<typename Cv::FrP>;
-  const bool glv = c->glv_batch;
+  const bool glv = c->glv_batch &&
+                   (Cv::ID == 1 || (flags & (KZGMI_FLAG_SUBGROUP_CHECK | KZGMI_FLAG_TRUSTED_G1)) != 0);
   const size_t PH = 2 * n + 1;  // GLV: phi(pts[j]) at pts[PH + j]
   const size_t npts = glv ? 2 * PH : PH;
   using L = Launch<Cv>;
   CHK(s.pts.ensure(npts * sizeof(Affine<Cv>)));
   CHK(s.inf.ensure(npts));
-  const bool powers = (flags & (KZGMI_FLAG_POWERS | KZGMI_FLAG_FIAT_SHAMIR)) != 0;
+  // powers: r_i = r^i (255-bit, caller-supplied r).  Fiat-Shamir: r from the transcript, then
+  // the seeded 127-bit randomisers with seed = r (so 32n MSM entries, as with a host seed).
+  const bool powers = (flags & KZGMI_FLAG_POWERS) != 0;
   if (glv) {
     CHK(s.glv_s.ensure(n * 32));
     CHK(s.glv_t.ensure(32));
@@ -309,7 +317,7 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
                        s.scal_r.template as<uint32_t>(), s.scal_s.template as<uint32_t>(), s.tpart.p,
                        s.scal_t.template as<uint32_t>(), err);
   else
-    L::scalar_prep(st, seed, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n,
+    L::scalar_prep(st, seed, (flags & KZGMI_FLAG_FIAT_SHAMIR) ? s.chal.template as<uint32_t>() : nullptr, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n,
                    s.scal_r.template as<uint32_t>(), s.scal_s.template as<uint32_t>(), s.tpart.p,
                    s.scal_t.template as<uint32_t>(), err);
   const uint32_t nn = (uint32_t)n;
@@ -644,7 +652,7 @@ int kzgmi_last_combination(kzgmi_ctx* c, uint8_t* a_out, uint8_t* b_out) {
 namespace {
 template <class Cv>
 int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t n) {
-  const bool glv = c->glv_msm;
+  const bool glv = c->glv_msm && (Cv::ID == 1 || c->msm_trusted_g1);
   CHK(s.pts.ensure((glv ? 2 : 1) * n * sizeof(Affine<Cv>)));
   CHK(s.inf.ensure((glv ? 2 : 1) * n));
   CHK(s.scal_s.ensure(n * 32));
@@ -899,7 +907,7 @@ int kzgmi_batch_partial_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slo
                                      const uint8_t* seed32, uint32_t flags, void* d_partial_out) {
   if (flags & ~kAllFlags) return fail(KZGMI_ERR_ARG, "unknown flags");
   if (flags & KZGMI_FLAG_FIAT_SHAMIR)
-    return fail(KZGMI_ERR_ARG, "shards take r via KZGMI_FLAG_POWERS (see kzgmi_fs_challenge_from_digests_device)");
+    return fail(KZGMI_ERR_ARG, "shards take the Fiat-Shamir r as seed32 (see kzgmi_fs_challenge_from_digests_device)");
   CHK(check_ctx(c, slot));
   if (!srs || srs->ctx != c || !d_partial_out) return fail(KZGMI_ERR_ARG, "bad argument");
   if (!seed32) return fail(KZGMI_ERR_ARG, "sharded verification needs an explicit shared seed");
@@ -1316,6 +1324,14 @@ int kzgmi_set_glv(kzgmi_ctx* c, int msm, int batch) {
     if (s.pending) return fail(KZGMI_ERR_ARG, "kzgmi_set_glv with jobs in flight");
   c->glv_msm = msm != 0;
   c->glv_batch = batch != 0;
+  return 0;
+}
+
+int kzgmi_set_trusted_g1(kzgmi_ctx* c, int on) {
+  CHK(check_ctx(c));
+  for (auto& s : c->slots)
+    if (s.pending) return fail(KZGMI_ERR_ARG, "kzgmi_set_trusted_g1 with jobs in flight");
+  c->msm_trusted_g1 = on != 0;
   return 0;
 }
 

@@ -153,10 +153,13 @@ __global__ void k_convert_g2(const uint8_t* __restrict__ bytes, uint32_t n, G2Af
 
 // ------------------------------------------------------------------------------ scalar prep
 // r_i (127-bit, 4 words), s_i = r_i z_i mod r (8 words), per-block partial sum of r_i y_i.
+// seed_dev != null: the seed's 8 big-endian words are read from device memory (the
+// Fiat-Shamir challenge r computed on the GPU by k_fs_challenge) instead of `seed`.
 constexpr int PREP_BLOCK = 256;
 
 template <class Cv>
-__global__ void __launch_bounds__(PREP_BLOCK) k_scalar_prep(Seed seed, uint64_t index_offset,
+__global__ void __launch_bounds__(PREP_BLOCK) k_scalar_prep(Seed seed, const uint32_t* __restrict__ seed_dev,
+                                                            uint64_t index_offset,
                                                             const uint8_t* __restrict__ zs, const uint8_t* __restrict__ ys,
                                                             uint32_t n, uint32_t* __restrict__ r_out,
                                                             uint32_t* __restrict__ s_out, Fp<typename Cv::FrP>* __restrict__ tpart,
@@ -165,6 +168,10 @@ __global__ void __launch_bounds__(PREP_BLOCK) k_scalar_prep(Seed seed, uint64_t 
   using F = Fp<R>;
   __shared__ F lds[PREP_BLOCK];
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (seed_dev) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) seed.w[k] = seed_dev[k];
+  }
   F acc = F::zero();
   if (i < n) {
     uint32_t wz[8], wy[8];

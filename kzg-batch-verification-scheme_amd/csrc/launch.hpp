@@ -33,7 +33,8 @@ struct Launch {
   static void endo_points(hipStream_t st, const AF* src, const uint8_t* src_inf, uint32_t n, AF* dst, uint8_t* dst_inf);
   static void convert_g2(hipStream_t st, const uint8_t* bytes, uint32_t n, G2Aff<Cv>* out, uint8_t* inf,
                          uint32_t* err);
-  static void scalar_prep(hipStream_t st, const Seed& seed, uint64_t index_offset, const uint8_t* zs,
+  static void scalar_prep(hipStream_t st, const Seed& seed, const uint32_t* seed_dev, uint64_t index_offset,
+                          const uint8_t* zs,
                           const uint8_t* ys, uint32_t n, uint32_t* r_out, uint32_t* s_out, void* tpart,
                           uint32_t* negt, uint32_t* err);
   static size_t tpart_bytes(uint32_t n);

@@ -52,12 +52,13 @@ size_t Launch<Cv>::tpart_bytes(uint32_t n) {
   return (size_t)grid_for(n, PREP_BLOCK) * sizeof(Fp<typename Cv::FrP>);
 }
 template <class Cv>
-void Launch<Cv>::scalar_prep(hipStream_t st, const Seed& seed, uint64_t index_offset, const uint8_t* zs,
+void Launch<Cv>::scalar_prep(hipStream_t st, const Seed& seed, const uint32_t* seed_dev, uint64_t index_offset,
+                             const uint8_t* zs,
                              const uint8_t* ys, uint32_t n, uint32_t* r_out, uint32_t* s_out, void* tpart,
                              uint32_t* negt, uint32_t* err) {
   using FrF = Fp<typename Cv::FrP>;
   const uint32_t nblk = grid_for(n, PREP_BLOCK);
-  k_scalar_prep<Cv><<<nblk, PREP_BLOCK, 0, st>>>(seed, index_offset, zs, ys, n, r_out, s_out, (FrF*)tpart, err);
+  k_scalar_prep<Cv><<<nblk, PREP_BLOCK, 0, st>>>(seed, seed_dev, index_offset, zs, ys, n, r_out, s_out, (FrF*)tpart, err);
   k_tsum<Cv><<<1, 256, 0, st>>>((const FrF*)tpart, nblk, negt);
 }
 template <class Cv>
@@ -123,7 +124,7 @@ template void Launch<C_>::subgroup_check(hipStream_t, const Affine<C_>*, const u
 template void Launch<C_>::convert_scalars(hipStream_t, const uint8_t*, uint32_t, uint32_t*, uint32_t*);
 template void Launch<C_>::convert_g2(hipStream_t, const uint8_t*, uint32_t, G2Aff<C_>*, uint8_t*, uint32_t*);
 template size_t Launch<C_>::tpart_bytes(uint32_t);
-template void Launch<C_>::scalar_prep(hipStream_t, const Seed&, uint64_t, const uint8_t*, const uint8_t*, uint32_t,
+template void Launch<C_>::scalar_prep(hipStream_t, const Seed&, const uint32_t*, uint64_t, const uint8_t*, const uint8_t*, uint32_t,
                                       uint32_t*, uint32_t*, void*, uint32_t*, uint32_t*);
 template void Launch<C_>::fs_leaves(hipStream_t, const uint8_t*, const uint8_t*, const uint8_t*, const uint8_t*,
                                      uint32_t, uint64_t, bool, uint32_t*);

@@ -84,6 +84,7 @@ def lib():
         "kzgmi_msm_g1_device_async": ([vp, c.c_int, c.c_int, vp, vp, sz], c.c_int),
         "kzgmi_msm_wait": ([vp, c.c_int, u8p], c.c_int),
         "kzgmi_set_glv": ([vp, c.c_int, c.c_int], c.c_int),
+        "kzgmi_set_trusted_g1": ([vp, c.c_int], c.c_int),
         "kzgmi_msm_partial_device_async": ([vp, c.c_int, c.c_int, vp, vp, sz, vp], c.c_int),
         "kzgmi_msm_combine_device_async": ([vp, c.c_int, c.c_int, vp, c.c_int], c.c_int),
         "kzgmi_partial_bytes": ([c.c_int], sz),
@@ -120,7 +121,7 @@ def exported_symbols():
         "kzgmi_fs_challenge_device", "kzgmi_fs_chunk_digests_device",
         "kzgmi_fs_challenge_from_digests_device",
         "kzgmi_last_combination", "kzgmi_msm_g1", "kzgmi_msm_g1_device", "kzgmi_msm_g1_device_async",
-        "kzgmi_msm_wait", "kzgmi_set_glv", "kzgmi_msm_partial_device_async", "kzgmi_msm_combine_device_async", "kzgmi_partial_bytes",
+        "kzgmi_msm_wait", "kzgmi_set_glv", "kzgmi_set_trusted_g1", "kzgmi_msm_partial_device_async", "kzgmi_msm_combine_device_async", "kzgmi_partial_bytes",
         "kzgmi_batch_partial_device", "kzgmi_batch_combine_device", "kzgmi_batch_partial_device_async",
         "kzgmi_batch_combine_device_async", "kzgmi_msm_partial_device",
         "kzgmi_msm_combine_device", "kzgmi_pairing", "kzgmi_gen_g1", "kzgmi_gen_tuples",
@@ -132,14 +133,16 @@ FLAG_COMPRESSED = 1
 FLAG_SUBGROUP_CHECK = 2
 FLAG_POWERS = 4
 FLAG_FIAT_SHAMIR = 8
+FLAG_TRUSTED_G1 = 16
 ERR_NOT_IN_SUBGROUP = -7
 FS_CHUNK = 4096
 
 
 def _flags(compressed: bool = False, subgroup_check: bool = False, fiat_shamir: bool = False,
-           challenge=None) -> int:
+           challenge=None, trusted_g1: bool = False) -> int:
     return ((FLAG_COMPRESSED if compressed else 0) | (FLAG_SUBGROUP_CHECK if subgroup_check else 0)
-            | (FLAG_FIAT_SHAMIR if fiat_shamir else 0) | (FLAG_POWERS if challenge is not None else 0))
+            | (FLAG_FIAT_SHAMIR if fiat_shamir else 0) | (FLAG_POWERS if challenge is not None else 0)
+            | (FLAG_TRUSTED_G1 if trusted_g1 else 0))
 
 
 def _challenge_seed(seed, challenge):
@@ -241,12 +244,13 @@ class Context:
     # ------------------------------------------------------------------ batch verify
     def batch_verify(self, srs: Srs, commitments, zs, ys, proofs, seed: Optional[bytes] = None,
                      n: Optional[int] = None, compressed: bool = False, subgroup_check: bool = False,
-                     fiat_shamir: bool = False, challenge=None) -> bool:
+                     fiat_shamir: bool = False, challenge=None, trusted_g1: bool = False) -> bool:
         """BASELINE.json:5 batch_verify.  compressed: C/pi are compressed G1 encodings;
         subgroup_check: reject points outside G1 (KZGMI_ERR_NOT_IN_SUBGROUP); fiat_shamir:
-        r_i = r^i with r hashed from the inputs on the GPU; challenge: r_i = r^i for a
-        caller-supplied r (e.g. the EIP-4844 transcript's)."""
-        flags = _flags(compressed, subgroup_check, fiat_shamir, challenge)
+        randomisers seeded with a challenge hashed from the inputs on the GPU; challenge:
+        r_i = r^i for a caller-supplied r (e.g. the EIP-4844 transcript's); trusted_g1: the
+        points are known G1 members (enables GLV on BLS12-381)."""
+        flags = _flags(compressed, subgroup_check, fiat_shamir, challenge, trusted_g1)
         g1b = (1 if compressed else 2) * FP_BYTES[srs.curve]
         ok = ctypes.c_int(-1)
         sd = _challenge_seed(seed, challenge)
@@ -273,11 +277,12 @@ class Context:
 
     def batch_verify_async(self, srs: Srs, slot: int, commitments, zs, ys, proofs, n: int,
                            seed: Optional[bytes] = None, compressed: bool = False, subgroup_check: bool = False,
-                           fiat_shamir: bool = False, challenge=None):
+                           fiat_shamir: bool = False, challenge=None, trusted_g1: bool = False):
         _check(lib().kzgmi_batch_verify_device_ex_async(self.handle, srs.handle, int(slot), _dptr(commitments),
                                                         _dptr(zs), _dptr(ys), _dptr(proofs), n,
                                                         _challenge_seed(seed, challenge),
-                                                        _flags(compressed, subgroup_check, fiat_shamir, challenge)))
+                                                        _flags(compressed, subgroup_check, fiat_shamir, challenge,
+                                                               trusted_g1)))
 
     # ------------------------------------------------------------------ prover commit
     def load_commit_key(self, curve: str, g1_powers: bytes, n: Optional[int] = None) -> CommitKey:
@@ -394,13 +399,15 @@ class Context:
         return bool(ok.value)
 
     def batch_partial_async(self, srs: Srs, slot: int, commitments, zs, ys, proofs, n: int, index_offset: int,
-                            seed, out, compressed: bool = False, subgroup_check: bool = False, challenge=None):
+                            seed, out, compressed: bool = False, subgroup_check: bool = False, challenge=None,
+                            trusted_g1: bool = False):
         """Enqueue this shard's partial (A_k, B_k) on `slot`; complete with wait(slot).
         challenge: r_i = r^(index_offset + i) (pass seed=None)."""
         _check(lib().kzgmi_batch_partial_device_async(self.handle, srs.handle, int(slot), _dptr(commitments),
                                                       _dptr(zs), _dptr(ys), _dptr(proofs), n, int(index_offset),
                                                       _challenge_seed(seed, challenge),
-                                                      _flags(compressed, subgroup_check, False, challenge),
+                                                      _flags(compressed, subgroup_check, False, challenge,
+                                                             trusted_g1),
                                                       _dptr(out)))
 
     def batch_combine_async(self, srs: Srs, slot: int, partials, n_parts: int):
@@ -459,6 +466,10 @@ class Context:
         """GLV split of full Fr scalars for MSMs / batch verification."""
         _check(lib().kzgmi_set_glv(self.handle, int(bool(msm)), int(bool(batch))))
 
+    def set_trusted_g1(self, on: bool = True):
+        """MSM inputs on this context are known G1 members (BLS12-381 MSMs may then use GLV)."""
+        _check(lib().kzgmi_set_trusted_g1(self.handle, int(bool(on))))
+
     def set_profiling(self, on: bool):
         _check(lib().kzgmi_set_profiling(self.handle, 1 if on else 0))
 
@@ -498,10 +509,12 @@ def load_srs(curve: str, g2: bytes, tau_g2: bytes, ctx: Optional[Context] = None
 
 
 def batch_verify(commitments, zs, ys, proofs, srs: Srs, seed: Optional[bytes] = None, compressed: bool = False,
-                 subgroup_check: bool = False, fiat_shamir: bool = False, challenge=None) -> bool:
+                 subgroup_check: bool = False, fiat_shamir: bool = False, challenge=None,
+                 trusted_g1: bool = False) -> bool:
     """BASELINE.json:5 batch_verify(commitments, zs, ys, proofs, srs) on the GPU."""
     return srs.ctx.batch_verify(srs, commitments, zs, ys, proofs, seed=seed, compressed=compressed,
-                                subgroup_check=subgroup_check, fiat_shamir=fiat_shamir, challenge=challenge)
+                                subgroup_check=subgroup_check, fiat_shamir=fiat_shamir, challenge=challenge,
+                                trusted_g1=trusted_g1)
 
 
 def msm_g1(curve: str, points, scalars, ctx: Optional[Context] = None) -> bytes:

@@ -67,8 +67,9 @@ def sharded_batch_verify(backend, srs, commitments, zs, ys, proofs, n_local: int
     """Verify this rank's shard as part of a global batch; collective over `group`.
 
     commitments/zs/ys/proofs: this rank's shard (device tensors on the GPU path).
-    fiat_shamir: r_i = r^i with r from the whole batch's transcript (fs_challenge_sharded;
-    shards from shard_range(n_total, world, rank, align=4096)); seed is ignored.
+    fiat_shamir: the counter-mode r_i seeded with the whole batch's transcript challenge r
+    (fs_challenge_sharded; shards from shard_range(n_total, world, rank, align=4096)); seed is
+    ignored.
     Returns the global verdict on every rank.
     """
     import torch
@@ -81,8 +82,8 @@ def sharded_batch_verify(backend, srs, commitments, zs, ys, proofs, n_local: int
     if fiat_shamir:
         r = fs_challenge_sharded(backend, srs.curve, commitments, zs, ys, proofs, n_local, offset, n_total,
                                  compressed=compressed, group=group)
-        backend.batch_partial_async(srs, 0, commitments, zs, ys, proofs, n_local, offset, None, local,
-                                    compressed=compressed, challenge=r)
+        backend.batch_partial_async(srs, 0, commitments, zs, ys, proofs, n_local, offset,
+                                    r.to_bytes(32, "big"), local, compressed=compressed)
         backend.wait(0)
     else:
         backend.batch_partial(srs, commitments, zs, ys, proofs, n_local, offset, seed, local)

@@ -311,3 +311,9 @@ def fs_challenge(commitments: Sequence[G1Point], zs, ys, proofs: Sequence[G1Poin
     h = hashlib.sha256(FS_ROOT_TAG + n.to_bytes(8, "big") + merkle_root(leaves)).digest()
     r = int.from_bytes(h, "big") % C.r
     return r if r else 1
+
+
+def fs_seed(commitments, zs, ys, proofs, C: CurveParams) -> bytes:
+    """KZGMI_FLAG_FIAT_SHAMIR randomisers: the counter-mode r_i of `randomizer` seeded with
+    be32(fs_challenge(...)), i.e. batch_combination(..., seed=fs_seed(...))."""
+    return fs_challenge(commitments, zs, ys, proofs, C).to_bytes(32, "big")

@@ -61,13 +61,19 @@ def test_fs_golden(ctx, curve, golden):
         cc, pc_ = O.g1_compress(curve, cm, n), O.g1_compress(curve, pf, n)
         assert ctx.fs_challenge(curve, _dev(cc), _dev(zb), _dev(yb), _dev(pc_), n, compressed=True) == r
         srs = ctx.load_srs(curve, h(g["g2"]), h(g["tau_g2"]))
-        ok, A, B = O.batch_verify_powers(curve, cm, zb, yb, pf, n, h(g["g2"]), h(g["tau_g2"]), r)
+        # Fiat-Shamir mode = the seeded 127-bit randomisers with seed = be32(r)
+        ok, A, B = O.batch_verify(curve, cm, zb, yb, pf, n, h(g["g2"]), h(g["tau_g2"]), r.to_bytes(32, "big"),
+                                  want_ab=True)
         assert ok is True
         assert ctx.batch_verify(srs, cm, zb, yb, pf, fiat_shamir=True) is True
         assert ctx.last_combination(curve) == (A, B)
         assert ctx.batch_verify(srs, cc, zb, yb, pc_, fiat_shamir=True, compressed=True, subgroup_check=True) is True
-        assert ctx.batch_verify(srs, cm, zb, yb, pf, challenge=r) is True
         assert ctx.last_combination(curve) == (A, B)
+        # powers mode with the same r: r_i = r^i
+        okp, Ap, Bp = O.batch_verify_powers(curve, cm, zb, yb, pf, n, h(g["g2"]), h(g["tau_g2"]), r)
+        assert okp is True
+        assert ctx.batch_verify(srs, cm, zb, yb, pf, challenge=r) is True
+        assert ctx.last_combination(curve) == (Ap, Bp)
         yb2 = bytearray(yb)
         yb2[32 * (n - 1) + 31] ^= 1
         assert ctx.batch_verify(srs, cm, zb, bytes(yb2), pf, fiat_shamir=True) is False
@@ -92,7 +98,8 @@ def test_powers_arbitrary_r(ctx, curve, golden):
 @pytest.mark.parametrize("curve,n", [("bls12_381", 3 * 4096 + 100), ("bn254", 9000)])
 def test_fs_multichunk_and_shards(ctx, curve, n):
     """Several 4096-leaf subtrees (non-power-of-two n); 4096-aligned shards: gathered subtree
-    roots give the same r, and shard partials with r^(offset + i) combine to the whole."""
+    roots give the same r; shard partials seeded with be32(r) (the Fiat-Shamir randomisers) and
+    with r^(offset + i) (powers mode) each combine to the whole."""
     import torch
     C = pc.CURVES[curve]
     tau = 31337
@@ -112,13 +119,14 @@ def test_fs_multichunk_and_shards(ctx, curve, n):
     srs = ctx.load_srs(curve, g2, tg2)
     pb = ctx.partial_bytes(curve)
     parts = torch.empty(2 * 2 * pb, dtype=torch.uint8, device="cuda")
-    for k, (lo, hi) in enumerate([(0, cut), (cut, n)]):
-        ctx.batch_partial_async(srs, 0, Cm[lo * g1b:hi * g1b], z[lo * 32:hi * 32], y[lo * 32:hi * 32],
-                                P[lo * g1b:hi * g1b], hi - lo, lo, None, parts[2 * k * pb:2 * (k + 1) * pb], challenge=r)
-        assert ctx.wait(0) is True
-    assert ctx.batch_combine(srs, parts, 2) is True
+    for kw in ({"seed": r.to_bytes(32, "big")}, {"seed": None, "challenge": r}):
+        for k, (lo, hi) in enumerate([(0, cut), (cut, n)]):
+            ctx.batch_partial_async(srs, 0, Cm[lo * g1b:hi * g1b], z[lo * 32:hi * 32], y[lo * 32:hi * 32],
+                                    P[lo * g1b:hi * g1b], hi - lo, lo, out=parts[2 * k * pb:2 * (k + 1) * pb], **kw)
+            assert ctx.wait(0) is True
+        assert ctx.batch_combine(srs, parts, 2) is True
     assert ctx.batch_verify(srs, Cm, z, y, P, n=n, fiat_shamir=True) is True
-    ok, A, B = O.batch_verify_powers(curve, hb[0], hb[1], hb[2], hb[3], n, g2, tg2, r)
+    ok, A, B = O.batch_verify(curve, hb[0], hb[1], hb[2], hb[3], n, g2, tg2, r.to_bytes(32, "big"), want_ab=True)
     assert ok is True and ctx.last_combination(curve) == (A, B)
 
 
@@ -136,7 +144,7 @@ def test_fs_full_size(ctx):
     tg2 = O.g2_mul(curve, g2, tau)
     srs = ctx.load_srs(curve, g2, tg2)
     assert ctx.batch_verify(srs, Cm, z, y, P, n=n, fiat_shamir=True) is True
-    ok, A, B = O.batch_verify_powers(curve, hb[0], hb[1], hb[2], hb[3], n, g2, tg2, r)
+    ok, A, B = O.batch_verify(curve, hb[0], hb[1], hb[2], hb[3], n, g2, tg2, r.to_bytes(32, "big"), want_ab=True)
     assert ok is True and ctx.last_combination(curve) == (A, B)
     y[5] ^= 1
     assert ctx.batch_verify(srs, Cm, z, y, P, n=n, fiat_shamir=True) is False

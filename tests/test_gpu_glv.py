@@ -1,7 +1,10 @@
 """GLV endomorphism on the GPU: bit-exact vs the C oracle.
 
-GLV regroups the same sum (k P = k0 P + k1 phi(P)), so every result must equal the oracle's
-plain double-and-add MSM / batch combination exactly, with GLV on or off.  Scalars come from
+GLV regroups the same sum (k P = k0 P + k1 phi(P)) for P in G1, so every result must equal
+the oracle's plain double-and-add MSM / batch combination exactly, with GLV on or off.  On
+BLS12-381 (cofactor > 1) the split is used only for points declared or checked to be in G1
+(kzgmi_set_trusted_g1, KZGMI_FLAG_TRUSTED_G1 / KZGMI_FLAG_SUBGROUP_CHECK); a non-member point
+in an undeclared MSM must still give the plain result.  Scalars come from
 oracle/pyspec/glv.edge_scalars (0, 1, r - 1, +-lambda, Babai rounding boundaries, the
 largest halves of a random search); the decomposition itself is pinned on the CPU in
 tests/test_glv.py.
@@ -25,6 +28,7 @@ CURVES = ["bls12_381", "bn254"]
 def ctx():
     import kzgmi
     c = kzgmi.Context(0, 2)
+    c.set_trusted_g1(True)
     yield c
     c.set_glv(msm=True, batch=True)
     c.close()
@@ -69,6 +73,24 @@ def test_msm_random_glv(ctx, curve):
         assert ctx.msm_g1(curve, pts, sc) == O.msm_g1(curve, pts, sc, n), n
 
 
+def test_msm_non_subgroup_point_untrusted(ctx):
+    """BLS12-381 MSM over a point outside G1: without the trusted-G1 declaration the plain
+    (non-GLV) result, bit-exact vs the oracle; the declaration is per context."""
+    from pointcases import non_subgroup_points
+    curve = "bls12_381"
+    C = pc.CURVES[curve]
+    n = 40
+    pts = bytearray(_points(curve, n, 8))
+    pts[96 * 3:96 * 4] = pk.g1_to_bytes(non_subgroup_points(1, seed=4)[0], C)
+    pts = bytes(pts)
+    sc = b"".join(pk.fr_to_bytes(k) for k in glv.edge_scalars(curve, n)[:n])
+    try:
+        ctx.set_trusted_g1(False)
+        assert ctx.msm_g1(curve, pts, sc) == O.msm_g1(curve, pts, sc, n)
+    finally:
+        ctx.set_trusted_g1(True)
+
+
 def _batch(ctx, torch, curve, n, tau, seed):
     C = pc.CURVES[curve]
     g1b = 2 * C.fp_bytes
@@ -102,13 +124,14 @@ def test_batch_verify_glv_modes(ctx, curve):
     try:
         for on in (True, False):
             ctx.set_glv(msm=True, batch=on)
-            assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n) is True
-            assert ctx.last_combination(curve) == (Ao, Bo), on
-            assert ctx.batch_verify(srs, Cm, z, y, P, n=n, challenge=r) is True
-            assert ctx.last_combination(curve) == (Ap, Bp), on
-            assert ctx.batch_verify(srs, Cm, z, y, P, n=n, fiat_shamir=True) is True
-            assert ctx.batch_verify(srs, Cm, z, ybad, P, seed=vseed, n=n) is False
-            assert ctx.batch_verify(srs, Cm, z, ybad, P, n=n, fiat_shamir=True) is False
+            for tr in (True, False):
+                assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n, trusted_g1=tr) is True
+                assert ctx.last_combination(curve) == (Ao, Bo), (on, tr)
+                assert ctx.batch_verify(srs, Cm, z, y, P, n=n, challenge=r, trusted_g1=tr) is True
+                assert ctx.last_combination(curve) == (Ap, Bp), (on, tr)
+                assert ctx.batch_verify(srs, Cm, z, y, P, n=n, fiat_shamir=True, trusted_g1=tr) is True
+                assert ctx.batch_verify(srs, Cm, z, ybad, P, seed=vseed, n=n, trusted_g1=tr) is False
+                assert ctx.batch_verify(srs, Cm, z, ybad, P, n=n, fiat_shamir=True, trusted_g1=tr) is False
     finally:
         ctx.set_glv(msm=True, batch=True)
     assert ok_o and okp

@@ -198,3 +198,20 @@ def test_powers_mode_oracle_vs_spec(curve, golden):
     yb2 = bytearray(yb)
     yb2[31] ^= 1
     assert O.batch_verify_powers(curve, cm, zb, bytes(yb2), pf, n, h(g["g2"]), h(g["tau_g2"]), r)[0] is False
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_fiat_shamir_mode_oracle_vs_spec(curve, golden):
+    """KZGMI_FLAG_FIAT_SHAMIR: seeded 127-bit r_i with seed = be32(r_FS): C oracle == spec."""
+    C = pc.CURVES[curve]
+    g = golden("%s_batch_n16.json" % curve)
+    h = bytes.fromhex
+    n, g1b = 16, 2 * C.fp_bytes
+    cm, pf, zb, yb = h(g["commitments"]), h(g["proofs"]), h(g["zs"]), h(g["ys"])
+    pts = lambda b: [pk.g1_from_bytes(b[i * g1b:(i + 1) * g1b], C) for i in range(n)]  # noqa: E731
+    ints = lambda b: [int.from_bytes(b[32 * i:32 * i + 32], "big") for i in range(n)]  # noqa: E731
+    seed = pk.fs_seed(pts(cm), ints(zb), ints(yb), pts(pf), C)
+    ok, A, B = O.batch_verify(curve, cm, zb, yb, pf, n, h(g["g2"]), h(g["tau_g2"]), seed, want_ab=True)
+    As, Bs = pk.batch_combination(pts(cm), ints(zb), ints(yb), pts(pf), seed, C)
+    assert ok is True and A == pk.g1_to_bytes(As, C) and B == pk.g1_to_bytes(Bs, C)
+    assert all(pk.randomizer(seed, i) < 1 << 127 for i in range(n))
