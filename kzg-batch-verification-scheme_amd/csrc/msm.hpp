@@ -291,8 +291,13 @@ KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_
   store_xyzz(dst, acc);
 }
 
+#ifdef KZ_ACC_WAVES
+#define KZ_ACC_ATTR __attribute__((amdgpu_waves_per_eu(KZ_ACC_WAVES, KZ_ACC_WAVES)))
+#else
+#define KZ_ACC_ATTR
+#endif
 template <class Cv>
-__global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__ total_p,
+__global__ void __launch_bounds__(256) KZ_ACC_ATTR k_accumulate(const uint32_t* __restrict__ total_p,
                                                     const uint32_t* __restrict__ sorted_val,
                                                     const uint32_t* __restrict__ sorted_key,
                                                     const uint32_t* __restrict__ off,
@@ -308,6 +313,27 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__
   const uint32_t end = min(start + ACC_CHUNK, total);
   Xyzz<Cv> acc = Xyzz<Cv>::inf();
   uint32_t cur = sorted_key[start];
+#ifdef KZ_ACC_PREFETCH
+  // software pipelining: the gather of entry e+1 is issued before the addition of entry e
+  uint32_t vn = sorted_val[start];
+  Affine<Cv> pn = load_affine(pts, vn >> 1);
+  for (uint32_t e = start; e < end; ++e) {
+    uint32_t key = sorted_key[e];
+    if (key != cur) {
+      acc_flush(acc, cur, chunk, start, off, cnt, buckets, part_first, part_last);
+      acc = Xyzz<Cv>::inf();
+      cur = key;
+    }
+    const uint32_t v = vn;
+    Affine<Cv> p = pn;
+    if (e + 1 < end) {
+      vn = sorted_val[e + 1];
+      pn = load_affine(pts, vn >> 1);
+    }
+    p.y = fp_cneg(p.y, (v & 1) != 0);
+    acc = xyzz_add_affine(acc, p);
+  }
+#else
   for (uint32_t e = start; e < end; ++e) {
     uint32_t key = sorted_key[e];
     if (key != cur) {
@@ -323,6 +349,7 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__
     p.y = fp_cneg(p.y, (v & 1) != 0);
     acc = xyzz_add_affine(acc, p);
   }
+#endif
   acc_flush(acc, cur, chunk, start, off, cnt, buckets, part_first, part_last);
 }
 

@@ -36,7 +36,7 @@ write_kib = sum(write) / len(write)
 acc = [r for r in rows if r["Name"].startswith("void kzgmi::k_accumulate<kzgmi::Bls12_381>")][0]
 out = {
     "kernel": "k_accumulate<Bls12_381>",
-    "command": "bench.py --steps 24 --warmup 8 --no-cpu --msm-steps 2 --fs-steps 0 --compressed-steps 0 (n = 2^20)",
+    "command": "bench.py --steps 24 --warmup 8 --no-cpu --msm-steps 0 --fs-steps 0 --compressed-steps 0 --trusted-steps 0 --commit-steps 0 (n = 2^20)",
     "launches_fetch": len(fetch), "launches_write": len(write),
     "FETCH_SIZE_KiB_per_launch_raw": fetch_kib,
     "WRITE_SIZE_KiB_per_launch": write_kib,
