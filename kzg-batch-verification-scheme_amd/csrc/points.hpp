@@ -13,8 +13,8 @@
 // Subgroup test (BLS12-381 only; BN254 G1 has cofactor 1): P in G1 <=> phi(P) = [-x^2] P with
 // phi(x, y) = (beta x, y) (Scott, "A note on group membership tests for G1, G2 and GT on
 // BLS pairing-friendly curves", 2021).  [x^2]P = [|x|]([|x|]P): 2 x 63 doublings + 2 x 5
-// additions, one thread per point; beta is chosen in tools/gen_params.py by checking the
-// identity on the generator.
+// additions in Jacobian coordinates, one thread per point; beta is chosen in
+// tools/gen_params.py by checking the identity on the generator.
 #pragma once
 #include <type_traits>
 
@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(256) k_decompress_points(const uint8_t* __rest
     } else {
       a.x = fp_to_mont(x);
       const F rhs = fp_add(fp_mul(fp_sqr(a.x), a.x), F::from_const(Cv::K::B_M));
-      F y = fp_pow_words(rhs, P::SQRT_EXP);
+      F y = fp_pow_sqrt(rhs);
       if (!(fp_sqr(y) == rhs)) {
         raise_err(err, DERR_NOT_ON_CURVE);
         is_inf = true;
@@ -126,16 +126,95 @@ __global__ void __launch_bounds__(256) k_compress_points(const uint8_t* __restri
   store_words(out + (size_t)i * 4 * N, o);
 }
 
+// ---- Jacobian coordinates for the membership test (x = X/Z^2, y = Y/Z^3, infinity Z = 0):
+// the test is ~126 doublings, and a = 0 Jacobian doubling (dbl-2009-l, 2M + 5S = 7 products)
+// is cheaper than XYZZ doubling (6M + 3S = 9); the 10 additions cost a little more (madd
+// 7M + 4S, add 11M + 5S vs 8M + 2S, 12M + 2S): ~1020 instead of ~1255 products per point.
+template <class Cv>
+struct Jac {
+  using F = Fp<typename Cv::FpP>;
+  F x, y, z;
+  KZ_DEV bool is_inf() const { return z.is_zero(); }
+};
+
+template <class Cv>
+KZ_DEV Jac<Cv> jac_dbl(const Jac<Cv>& p) {
+  auto A = fp_sqr(p.x);
+  auto B = fp_sqr(p.y);
+  auto C = fp_sqr(B);
+  auto D = fp_dbl(fp_sub(fp_sub(fp_sqr(fp_add(p.x, B)), A), C));
+  auto E = fp_mul3(A);
+  auto Fv = fp_sqr(E);
+  Jac<Cv> r;
+  r.x = fp_sub(Fv, fp_dbl(D));
+  r.y = fp_sub(fp_mul(E, fp_sub(D, r.x)), fp_mul8(C));
+  r.z = fp_dbl(fp_mul(p.y, p.z));
+  return r;  // Z = 0 stays 0
+}
+
+// p + q, q affine (madd-2007-bl) with the exceptional cases
+template <class Cv>
+KZ_DEV Jac<Cv> jac_add_affine(const Jac<Cv>& p, const Affine<Cv>& q) {
+  using F = typename Jac<Cv>::F;
+  if (p.is_inf()) return {q.x, q.y, F::one()};
+  auto Z1Z1 = fp_sqr(p.z);
+  auto U2 = fp_mul(q.x, Z1Z1);
+  auto S2 = fp_mul(q.y, fp_mul(p.z, Z1Z1));
+  auto H = fp_sub(U2, p.x);
+  auto rr = fp_dbl(fp_sub(S2, p.y));
+  if (H.is_zero()) {
+    if (rr.is_zero()) return jac_dbl(Jac<Cv>{q.x, q.y, F::one()});
+    return {F::one(), F::one(), F::zero()};
+  }
+  auto HH = fp_sqr(H);
+  auto I = fp_mul4(HH);
+  auto J = fp_mul(H, I);
+  auto V = fp_mul(p.x, I);
+  Jac<Cv> r;
+  r.x = fp_sub(fp_sub(fp_sqr(rr), J), fp_dbl(V));
+  r.y = fp_sub(fp_mul(rr, fp_sub(V, r.x)), fp_dbl(fp_mul(p.y, J)));
+  r.z = fp_sub(fp_sub(fp_sqr(fp_add(p.z, H)), Z1Z1), HH);
+  return r;
+}
+
+// p + q, both Jacobian (add-2007-bl) with the exceptional cases
+template <class Cv>
+KZ_DEV Jac<Cv> jac_add(const Jac<Cv>& p, const Jac<Cv>& q) {
+  using F = typename Jac<Cv>::F;
+  if (p.is_inf()) return q;
+  if (q.is_inf()) return p;
+  auto Z1Z1 = fp_sqr(p.z);
+  auto Z2Z2 = fp_sqr(q.z);
+  auto U1 = fp_mul(p.x, Z2Z2);
+  auto U2 = fp_mul(q.x, Z1Z1);
+  auto S1 = fp_mul(p.y, fp_mul(q.z, Z2Z2));
+  auto S2 = fp_mul(q.y, fp_mul(p.z, Z1Z1));
+  auto H = fp_sub(U2, U1);
+  auto rr = fp_dbl(fp_sub(S2, S1));
+  if (H.is_zero()) {
+    if (rr.is_zero()) return jac_dbl(p);
+    return {F::one(), F::one(), F::zero()};
+  }
+  auto I = fp_sqr(fp_dbl(H));
+  auto J = fp_mul(H, I);
+  auto V = fp_mul(U1, I);
+  Jac<Cv> r;
+  r.x = fp_sub(fp_sub(fp_sqr(rr), J), fp_dbl(V));
+  r.y = fp_sub(fp_mul(rr, fp_sub(V, r.x)), fp_dbl(fp_mul(S1, J)));
+  r.z = fp_mul(fp_sub(fp_sub(fp_sqr(fp_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  return r;
+}
+
 // [|x|] q by the fixed bit pattern of the BLS parameter (uniform control flow)
 template <class Cv, class Base>
-KZ_DEV Xyzz<Cv> mul_by_x_abs(const Base& q, const Xyzz<Cv>& q_xyzz) {
+KZ_DEV Jac<Cv> mul_by_x_abs(const Base& q, const Jac<Cv>& q_jac) {
   constexpr uint64_t X = Cv::K::X_ABS;
-  Xyzz<Cv> acc = q_xyzz;  // top bit
+  Jac<Cv> acc = q_jac;  // top bit
   for (int b = 62; b >= 0; --b) {
-    acc = xyzz_dbl(acc);
+    acc = jac_dbl(acc);
     if ((X >> b) & 1) {
-      if constexpr (std::is_same_v<Base, Affine<Cv>>) acc = xyzz_add_affine(acc, q);
-      else acc = xyzz_add(acc, q);
+      if constexpr (std::is_same_v<Base, Affine<Cv>>) acc = jac_add_affine(acc, q);
+      else acc = jac_add(acc, q);
     }
   }
   return acc;
@@ -151,11 +230,12 @@ __global__ void __launch_bounds__(256) k_subgroup_check(const Affine<Cv>* __rest
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || inf[i]) return;
   const Affine<Cv> p = pts[i];
-  const Xyzz<Cv> q1 = mul_by_x_abs<Cv>(p, xyzz_from_affine(p));
-  const Xyzz<Cv> q2 = mul_by_x_abs<Cv>(q1, q1);  // [x^2] p
-  // p in G1 <=> q2 == -phi(p) = (beta x, -y): X2 == beta x ZZ2 and Y2 == -y ZZZ2, q2 finite
+  const Jac<Cv> q1 = mul_by_x_abs<Cv>(p, Jac<Cv>{p.x, p.y, F::one()});
+  const Jac<Cv> q2 = mul_by_x_abs<Cv>(q1, q1);  // [x^2] p
+  // p in G1 <=> q2 == -phi(p) = (beta x, -y): X2 == beta x Z2^2 and Y2 == -y Z2^3, q2 finite
   const F bx = fp_mul(F::from_const(Cv::K::BETA_M), p.x);
-  const bool ok = !q2.is_inf() && q2.x == fp_mul(bx, q2.zz) && q2.y == fp_mul(fp_neg(p.y), q2.zzz);
+  const F z2 = fp_sqr(q2.z);
+  const bool ok = !q2.is_inf() && q2.x == fp_mul(bx, z2) && q2.y == fp_mul(fp_neg(p.y), fp_mul(z2, q2.z));
   if (!ok) raise_err(err, DERR_NOT_IN_SUBGROUP);
 }
 

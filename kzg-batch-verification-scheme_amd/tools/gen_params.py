@@ -146,6 +146,39 @@ def glv_lines(p, r, g1, n, M, lam=None):
     ]
 
 
+def window_steps(e, w=4):
+    """Sliding-window (width w) left-to-right schedule for x^e: the first odd window value
+    (table index), then (squarings, table index or 255 = none) pairs.  Table k = x^(2k+1)."""
+    bits = bin(e)[2:]
+    i, first, steps = 0, None, []
+    pending = 0
+    while i < len(bits):
+        if bits[i] == "0":
+            pending += 1
+            i += 1
+            continue
+        j = min(i + w, len(bits))
+        while bits[j - 1] == "0":
+            j -= 1
+        val = int(bits[i:j], 2)
+        if first is None:
+            first = (val - 1) // 2
+        else:
+            steps.append((pending + (j - i), (val - 1) // 2))
+        pending = 0
+        i = j
+    if pending:
+        steps.append((pending, 255))
+    # check
+    acc = 2 * first + 1
+    for sq, k in steps:
+        acc <<= sq
+        if k != 255:
+            acc += 2 * k + 1
+    assert acc == e
+    return first, steps
+
+
 def main():
     out = ["// GENERATED by tools/gen_params.py -- do not edit.",
            "// 32-bit little-endian limbs; *_M = Montgomery form (R = 2^(32*N)).",
@@ -165,6 +198,15 @@ def main():
         out.append("  static constexpr uint32_t PM2[N] = %s;" % arr(p - 2, n))
         assert p % 4 == 3
         out.append("  static constexpr uint32_t SQRT_EXP[N] = %s;  // (p+1)/4: sqrt for p = 3 mod 4" % arr((p + 1) // 4, n))
+        first, steps = window_steps((p + 1) // 4)
+        out.append("  // x^((p+1)/4) by a width-4 sliding window over the odd powers x^(2k+1), k < 8:")
+        out.append("  // start at table[SQRT_FIRST]; step s: SQRT_SQR[s] squarings, then * table[SQRT_IDX[s]]")
+        out.append("  // (255: none) -- %d squarings + %d multiplications" % (sum(q for q, _ in steps),
+                                                                              sum(1 for _, k in steps if k != 255)))
+        out.append("  static constexpr int SQRT_FIRST = %d;" % first)
+        out.append("  static constexpr int SQRT_STEPS = %d;" % len(steps))
+        out.append("  static constexpr uint8_t SQRT_SQR[%d] = {%s};" % (len(steps), ", ".join(str(q) for q, _ in steps)))
+        out.append("  static constexpr uint8_t SQRT_IDX[%d] = {%s};" % (len(steps), ", ".join(str(k) for _, k in steps)))
         out.append("  static constexpr uint32_t HALF[N] = %s;  // (p-1)/2, raw: y > HALF <=> 'largest'" % arr((p - 1) // 2, n))
         out.append("};")
         out.append("struct %sFrParams {" % name)
