@@ -385,9 +385,10 @@ def main():
                 ctx.msm_g1_async(curve, sl, Cm, z, n)
                 mk[0] += 1
 
-            def mdrain():
+            def mdrain():  # oldest first; fewer than `slots` submitted -> slots 0..mk-1
+                first = mk[0] % slots if mk[0] >= slots else 0
                 for i in range(min(mk[0], slots)):
-                    results.append(ctx.msm_wait((mk[0] + i) % slots))
+                    results.append(ctx.msm_wait((first + i) % slots))
                 mk[0] = 0
         for _ in range(min(slots, steps)):
             submit()

@@ -69,6 +69,7 @@ struct Slot {
   DevBuf buckets, pfirst, plast, R, U, scratch, winsum, res, flags, stage, outb;
   DevBuf fs_leaves, fs_tmp, fs_top, pow, chal;  // Fiat-Shamir / powers-of-r randomisers
   DevBuf glv_r, glv_s, glv_t;                    // GLV half scalars (glv.hpp): [h0 x n | h1 x n]
+  DevBuf digits;                                 // signed window digit codes of every term (msm.hpp)
   int* host_flags = nullptr;  // pinned: [ok, err]
   uint8_t* host_out = nullptr;  // pinned: encoded MSM result of an async MSM job
   hipEvent_t ev[kNumPhases + 1] = {};
@@ -176,8 +177,16 @@ int map_device_err(uint32_t e) {
 
 // ------------------------------------------------------------------------------ MSM core
 template <class Cv>
-int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl, uint32_t nsets, size_t emax, const MsmWindows& mw,
+int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, size_t emax, const MsmWindows& mw,
                  const Affine<Cv>* pts = nullptr, const uint8_t* inf = nullptr) {
+  TermList tl = tl_in;  // + each class's offset in the digit array
+  size_t ndig = 0;
+  for (uint32_t k = 0; k < tl.nclass; ++k) {
+    tl.c[k].dig_base = (uint32_t)ndig;
+    ndig += (size_t)tl.c[k].count * tl.c[k].nwin;
+  }
+  if (ndig >= (1ull << 32)) return fail(KZGMI_ERR_ARG, "too many window digits for one call");
+  CHK(s.digits.ensure(ndig * 4));
   using XY = Xyzz<Cv>;
   if (!pts) pts = s.pts.template as<Affine<Cv>>();  // default: the slot's converted points
   if (!inf) inf = s.inf.template as<uint8_t>();
@@ -200,7 +209,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl, uint32_t nsets, size
   CHK(s.res.ensure(2 * sizeof(XY)));
   hipStream_t st = s.stream;
   using L = Launch<Cv>;
-  L::sort(st, tl, nsets, inf, s.coarse.template as<uint32_t>(), s.ent.template as<uint64_t>(),
+  L::sort(st, tl, nsets, inf, s.digits.template as<uint32_t>(), s.coarse.template as<uint32_t>(), s.ent.template as<uint64_t>(),
           s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.total.template as<uint32_t>(),
           s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>());
   mark(c, s, PH_SORT + 1);
@@ -464,7 +473,7 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
     DevBuf* bufs[] = {&s.pts, &s.inf, &s.scal_r, &s.scal_s, &s.scal_t, &s.tpart, &s.cnt, &s.off, &s.coarse, &s.ent,
                       &s.total, &s.sval, &s.skey, &s.buckets, &s.pfirst, &s.plast, &s.R, &s.U, &s.scratch,
                       &s.winsum, &s.res, &s.flags, &s.stage, &s.outb, &s.fs_leaves, &s.fs_tmp,
-                      &s.fs_top, &s.pow, &s.chal, &s.glv_r, &s.glv_s, &s.glv_t};
+                      &s.fs_top, &s.pow, &s.chal, &s.glv_r, &s.glv_s, &s.glv_t, &s.digits};
     for (DevBuf* b : bufs) b->release();
     for (auto& e : s.ev)
       if (e) (void)hipEventDestroy(e);

@@ -11,9 +11,11 @@ struct Launch {
   using XY = Xyzz<Cv>;
   using AF = Affine<Cv>;
   // ---- MSM (launch_msm.hip)
-  // coarse: 3 * nsets * 256 u32 (counts, offsets, cursors), ent: emax u64
-  static void sort(hipStream_t st, const TermList& tl, uint32_t nsets, const uint8_t* inf, uint32_t* coarse,
-                   uint64_t* ent, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval, uint32_t* skey);
+  // digits: sum_k count_k * nwin_k u32 (tl.c[k].dig_base set), coarse: 3 * nsets * 256 u32
+  // (counts, offsets, cursors), ent: emax u64
+  static void sort(hipStream_t st, const TermList& tl, uint32_t nsets, const uint8_t* inf, uint32_t* digits,
+                   uint32_t* coarse, uint64_t* ent, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
+                   uint32_t* skey);
   static void accumulate(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* sval,
                          const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts, XY* buckets,
                          XY* pfirst, XY* plast);

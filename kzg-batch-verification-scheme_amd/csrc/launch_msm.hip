@@ -4,17 +4,19 @@
 namespace kzgmi {
 
 template <class Cv>
-void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const uint8_t* inf, uint32_t* coarse,
-                      uint64_t* ent, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval, uint32_t* skey) {
+void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const uint8_t* inf, uint32_t* digits,
+                      uint32_t* coarse, uint64_t* ent, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
+                      uint32_t* skey) {
   const uint32_t nbins = nsets * BINS_PER_SET;
   uint32_t* ccnt = coarse;
   uint32_t* coff = coarse + nbins;
   uint32_t* ccur = coarse + 2 * nbins;
   (void)hipMemsetAsync(ccnt, 0, (size_t)nbins * 4, st);
   const uint32_t tiles = num_tiles_host(tl);
-  if (tiles) k_bin_count<<<tiles, 256, 0, st>>>(tl, inf, ccnt);
+  if (tl.total) k_digits<<<grid_for(tl.total, 256), 256, 0, st>>>(tl, inf, digits);
+  if (tiles) k_bin_count<<<tiles, 256, 0, st>>>(tl, digits, ccnt);
   k_bin_scan<<<1, 1024, 0, st>>>(ccnt, nbins, coff, ccur, total);
-  if (tiles) k_bin_scatter<<<tiles, 256, 0, st>>>(tl, inf, ccur, ent);
+  if (tiles) k_bin_scatter<<<tiles, 256, 0, st>>>(tl, digits, ccur, ent);
   k_fine_sort<<<nbins, 256, 0, st>>>(coff, ccnt, ent, off, cnt, sval, skey);
 }
 
@@ -39,8 +41,8 @@ void Launch<Cv>::window_combine(hipStream_t st, const MsmWindows& mw, const XY* 
   k_window_combine<Cv><<<1, 64, 0, st>>>(mw, winsum, res);
 }
 
-template void Launch<KZ_CURVE_T>::sort(hipStream_t, const TermList&, uint32_t, const uint8_t*, uint32_t*, uint64_t*,
-                                       uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*);
+template void Launch<KZ_CURVE_T>::sort(hipStream_t, const TermList&, uint32_t, const uint8_t*, uint32_t*, uint32_t*,
+                                       uint64_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*);
 template void Launch<KZ_CURVE_T>::accumulate(hipStream_t, size_t, const uint32_t*, const uint32_t*, const uint32_t*,
                                              const uint32_t*, const uint32_t*, const Affine<KZ_CURVE_T>*,
                                              Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*);

@@ -36,6 +36,8 @@ struct TermClass {
   const uint32_t* scal; // LE words, standard (non-Montgomery) form
   uint32_t win_off;     // window of the scalar that local window 0 reads (fixed-base tables:
                         // row w of 2^(16w)-shifted points reads digit w into one bucket set)
+  uint32_t dig_base;    // first digit code of this class in the digit array (set by the host:
+                        // digit (w, i) at dig_base + w * count + i)
 };
 struct TermList {
   TermClass c[MAX_CLASSES];
@@ -76,52 +78,65 @@ KZ_DEV TileRef tile_decode(const TermList& tl, uint32_t t) {
   return {k, (int)(t / chunks), t % chunks};
 }
 
-// signed 16-bit digit of window w (recoding windows 0..w; carry-propagating).  4-word
-// scalars are half-size (< 2^127): bit 127 is a sign flag (GLV halves, glv.hpp) returned in
-// `neg` -- the term then uses -P.
-KZ_DEV int signed_digit(const TermClass& C, uint32_t local, int w, bool& neg) {
-  const uint32_t* s = C.scal + (size_t)local * C.scal_stride;
+// All signed digits of every term, once: one thread per term reads its scalar once and walks
+// the carry chain over its windows (the count and scatter passes used to recompute the chain
+// from the scalar for every window: nwin scalar reads per term per pass).  Code = 0 for a zero
+// digit or a point at infinity, else |d| | (entry sign << 31) with entry sign = (d < 0) xor the
+// half-scalar's sign flag.
+static __global__ void __launch_bounds__(256) k_digits(TermList tl, const uint8_t* __restrict__ inf,
+                                                uint32_t* __restrict__ digits) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  int k = 0;
+  for (; k < (int)tl.nclass; ++k) {
+    if (i < tl.c[k].count) break;
+    i -= tl.c[k].count;
+  }
+  if (k >= (int)tl.nclass) return;
+  const TermClass& C = tl.c[k];
+  const uint32_t* sp = C.scal + (size_t)i * C.scal_stride;
   uint32_t w8[8];
-  neg = false;
+  bool neg = false;
   if (C.scal_words == 4) {
-    uint4 q = *reinterpret_cast<const uint4*>(s);
+    const uint4 q = *reinterpret_cast<const uint4*>(sp);
     neg = (q.w >> 31) != 0;
     w8[0] = q.x; w8[1] = q.y; w8[2] = q.z; w8[3] = q.w & 0x7fffffffu;
     w8[4] = w8[5] = w8[6] = w8[7] = 0;
   } else {
-    uint4 q0 = *reinterpret_cast<const uint4*>(s);
-    uint4 q1 = *reinterpret_cast<const uint4*>(s + 4);
+    const uint4 q0 = *reinterpret_cast<const uint4*>(sp);
+    const uint4 q1 = *reinterpret_cast<const uint4*>(sp + 4);
     w8[0] = q0.x; w8[1] = q0.y; w8[2] = q0.z; w8[3] = q0.w;
     w8[4] = q1.x; w8[5] = q1.y; w8[6] = q1.z; w8[7] = q1.w;
   }
+  const bool is_inf = inf[C.pt_base + i] != 0;
+  const int w0 = (int)C.win_off, w1 = (int)(C.win_off + C.nwin);
   uint32_t carry = 0;
-  int d = 0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    if (i > w) break;
-    uint32_t raw = (w8[i >> 1] >> ((i & 1) * 16)) & 0xffffu;
-    d = (int)(raw + carry);
+  for (int w = 0; w < 16; ++w) {
+    if (w >= w1) break;
+    const uint32_t raw = (w8[w >> 1] >> ((w & 1) * 16)) & 0xffffu;
+    int d = (int)(raw + carry);
     if (d > NBUCKETS) { d -= (1 << WBITS); carry = 1; } else { carry = 0; }
+    if (w >= w0) {
+      uint32_t code = 0;
+      if (d != 0 && !is_inf) code = (uint32_t)(d < 0 ? -d : d) | ((d < 0) != neg ? 0x80000000u : 0u);
+      digits[C.dig_base + (size_t)(w - w0) * C.count + i] = code;
+    }
   }
-  return d;
 }
 
-static __global__ void __launch_bounds__(256) k_bin_count(TermList tl, const uint8_t* __restrict__ inf,
+static __global__ void __launch_bounds__(256) k_bin_count(TermList tl, const uint32_t* __restrict__ digits,
                                                    uint32_t* __restrict__ coarse_cnt) {
   __shared__ uint32_t hist[BINS_PER_SET];
   const TileRef T = tile_decode(tl, blockIdx.x);
   const TermClass& C = tl.c[T.k];
+  const uint32_t* dg = digits + C.dig_base + (size_t)T.w * C.count;
   hist[threadIdx.x] = 0;
   __syncthreads();
+#pragma unroll
   for (int j = 0; j < TILE_TERMS / 256; ++j) {
-    uint32_t local = T.c * TILE_TERMS + j * 256 + threadIdx.x;
-    if (local >= C.count || inf[C.pt_base + local]) continue;
-    bool ng;
-    int d = signed_digit(C, local, T.w + (int)C.win_off, ng);
-    if (d != 0) {
-      uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-      atomicAdd(&hist[(mag - 1) >> COARSE_SHIFT], 1u);
-    }
+    const uint32_t local = T.c * TILE_TERMS + j * 256 + threadIdx.x;
+    const uint32_t code = local < C.count ? dg[local] : 0u;
+    if (code) atomicAdd(&hist[((code & 0x7fffffffu) - 1) >> COARSE_SHIFT], 1u);
   }
   __syncthreads();
   uint32_t h = hist[threadIdx.x];
@@ -159,7 +174,7 @@ static __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __rest
   if (threadIdx.x == 1023) *total = s[1023];
 }
 
-static __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint8_t* __restrict__ inf,
+static __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t* __restrict__ digits,
                                                      uint32_t* __restrict__ coarse_cursor,
                                                      uint64_t* __restrict__ tmp) {
   __shared__ uint32_t hist[BINS_PER_SET];
@@ -167,22 +182,19 @@ static __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const u
   const TileRef T = tile_decode(tl, blockIdx.x);
   const TermClass& C = tl.c[T.k];
   const uint32_t set = C.set_base + T.w;
+  const uint32_t* dg = digits + C.dig_base + (size_t)T.w * C.count;
   hist[threadIdx.x] = 0;
   __syncthreads();
   uint32_t rank[TILE_TERMS / 256], key[TILE_TERMS / 256], ent[TILE_TERMS / 256];
 #pragma unroll
   for (int j = 0; j < TILE_TERMS / 256; ++j) {
     key[j] = 0xffffffffu;
-    uint32_t local = T.c * TILE_TERMS + j * 256 + threadIdx.x;
-    if (local >= C.count) continue;
-    uint32_t pt = C.pt_base + local;
-    if (inf[pt]) continue;
-    bool ng;
-    int d = signed_digit(C, local, T.w + (int)C.win_off, ng);
-    if (d == 0) continue;
-    uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+    const uint32_t local = T.c * TILE_TERMS + j * 256 + threadIdx.x;
+    const uint32_t code = local < C.count ? dg[local] : 0u;
+    if (!code) continue;
+    const uint32_t mag = code & 0x7fffffffu;
     key[j] = set * NBUCKETS + (mag - 1);
-    ent[j] = (pt << 1) | ((d < 0) != ng ? 1u : 0u);
+    ent[j] = ((C.pt_base + local) << 1) | (code >> 31);
     rank[j] = atomicAdd(&hist[(mag - 1) >> COARSE_SHIFT], 1u);
   }
   __syncthreads();
@@ -196,7 +208,13 @@ static __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const u
   }
 }
 
-// one workgroup per coarse bin g: LDS counting sort of its entries by the low 7 key bits
+// one workgroup per coarse bin g: LDS counting sort of its entries by the low 7 key bits.
+// Both passes over the bin's entries issue FINE_ILP independent loads per thread before
+// using them (the loop is latency-bound otherwise); the LDS footprint stays ~1 KiB so many
+// workgroups share a CU.  (A ranked single-atomic-pass variant with a 24 KiB rank array
+// measured slower: 0.73 vs 0.59 ms, fewer resident workgroups.)
+constexpr int FINE_ILP = 4;
+
 static __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ coarse_off,
                                                    const uint32_t* __restrict__ coarse_cnt,
                                                    const uint64_t* __restrict__ tmp,
@@ -207,27 +225,55 @@ static __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __rest
   __shared__ uint32_t cursor[FINE];
   const uint32_t g = blockIdx.x;
   const uint32_t start = coarse_off[g], count = coarse_cnt[g];
-  if (threadIdx.x < FINE) fine[threadIdx.x] = 0;
+  const uint32_t t = threadIdx.x;
+  if (t < FINE) fine[t] = 0;
   __syncthreads();
-  for (uint32_t e = threadIdx.x; e < count; e += 256) atomicAdd(&fine[(uint32_t)(tmp[start + e] >> 32) & (FINE - 1)], 1u);
-  __syncthreads();
-  if (threadIdx.x == 0) {  // 128-entry exclusive scan
-    uint32_t run = 0;
-    for (int f = 0; f < FINE; ++f) { cursor[f] = run; run += fine[f]; }
+  for (uint32_t e0 = t; e0 < count; e0 += 256 * FINE_ILP) {
+    uint32_t k[FINE_ILP];
+#pragma unroll
+    for (int j = 0; j < FINE_ILP; ++j) {
+      const uint32_t e = e0 + 256 * j;
+      k[j] = e < count ? (uint32_t)(tmp[start + e] >> 32) : 0xffffffffu;
+    }
+#pragma unroll
+    for (int j = 0; j < FINE_ILP; ++j)
+      if (k[j] != 0xffffffffu) atomicAdd(&fine[k[j] & (FINE - 1)], 1u);
   }
   __syncthreads();
-  if (threadIdx.x < FINE) {
-    uint32_t key = g * FINE + threadIdx.x;
-    off[key] = start + cursor[threadIdx.x];
-    cnt[key] = fine[threadIdx.x];
+  // exclusive scan of the 128 fine counts (threads 0..127, Hillis-Steele in LDS)
+  __shared__ uint32_t scan[FINE];
+  const uint32_t tot = t < FINE ? fine[t] : 0u;
+  if (t < FINE) scan[t] = tot;
+  __syncthreads();
+  for (int d = 1; d < FINE; d <<= 1) {
+    const uint32_t x = (t < FINE && t >= (uint32_t)d) ? scan[t - d] : 0u;
+    __syncthreads();
+    if (t < FINE) scan[t] += x;
+    __syncthreads();
+  }
+  if (t < FINE) {
+    const uint32_t base = scan[t] - tot;
+    cursor[t] = base;
+    const uint32_t key = g * FINE + t;
+    off[key] = start + base;
+    cnt[key] = tot;
   }
   __syncthreads();
-  for (uint32_t e = threadIdx.x; e < count; e += 256) {
-    uint64_t v = tmp[start + e];
-    uint32_t key = (uint32_t)(v >> 32);
-    uint32_t pos = start + atomicAdd(&cursor[key & (FINE - 1)], 1u);
-    sorted_val[pos] = (uint32_t)v;
-    sorted_key[pos] = key;
+  for (uint32_t e0 = t; e0 < count; e0 += 256 * FINE_ILP) {
+    uint64_t v[FINE_ILP];
+#pragma unroll
+    for (int j = 0; j < FINE_ILP; ++j) {
+      const uint32_t e = e0 + 256 * j;
+      v[j] = e < count ? tmp[start + e] : ~0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < FINE_ILP; ++j) {
+      if (v[j] == ~0ull) continue;
+      const uint32_t key = (uint32_t)(v[j] >> 32);
+      const uint32_t pos = start + atomicAdd(&cursor[key & (FINE - 1)], 1u);
+      sorted_val[pos] = (uint32_t)v[j];
+      sorted_key[pos] = key;
+    }
   }
 }
 
