@@ -10,6 +10,7 @@
 
 #include <sys/random.h>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <algorithm>
@@ -93,6 +94,10 @@ struct kzgmi_ctx {
   bool glv_msm = true;      // enable knobs (kzgmi_set_glv; A/B measurements)
   bool glv_batch = true;
   bool msm_trusted_g1 = false;
+  // accumulation grid cap: one resident round (CUs x 4 SIMDs x 3 waves x 64 lanes at the
+  // kernel's 161 VGPRs) of equal chunks instead of 64-entry chunks in 2-3 partial rounds:
+  // 113 -> 116 batch-verifies/s pipelined (tools/ab_env.sh).  0 = uncapped.
+  size_t acc_threads = 0;
   double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
   int phase_calls = 0;
   DevBuf table[2], table_base[2];
@@ -191,7 +196,10 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   if (!pts) pts = s.pts.template as<Affine<Cv>>();  // default: the slot's converted points
   if (!inf) inf = s.inf.template as<uint8_t>();
   const uint32_t NB = nsets * NBUCKETS;
-  const size_t nchunks = (emax + ACC_CHUNK - 1) / ACC_CHUNK + 1;
+  // accumulation threads: 64-entry chunks, at most acc_threads of them (then equal longer chunks)
+  size_t nchunks = (emax + ACC_CHUNK - 1) / ACC_CHUNK + 1;
+  if (c->acc_threads && nchunks > c->acc_threads) nchunks = c->acc_threads;
+  nchunks = (nchunks + 255) / 256 * 256;  // = the launched thread count (part arrays indexed by thread)
   CHK(s.cnt.ensure((size_t)NB * 4));
   CHK(s.off.ensure((size_t)NB * 4));
   CHK(s.coarse.ensure((size_t)3 * nsets * BINS_PER_SET * 4));
@@ -452,6 +460,10 @@ int kzgmi_ctx_create(kzgmi_ctx** out, int device_id, int pipeline_slots) {
   HIPCHK(hipSetDevice(device_id));
   kzgmi_ctx* c = new kzgmi_ctx();
   c->device = device_id;
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_id) == hipSuccess && ncu > 0)
+    c->acc_threads = (size_t)ncu * 4 * 3 * 64;
+  if (const char* e = getenv("KZGMI_ACC_THREADS")) c->acc_threads = (size_t)strtoull(e, nullptr, 10);
   c->slots.resize(pipeline_slots);
   for (auto& s : c->slots) {
     if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||

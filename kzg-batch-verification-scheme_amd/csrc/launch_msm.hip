@@ -24,8 +24,11 @@ template <class Cv>
 void Launch<Cv>::accumulate(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* sval,
                             const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts, XY* buckets,
                             XY* pfirst, XY* plast) {
-  k_accumulate<Cv><<<grid_for(nchunks, 256), 256, 0, st>>>(total, sval, skey, off, cnt, pts, buckets, pfirst, plast);
-  k_fixup<Cv><<<grid_for(nchunks, 256), 256, 0, st>>>(total, skey, off, cnt, pfirst, plast, buckets);
+  // nchunks threads (rounded up to whole 256-thread blocks); both kernels derive the chunk
+  // length from the same grid
+  const unsigned blocks = grid_for(nchunks, 256);
+  k_accumulate<Cv><<<blocks, 256, 0, st>>>(total, sval, skey, off, cnt, pts, buckets, pfirst, plast);
+  k_fixup<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, pfirst, plast, buckets);
 }
 
 template <class Cv>

@@ -325,25 +325,29 @@ KZ_DEV Xyzz<Cv> load_xyzz(const Xyzz<Cv>* src) {
 }
 
 // ------------------------------------------------------------------------------ accumulation
+// Chunk length: every accumulation thread owns `len` consecutive sorted entries, len =
+// max(ACC_CHUNK, ceil(total / nthreads)) for the launched thread count nthreads (the same
+// value in k_accumulate and k_fixup).  nthreads >= total / ACC_CHUNK gives the fixed 64-entry
+// chunks; a smaller grid gives longer, equal chunks (fewer pieces, no partial last round).
+KZ_DEV uint32_t acc_chunk_len(uint32_t total, uint32_t nthreads) {
+  const uint32_t per = (total + nthreads - 1) / nthreads;
+  return per > (uint32_t)ACC_CHUNK ? per : (uint32_t)ACC_CHUNK;
+}
+
 template <class Cv>
-KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_t start,
+KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_t start, uint32_t len,
                       const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
                       Xyzz<Cv>* __restrict__ buckets, Xyzz<Cv>* __restrict__ part_first,
                       Xyzz<Cv>* __restrict__ part_last) {
   uint32_t o = off[key];
   bool started_before = o < start;
-  bool ends_after = o + cnt[key] > start + ACC_CHUNK;
+  bool ends_after = o + cnt[key] > start + len;
   Xyzz<Cv>* dst = started_before ? &part_first[chunk] : ends_after ? &part_last[chunk] : &buckets[key];
   store_xyzz(dst, acc);
 }
 
-#ifdef KZ_ACC_WAVES
-#define KZ_ACC_ATTR __attribute__((amdgpu_waves_per_eu(KZ_ACC_WAVES, KZ_ACC_WAVES)))
-#else
-#define KZ_ACC_ATTR
-#endif
 template <class Cv>
-__global__ void __launch_bounds__(256) KZ_ACC_ATTR k_accumulate(const uint32_t* __restrict__ total_p,
+__global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__ total_p,
                                                     const uint32_t* __restrict__ sorted_val,
                                                     const uint32_t* __restrict__ sorted_key,
                                                     const uint32_t* __restrict__ off,
@@ -353,37 +357,17 @@ __global__ void __launch_bounds__(256) KZ_ACC_ATTR k_accumulate(const uint32_t* 
                                                     Xyzz<Cv>* __restrict__ part_first,
                                                     Xyzz<Cv>* __restrict__ part_last) {
   const uint32_t total = *total_p;
+  const uint32_t len = acc_chunk_len(total, gridDim.x * blockDim.x);
   const uint32_t chunk = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t start = chunk * ACC_CHUNK;
+  const uint32_t start = chunk * len;
   if (start >= total) return;
-  const uint32_t end = min(start + ACC_CHUNK, total);
+  const uint32_t end = min(start + len, total);
   Xyzz<Cv> acc = Xyzz<Cv>::inf();
   uint32_t cur = sorted_key[start];
-#ifdef KZ_ACC_PREFETCH
-  // software pipelining: the gather of entry e+1 is issued before the addition of entry e
-  uint32_t vn = sorted_val[start];
-  Affine<Cv> pn = load_affine(pts, vn >> 1);
   for (uint32_t e = start; e < end; ++e) {
     uint32_t key = sorted_key[e];
     if (key != cur) {
-      acc_flush(acc, cur, chunk, start, off, cnt, buckets, part_first, part_last);
-      acc = Xyzz<Cv>::inf();
-      cur = key;
-    }
-    const uint32_t v = vn;
-    Affine<Cv> p = pn;
-    if (e + 1 < end) {
-      vn = sorted_val[e + 1];
-      pn = load_affine(pts, vn >> 1);
-    }
-    p.y = fp_cneg(p.y, (v & 1) != 0);
-    acc = xyzz_add_affine(acc, p);
-  }
-#else
-  for (uint32_t e = start; e < end; ++e) {
-    uint32_t key = sorted_key[e];
-    if (key != cur) {
-      acc_flush(acc, cur, chunk, start, off, cnt, buckets, part_first, part_last);
+      acc_flush(acc, cur, chunk, start, len, off, cnt, buckets, part_first, part_last);
       acc = Xyzz<Cv>::inf();
       cur = key;
     }
@@ -395,11 +379,11 @@ __global__ void __launch_bounds__(256) KZ_ACC_ATTR k_accumulate(const uint32_t* 
     p.y = fp_cneg(p.y, (v & 1) != 0);
     acc = xyzz_add_affine(acc, p);
   }
-#endif
-  acc_flush(acc, cur, chunk, start, off, cnt, buckets, part_first, part_last);
+  acc_flush(acc, cur, chunk, start, len, off, cnt, buckets, part_first, part_last);
 }
 
-// joins the pieces of buckets that cross chunk boundaries
+// joins the pieces of buckets that cross chunk boundaries (launched with the same grid as
+// k_accumulate, so acc_chunk_len agrees)
 template <class Cv>
 __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ total_p,
                                                const uint32_t* __restrict__ sorted_key,
@@ -409,15 +393,16 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
                                                const Xyzz<Cv>* __restrict__ part_last,
                                                Xyzz<Cv>* __restrict__ buckets) {
   const uint32_t total = *total_p;
+  const uint32_t len = acc_chunk_len(total, gridDim.x * blockDim.x);
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x + 1;
-  const uint32_t start = c * ACC_CHUNK;
+  const uint32_t start = c * len;
   if (start >= total) return;
   uint32_t key = sorted_key[start];
   uint32_t o = off[key];
   if (o >= start) return;                 // bucket starts inside this chunk
-  uint32_t c0 = o / ACC_CHUNK;
+  uint32_t c0 = o / len;
   if (c0 != c - 1) return;                // a later continuation chunk: handled by c0+1
-  uint32_t c1 = (o + cnt[key] - 1) / ACC_CHUNK;
+  uint32_t c1 = (o + cnt[key] - 1) / len;
   Xyzz<Cv> acc = load_xyzz(&part_last[c0]);
   for (uint32_t cc = c; cc <= c1; ++cc) acc = xyzz_add(acc, load_xyzz(&part_first[cc]));
   store_xyzz(&buckets[key], acc);
