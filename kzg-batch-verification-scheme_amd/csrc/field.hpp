@@ -195,6 +195,85 @@ KZ_DEV Fp<P> fp_mul_ps(const Fp<P>& a, const Fp<P>& b) {
   return r;
 }
 
+// ---------------------------------------------------------------------------- lazy reduction
+// For the bucket-accumulation loop only: values live in [0, 2p) ("lazy") instead of [0, p).
+// With 4p < R (BLS12-381: 4p/R = 0.41, BN254: 0.33) the product-scanning Montgomery product
+// of two lazy inputs is (ab + mp)/R < p (4p/R + 1) < 2p, so it can skip its final
+// conditional subtraction (24 of its 661 VALU instructions); additions and subtractions keep
+// the range with one conditional correction by 2p, and zero tests accept {0, p}.  Values are
+// made canonical (fp_canon) before they leave the loop.
+template <class P>
+KZ_DEV Fp<P> fp_mul_lazy(const Fp<P>& a, const Fp<P>& b) {
+  constexpr int N = P::N;
+  uint32_t m[N];
+  Fp<P> t;
+  uint64_t acc = 0;
+  uint32_t top = 0;
+  _Pragma("unroll") for (int k = 0; k < N; ++k) {
+    _Pragma("unroll") for (int i = 0; i < k; ++i) {
+      mac32(acc, top, a.v[i], b.v[k - i]);
+      mac32s(acc, top, m[i], P::MOD[k - i]);
+    }
+    mac32(acc, top, a.v[k], b.v[0]);
+    m[k] = (uint32_t)acc * P::INV;
+    mac32s(acc, top, m[k], P::MOD[0]);
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+    top = 0;
+  }
+  _Pragma("unroll") for (int k = N; k < 2 * N - 1; ++k) {
+    _Pragma("unroll") for (int i = k - N + 1; i < N; ++i) {
+      mac32(acc, top, a.v[i], b.v[k - i]);
+      mac32s(acc, top, m[i], P::MOD[k - i]);
+    }
+    t.v[k - N] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+    top = 0;
+  }
+  t.v[N - 1] = (uint32_t)acc;
+  return t;  // < 2p
+}
+
+template <class P>
+KZ_DEV Fp<P> fp_sub_lazy(const Fp<P>& a, const Fp<P>& b) {  // a, b < 2p -> a - b mod p, < 2p
+  constexpr int N = P::N;
+  Fp<P> d, e;
+  uint32_t bw = 0;
+  _Pragma("unroll") for (int i = 0; i < N; ++i) d.v[i] = __builtin_subc(a.v[i], b.v[i], bw, &bw);
+  uint32_t c = 0;
+  _Pragma("unroll") for (int i = 0; i < N; ++i) e.v[i] = __builtin_addc(d.v[i], P::MOD2[i], c, &c);
+  _Pragma("unroll") for (int i = 0; i < N; ++i) d.v[i] = bw ? e.v[i] : d.v[i];
+  return d;
+}
+
+template <class P>
+KZ_DEV Fp<P> fp_add_lazy(const Fp<P>& a, const Fp<P>& b) {  // a, b < 2p -> a + b mod p, < 2p
+  constexpr int N = P::N;
+  Fp<P> s, d;
+  uint32_t c = 0;
+  _Pragma("unroll") for (int i = 0; i < N; ++i) s.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+  uint32_t bw = 0;
+  _Pragma("unroll") for (int i = 0; i < N; ++i) d.v[i] = __builtin_subc(s.v[i], P::MOD2[i], bw, &bw);
+  // a + b < 4p < 2^(32N): no carry out of s; s >= 2p iff no borrow
+  _Pragma("unroll") for (int i = 0; i < N; ++i) s.v[i] = bw ? s.v[i] : d.v[i];
+  return s;
+}
+
+template <class P>
+KZ_DEV bool fp_is_zero_lazy(const Fp<P>& a) {  // a < 2p: a = 0 mod p <=> a in {0, p}
+  uint32_t z = 0, q = 0;
+  _Pragma("unroll") for (int i = 0; i < P::N; ++i) { z |= a.v[i]; q |= a.v[i] ^ P::MOD[i]; }
+  return z == 0 || q == 0;
+}
+
+template <class P>
+KZ_DEV Fp<P> fp_canon(const Fp<P>& a) {  // a < 2p -> a mod p
+  Fp<P> d;
+  uint32_t bw = 0;
+  _Pragma("unroll") for (int i = 0; i < P::N; ++i) d.v[i] = __builtin_subc(a.v[i], P::MOD[i], bw, &bw);
+  _Pragma("unroll") for (int i = 0; i < P::N; ++i) d.v[i] = bw ? a.v[i] : d.v[i];
+  return d;
+}
+
 // Default multiplication used by every kernel.
 template <class P>
 KZ_DEV Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {

@@ -87,6 +87,36 @@ KZ_DEV Xyzz<Cv> xyzz_add_affine(const Xyzz<Cv>& p, const Affine<Cv>& q) {
   return r;
 }
 
+// Lazy-reduced form of xyzz_add_affine for the bucket-accumulation loop (field.hpp "lazy
+// reduction"): p's coordinates in [0, 2p), q canonical; result in [0, 2p).  The exceptional
+// cases canonicalise and use the canonical formulas (they do not occur for distinct points).
+template <class Cv>
+KZ_DEV Xyzz<Cv> xyzz_canon(const Xyzz<Cv>& p) {
+  return {fp_canon(p.x), fp_canon(p.y), fp_canon(p.zz), fp_canon(p.zzz)};
+}
+
+template <class Cv>
+KZ_DEV Xyzz<Cv> xyzz_add_affine_lazy(const Xyzz<Cv>& p, const Affine<Cv>& q) {
+  if (fp_is_zero_lazy(p.zz)) return xyzz_from_affine(q);
+  auto U2 = fp_mul_lazy(q.x, p.zz);
+  auto S2 = fp_mul_lazy(q.y, p.zzz);
+  auto P = fp_sub_lazy(U2, p.x);
+  auto R = fp_sub_lazy(S2, p.y);
+  if (fp_is_zero_lazy(P)) {
+    if (fp_is_zero_lazy(R)) return xyzz_dbl_affine(q);
+    return Xyzz<Cv>::inf();
+  }
+  auto PP = fp_mul_lazy(P, P);
+  auto PPP = fp_mul_lazy(P, PP);
+  auto Q = fp_mul_lazy(p.x, PP);
+  Xyzz<Cv> r;
+  r.x = fp_sub_lazy(fp_sub_lazy(fp_mul_lazy(R, R), PPP), fp_add_lazy(Q, Q));
+  r.y = fp_sub_lazy(fp_mul_lazy(R, fp_sub_lazy(Q, r.x)), fp_mul_lazy(p.y, PPP));
+  r.zz = fp_mul_lazy(p.zz, PP);
+  r.zzz = fp_mul_lazy(p.zzz, PPP);
+  return r;
+}
+
 // P + Q, both XYZZ.  add-2008-s with the exceptional cases.
 template <class Cv>
 KZ_DEV Xyzz<Cv> xyzz_add(const Xyzz<Cv>& p, const Xyzz<Cv>& q) {

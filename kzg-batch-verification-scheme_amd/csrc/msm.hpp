@@ -343,11 +343,11 @@ KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_
   bool started_before = o < start;
   bool ends_after = o + cnt[key] > start + len;
   Xyzz<Cv>* dst = started_before ? &part_first[chunk] : ends_after ? &part_last[chunk] : &buckets[key];
-  store_xyzz(dst, acc);
+  store_xyzz(dst, xyzz_canon(acc));  // the loop keeps coordinates lazily reduced (< 2p)
 }
 
 template <class Cv>
-__global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__ total_p,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_accumulate(const uint32_t* __restrict__ total_p,
                                                     const uint32_t* __restrict__ sorted_val,
                                                     const uint32_t* __restrict__ sorted_key,
                                                     const uint32_t* __restrict__ off,
@@ -377,7 +377,7 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__
 #endif
     Affine<Cv> p = load_affine(pts, v >> 1);
     p.y = fp_cneg(p.y, (v & 1) != 0);
-    acc = xyzz_add_affine(acc, p);
+    acc = xyzz_add_affine_lazy(acc, p);
   }
   acc_flush(acc, cur, chunk, start, len, off, cnt, buckets, part_first, part_last);
 }

@@ -192,6 +192,7 @@ def main():
         out.append("  static constexpr int N = %d;" % n)
         out.append("  static constexpr int BITS = %d;" % p.bit_length())
         out.append("  static constexpr uint32_t MOD[N] = %s;" % arr(p, n))
+        out.append("  static constexpr uint32_t MOD2[N] = %s;  // 2p (lazy reduction)" % arr(2 * p, n))
         out.append("  static constexpr uint32_t ONE[N] = %s;" % arr(R, n))
         out.append("  static constexpr uint32_t R2[N] = %s;" % arr(R * R % p, n))
         out.append("  static constexpr uint32_t INV = 0x%08xu;" % ((-pow(p, -1, 1 << 32)) % (1 << 32)))
