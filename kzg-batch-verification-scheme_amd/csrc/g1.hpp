@@ -111,7 +111,7 @@ KZ_DEV Xyzz<Cv> xyzz_add_affine_lazy(const Xyzz<Cv>& p, const Affine<Cv>& q) {
   auto Q = fp_mul_lazy(p.x, PP);
   Xyzz<Cv> r;
   r.x = fp_sub_lazy(fp_sub_lazy(fp_mul_lazy(R, R), PPP), fp_add_lazy(Q, Q));
-  r.y = fp_sub_lazy(fp_mul_lazy(R, fp_sub_lazy(Q, r.x)), fp_mul_lazy(p.y, PPP));
+  r.y = fp_mul2_lazy(R, fp_sub_lazy(Q, r.x), p.y, fp_neg_lazy(PPP));  // R (Q - X3) - Y1 PPP
   r.zz = fp_mul_lazy(p.zz, PP);
   r.zzz = fp_mul_lazy(p.zzz, PPP);
   return r;
