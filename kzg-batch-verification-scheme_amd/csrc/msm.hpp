@@ -210,10 +210,13 @@ static __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const u
 
 // one workgroup per coarse bin g: LDS counting sort of its entries by the low 7 key bits.
 // Both passes over the bin's entries issue FINE_ILP independent loads per thread before
-// using them (the loop is latency-bound otherwise); the LDS footprint stays ~1 KiB so many
-// workgroups share a CU.  (A ranked single-atomic-pass variant with a 24 KiB rank array
-// measured slower: 0.73 vs 0.59 ms, fewer resident workgroups.)
+// using them (the loops are latency-bound otherwise).  Bins of up to FINE_STAGE entries are
+// sorted into an LDS staging array and then written out contiguously (coalesced stores; the
+// bucket of output slot p comes from a 7-step search of the inclusive bucket scan) instead
+// of two scattered 4-byte stores per entry; larger bins (adversarial digit distributions,
+// or 16 bucket sets at n = 2^20) store directly.
 constexpr int FINE_ILP = 4;
+constexpr int FINE_STAGE = 8192;
 
 static __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ coarse_off,
                                                    const uint32_t* __restrict__ coarse_cnt,
@@ -223,9 +226,12 @@ static __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __rest
                                                    uint32_t* __restrict__ sorted_key) {
   __shared__ uint32_t fine[FINE];
   __shared__ uint32_t cursor[FINE];
+  __shared__ uint32_t scan[FINE];  // inclusive bucket scan
+  __shared__ uint32_t stage[FINE_STAGE];
   const uint32_t g = blockIdx.x;
   const uint32_t start = coarse_off[g], count = coarse_cnt[g];
   const uint32_t t = threadIdx.x;
+  const bool staged = count <= (uint32_t)FINE_STAGE;
   if (t < FINE) fine[t] = 0;
   __syncthreads();
   for (uint32_t e0 = t; e0 < count; e0 += 256 * FINE_ILP) {
@@ -240,12 +246,10 @@ static __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __rest
       if (k[j] != 0xffffffffu) atomicAdd(&fine[k[j] & (FINE - 1)], 1u);
   }
   __syncthreads();
-  // exclusive scan of the 128 fine counts (threads 0..127, Hillis-Steele in LDS)
-  __shared__ uint32_t scan[FINE];
   const uint32_t tot = t < FINE ? fine[t] : 0u;
   if (t < FINE) scan[t] = tot;
   __syncthreads();
-  for (int d = 1; d < FINE; d <<= 1) {
+  for (int d = 1; d < FINE; d <<= 1) {  // Hillis-Steele, threads 0..127
     const uint32_t x = (t < FINE && t >= (uint32_t)d) ? scan[t - d] : 0u;
     __syncthreads();
     if (t < FINE) scan[t] += x;
@@ -270,10 +274,24 @@ static __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __rest
     for (int j = 0; j < FINE_ILP; ++j) {
       if (v[j] == ~0ull) continue;
       const uint32_t key = (uint32_t)(v[j] >> 32);
-      const uint32_t pos = start + atomicAdd(&cursor[key & (FINE - 1)], 1u);
-      sorted_val[pos] = (uint32_t)v[j];
-      sorted_key[pos] = key;
+      const uint32_t p = atomicAdd(&cursor[key & (FINE - 1)], 1u);
+      if (staged) {
+        stage[p] = (uint32_t)v[j];
+      } else {
+        sorted_val[start + p] = (uint32_t)v[j];
+        sorted_key[start + p] = key;
+      }
     }
+  }
+  if (!staged) return;
+  __syncthreads();
+  for (uint32_t p = t; p < count; p += 256) {
+    uint32_t b = 0;  // smallest b with scan[b] > p
+#pragma unroll
+    for (int step = FINE / 2; step >= 1; step >>= 1)
+      if (scan[b + step - 1] <= p) b += step;
+    sorted_val[start + p] = stage[p];
+    sorted_key[start + p] = g * FINE + b;
   }
 }
 
