@@ -368,19 +368,6 @@ KZ_DEV bool fp_raw_lt_mod(const Fp<P>& raw) {
 }
 
 // ---------------------------------------------------------------------------- pow / inverse
-template <class P, int NW>
-KZ_DEV Fp<P> fp_pow_words(const Fp<P>& a, const uint32_t (&e)[NW]) {
-  Fp<P> acc = Fp<P>::one();
-  for (int w = NW - 1; w >= 0; --w) {
-    uint32_t ew = e[w];
-    for (int b = 31; b >= 0; --b) {
-      acc = fp_sqr(acc);
-      if ((ew >> b) & 1) acc = fp_mul(acc, a);
-    }
-  }
-  return acc;
-}
-
 // x^((p+1)/4) (square-root candidate, p = 3 mod 4) by the width-4 sliding-window schedule
 // generated into P::SQRT_* (tools/gen_params.py window_steps): 375 squarings + 78
 // multiplications + 8 for the odd-power table on BLS12-381, instead of 380 + 190 for plain
@@ -414,10 +401,6 @@ KZ_DEV Fp<P> fp_pow_sqrt(const Fp<P>& a) {
   }
   return acc;
 }
-
-// Fermat inverse (used where a throughput-oriented, branch-uniform inverse is wanted).
-template <class P>
-KZ_DEV Fp<P> fp_inv_fermat(const Fp<P>& a) { return fp_pow_words(a, P::PM2); }
 
 // Binary extended Euclid on Montgomery values (latency-oriented: single-lane tails such as
 // MSM-result normalisation).  Returns a^-1 in Montgomery form; 0 -> 0.
