@@ -424,22 +424,35 @@ def main():
         return
 
     # ---- roofline of the dominant kernel (bucket accumulation + fixup)
-    acc_ms = phases.get("accumulate", 0.0)
+    # kernel_ms: the k_accumulate + k_fixup phase of a non-pipelined batch (HIP events on the
+    # kernels' own stream, measured above in this run, same inputs) -- the execution time that
+    # rocprof's begin-to-end duration measures.  Inside the 12-deep pipelined region the same
+    # events also count the time a launch waits for CUs held by other batches, so that figure
+    # is reported separately (kernel_ms_in_pipelined_region) and the pipeline's own efficiency
+    # as compute.pipeline_frac.
+    acc_ms_pipe = phases.get("accumulate", 0.0)
+    acc_ms = (phases_single or {}).get("accumulate") or acc_ms_pipe
     alg_bytes = n * BYTES_PER_TUPLE[curve]
     achieved = alg_bytes / (acc_ms * 1e-3) if acc_ms > 0 else None
     fpmul_peak = ctx.probe_fpmul(curve)
-    # modelled Fp products in the accumulation: ~32 n window-terms x (8M + 2S) per mixed add
+    # algorithmic Fp products in the accumulation: 32 n window-terms x (8M + 2S) per mixed
+    # addition (the kernel shares one reduction between two of them)
     acc_fpmuls = 32 * n * 10
     # PMC traffic of the same kernel and config from the committed profile (tools/profile.sh:
     # separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE x 2 as MI355X_MICROARCH.md prescribes)
-    traffic, traffic_src, rocprof_ms = None, None, None
+    traffic, traffic_src, rocprof_ms, rocprof_src = None, None, None, None
     pmc_path = os.path.join(ROOT, "profiles", "r01", "rocprof", "pmc_accumulate.json")
+    single_path = os.path.join(ROOT, "profiles", "r01", "rocprof_single", "kernel_single.json")
     if curve == "bls12_381" and n == 1 << 20 and os.path.exists(pmc_path):
         with open(pmc_path) as f:
             pmc = json.load(f)
         traffic = pmc["traffic_bytes_per_launch"]
         traffic_src = "profiles/r01/rocprof/pmc_accumulate.json (%s)" % pmc["command"]
-        rocprof_ms = pmc["rocprof_avg_duration_ns"] / 1e6
+    if curve == "bls12_381" and n == 1 << 20 and os.path.exists(single_path):
+        with open(single_path) as f:
+            ks = json.load(f)
+        rocprof_ms = ks["accumulate_phase_avg_ms"]
+        rocprof_src = "profiles/r01/rocprof_single/kernel_single.json (%s)" % ks["command"]
     roofline = {
         "bound": "hbm",
         "achieved": achieved / 1e9 if achieved else None,
@@ -449,27 +462,24 @@ def main():
         "traffic": traffic,
         "traffic_source": traffic_src,
         "rocprof_kernel_avg_ms": rocprof_ms,
-        "timing_note": "kernel_ms = HIP events on the kernel's stream around k_accumulate + k_fixup in the "
-                       "12-deep pipelined region: includes time the launch waits for CUs held by other "
-                       "batches; rocprof_kernel_avg_ms is k_accumulate begin-to-end in the same pipelined "
-                       "command; compute.single_batch_* time the kernel alone",
+        "rocprof_source": rocprof_src,
+        "timing_note": "kernel_ms = HIP events around k_accumulate + k_fixup of a non-pipelined batch in "
+                       "this run (rocprof_kernel_avg_ms: the same two kernels, rocprofv3 kernel trace of "
+                       "single batches); kernel_ms_in_pipelined_region includes queueing behind other slots",
         "kernel": "k_accumulate+k_fixup (bucket accumulation)",
         "kernel_ms": acc_ms,
+        "kernel_ms_in_pipelined_region": acc_ms_pipe,
         "algorithmic_bytes": alg_bytes,
-        "note": "integer-multiply bound, not HBM: see compute",
+        "note": "integer-multiply (VALU) bound, not HBM: see compute",
         "compute": {
             "bound": "valu_mad_u64_u32",
+            "model": "10 Fp products (8M + 2S) per mixed addition, 32 n additions per batch",
             "achieved_fpmul_per_s": acc_fpmuls / (acc_ms * 1e-3) if acc_ms > 0 else None,
             "peak_fpmul_per_s": fpmul_peak,
             "frac": (acc_fpmuls / (acc_ms * 1e-3)) / fpmul_peak if acc_ms > 0 else None,
             # whole pipeline: accumulation products per second of wall time (batches/s x
             # products per batch) against the probe peak -- what the overlap actually sustains
             "pipeline_frac": acc_fpmuls * value / world / fpmul_peak,
-            # the same kernel timed alone (non-pipelined batch): its own efficiency, without
-            # the time-sharing with other slots' kernels that stretches the in-region figure
-            "single_batch_kernel_ms": (phases_single or {}).get("accumulate"),
-            "single_batch_frac": (acc_fpmuls / (phases_single["accumulate"] * 1e-3)) / fpmul_peak
-            if phases_single and phases_single.get("accumulate") else None,
         },
     }
     cpu = None
