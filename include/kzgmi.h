@@ -202,6 +202,9 @@ void kzgmi_ck_free(kzgmi_ck* ck);
 int kzgmi_commit(kzgmi_ctx* ctx, const kzgmi_ck* ck, const uint8_t* coeffs, size_t m, uint8_t* out);
 int kzgmi_commit_device(kzgmi_ctx* ctx, const kzgmi_ck* ck, const void* d_coeffs, size_t m,
                         uint8_t* out);
+/* Pipelined form: enqueue on workspace `slot`; kzgmi_msm_wait(ctx, slot, out) returns the
+ * commitment (G1 encoding). */
+int kzgmi_commit_device_async(kzgmi_ctx* ctx, const kzgmi_ck* ck, int slot, const void* d_coeffs, size_t m);
 
 /* Optimal-ate pairing e(P, Q) (cubed for BLS12-381, as in the oracle), 12 Fp values in
  * tower order, big-endian: 576 B (BLS12-381) / 384 B (BN254).  Test/diagnostic utility. */

@@ -783,13 +783,13 @@ void kzgmi_ck_free(kzgmi_ck* ck) {
   delete ck;
 }
 
-int kzgmi_commit_device(kzgmi_ctx* c, const kzgmi_ck* ck, const void* d_coeffs, size_t m, uint8_t* out) {
-  CHK(check_ctx(c));
+int kzgmi_commit_device_async(kzgmi_ctx* c, const kzgmi_ck* ck, int slot, const void* d_coeffs, size_t m) {
+  CHK(check_ctx(c, slot));
   if (!ck || ck->ctx != c) return fail(KZGMI_ERR_ARG, "commit key does not belong to this context");
-  if (!out || (m && !d_coeffs)) return fail(KZGMI_ERR_ARG, "null argument");
+  if (m && !d_coeffs) return fail(KZGMI_ERR_ARG, "null argument");
   if (m > ck->n) return fail(KZGMI_ERR_ARG, "more coefficients than commit-key points");
-  Slot& s = c->slots[0];
-  if (s.pending) return fail(KZGMI_ERR_ARG, "slot 0 busy: call kzgmi_slot_wait first");
+  Slot& s = c->slots[slot];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_msm_wait first");
   return dispatch(ck->curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     using L = Launch<Cv>;
@@ -821,10 +821,20 @@ int kzgmi_commit_device(kzgmi_ctx* c, const kzgmi_ck* ck, const void* d_coeffs, 
     }
     Launch<Cv>::encode_points(st, s.res.template as<Xyzz<Cv>>(), 1, s.outb.template as<uint8_t>());
     HIPCHK(hipGetLastError());
-    CHK(read_flags_sync(c, s));
-    HIPCHK(hipMemcpy(out, s.outb.p, gb, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(s.host_out, s.outb.p, gb, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
+    s.pending = true;
+    s.partial_job = false;
+    s.msm_job = true;
+    s.curve = Cv::ID;
     return 0;
   });
+}
+
+int kzgmi_commit_device(kzgmi_ctx* c, const kzgmi_ck* ck, const void* d_coeffs, size_t m, uint8_t* out) {
+  if (!out) return fail(KZGMI_ERR_ARG, "null argument");
+  CHK(kzgmi_commit_device_async(c, ck, 0, d_coeffs, m));
+  return kzgmi_msm_wait(c, 0, out);
 }
 
 int kzgmi_commit(kzgmi_ctx* c, const kzgmi_ck* ck, const uint8_t* coeffs, size_t m, uint8_t* out) {

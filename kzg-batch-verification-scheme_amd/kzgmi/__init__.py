@@ -84,6 +84,7 @@ def lib():
         "kzgmi_msm_g1_device_async": ([vp, c.c_int, c.c_int, vp, vp, sz], c.c_int),
         "kzgmi_msm_wait": ([vp, c.c_int, u8p], c.c_int),
         "kzgmi_set_glv": ([vp, c.c_int, c.c_int], c.c_int),
+        "kzgmi_commit_device_async": ([vp, vp, c.c_int, vp, sz], c.c_int),
         "kzgmi_set_trusted_g1": ([vp, c.c_int], c.c_int),
         "kzgmi_msm_partial_device_async": ([vp, c.c_int, c.c_int, vp, vp, sz, vp], c.c_int),
         "kzgmi_msm_combine_device_async": ([vp, c.c_int, c.c_int, vp, c.c_int], c.c_int),
@@ -121,7 +122,7 @@ def exported_symbols():
         "kzgmi_fs_challenge_device", "kzgmi_fs_chunk_digests_device",
         "kzgmi_fs_challenge_from_digests_device",
         "kzgmi_last_combination", "kzgmi_msm_g1", "kzgmi_msm_g1_device", "kzgmi_msm_g1_device_async",
-        "kzgmi_msm_wait", "kzgmi_set_glv", "kzgmi_set_trusted_g1", "kzgmi_msm_partial_device_async", "kzgmi_msm_combine_device_async", "kzgmi_partial_bytes",
+        "kzgmi_msm_wait", "kzgmi_set_glv", "kzgmi_commit_device_async", "kzgmi_set_trusted_g1", "kzgmi_msm_partial_device_async", "kzgmi_msm_combine_device_async", "kzgmi_partial_bytes",
         "kzgmi_batch_partial_device", "kzgmi_batch_combine_device", "kzgmi_batch_partial_device_async",
         "kzgmi_batch_combine_device_async", "kzgmi_msm_partial_device",
         "kzgmi_msm_combine_device", "kzgmi_pairing", "kzgmi_gen_g1", "kzgmi_gen_tuples",
@@ -311,6 +312,13 @@ class Context:
         return out.raw
 
     # ------------------------------------------------------------------ Fiat-Shamir
+    def commit_async(self, ck: CommitKey, slot: int, coeffs, m: int):
+        """Enqueue a fixed-base commitment of m device-resident coefficients on `slot`;
+        msm_wait(slot) returns it."""
+        self._msm_curve = getattr(self, "_msm_curve", {})
+        self._msm_curve[slot] = ck.curve
+        _check(lib().kzgmi_commit_device_async(self.handle, ck.handle, int(slot), _dptr(coeffs), int(m)))
+
     def fs_challenge(self, curve: str, commitments, zs, ys, proofs, n: int, compressed: bool = False) -> int:
         """r of KZGMI_FLAG_FIAT_SHAMIR for device-resident inputs."""
         out = ctypes.create_string_buffer(32)

@@ -21,7 +21,7 @@ TAU = 0x1F2E3D4C5B6A7988
 @pytest.fixture(scope="module")
 def ctx():
     import kzgmi
-    c = kzgmi.Context(0, 1)
+    c = kzgmi.Context(0, 2)
     yield c
     c.close()
 
@@ -68,6 +68,27 @@ def test_commit_matches_msm(ctx, curve):
     for cs in [[0] * 50, [C.r - 1] * 50, [0] * 49 + [7]]:
         assert ctx.commit(ck, _fr(cs)) == O.msm_g1(curve, powers[:50 * g1b], _fr(cs), 50)
     assert ctx.commit(ck, b"") == pk.g1_to_bytes(None, C)
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_commit_async_slots(ctx, curve):
+    """Pipelined commits: two in flight on slots 0/1, results in order, bit-exact."""
+    import torch
+    C = pc.CURVES[curve]
+    n = 200
+    powers = _powers(curve, n)
+    ck = ctx.load_commit_key(curve, powers)
+    rng = random.Random(8)
+    g1b = 2 * C.fp_bytes
+    css = [[rng.randrange(C.r) for _ in range(m)] for m in (200, 37, 0)]
+    dev = [torch.frombuffer(bytearray(_fr(cs) or bytes(32)), dtype=torch.uint8).cuda() for cs in css]
+    want = [O.msm_g1(curve, powers[:len(cs) * g1b], _fr(cs), len(cs)) for cs in css]
+    ctx.commit_async(ck, 0, dev[0], len(css[0]))
+    ctx.commit_async(ck, 1, dev[1], len(css[1]))
+    assert ctx.msm_wait(1) == want[1]
+    ctx.commit_async(ck, 1, dev[2], 0)
+    assert ctx.msm_wait(0) == want[0]
+    assert ctx.msm_wait(1) == want[2] == pk.g1_to_bytes(None, C)
 
 
 @pytest.mark.parametrize("curve", CURVES)
