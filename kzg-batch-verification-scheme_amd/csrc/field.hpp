@@ -161,18 +161,24 @@ KZ_DEV void mac32s(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b_uniform)
       : "v"(a), "s"(b_uniform));
 }
 
-template <class P>
-KZ_DEV Fp<P> fp_mul_ps(const Fp<P>& a, const Fp<P>& b) {
+// One column scan for every product form.  TWO: (a b + c d) R^-1 with ONE reduction (the a b,
+// c d and m p terms of a column go into the same 96-bit accumulator: <= 36 limb products per
+// column).  Returns t = (a b [+ c d] + m p) / R before any final correction.
+template <class P, bool TWO>
+KZ_DEV Fp<P> mont_scan(const Fp<P>& a, const Fp<P>& b, const Fp<P>& c, const Fp<P>& d) {
   constexpr int N = P::N;
-  uint32_t m[N], t[N];
+  uint32_t m[N];
+  Fp<P> t;
   uint64_t acc = 0;
   uint32_t top = 0;
   _Pragma("unroll") for (int k = 0; k < N; ++k) {
     _Pragma("unroll") for (int i = 0; i < k; ++i) {
       mac32(acc, top, a.v[i], b.v[k - i]);
+      if constexpr (TWO) mac32(acc, top, c.v[i], d.v[k - i]);
       mac32s(acc, top, m[i], P::MOD[k - i]);
     }
     mac32(acc, top, a.v[k], b.v[0]);
+    if constexpr (TWO) mac32(acc, top, c.v[k], d.v[0]);
     m[k] = (uint32_t)acc * P::INV;
     mac32s(acc, top, m[k], P::MOD[0]);  // low word becomes 0
     acc = (acc >> 32) | ((uint64_t)top << 32);
@@ -181,18 +187,31 @@ KZ_DEV Fp<P> fp_mul_ps(const Fp<P>& a, const Fp<P>& b) {
   _Pragma("unroll") for (int k = N; k < 2 * N - 1; ++k) {
     _Pragma("unroll") for (int i = k - N + 1; i < N; ++i) {
       mac32(acc, top, a.v[i], b.v[k - i]);
+      if constexpr (TWO) mac32(acc, top, c.v[i], d.v[k - i]);
       mac32s(acc, top, m[i], P::MOD[k - i]);
     }
-    t[k - N] = (uint32_t)acc;
+    t.v[k - N] = (uint32_t)acc;
     acc = (acc >> 32) | ((uint64_t)top << 32);
     top = 0;
   }
-  t[N - 1] = (uint32_t)acc;  // (ab + mp)/R < 2p < 2^(32N): no further words
+  t.v[N - 1] = (uint32_t)acc;  // < 2^(32N) for every caller's input bound: no further words
+  return t;
+}
+
+// t >= M ? t - M : t  for a modulus-sized constant M (P::MOD or P::MOD2)
+template <class P>
+KZ_DEV Fp<P> fp_csub(const Fp<P>& t, const uint32_t (&M)[P::N]) {
   Fp<P> r, d;
   uint32_t bw = 0;
-  _Pragma("unroll") for (int i = 0; i < N; ++i) d.v[i] = __builtin_subc(t[i], P::MOD[i], bw, &bw);
-  _Pragma("unroll") for (int i = 0; i < N; ++i) r.v[i] = bw ? t[i] : d.v[i];
+  _Pragma("unroll") for (int i = 0; i < P::N; ++i) d.v[i] = __builtin_subc(t.v[i], M[i], bw, &bw);
+  _Pragma("unroll") for (int i = 0; i < P::N; ++i) r.v[i] = bw ? t.v[i] : d.v[i];
   return r;
+}
+
+// canonical inputs < p: (ab + mp)/R < 2p, one conditional subtraction
+template <class P>
+KZ_DEV Fp<P> fp_mul_ps(const Fp<P>& a, const Fp<P>& b) {
+  return fp_csub<P>(mont_scan<P, false>(a, b, a, b), P::MOD);
 }
 
 // ---------------------------------------------------------------------------- lazy reduction
@@ -203,79 +222,25 @@ KZ_DEV Fp<P> fp_mul_ps(const Fp<P>& a, const Fp<P>& b) {
 // the range with one conditional correction by 2p, and zero tests accept {0, p}.  Values are
 // made canonical (fp_canon) before they leave the loop.
 template <class P>
+constexpr bool kFourPBelowR = P::MOD[P::N - 1] < (1u << 30);  // 4p < R = 2^(32N)
+template <class P>
+constexpr bool kEightPBelowR = P::MOD[P::N - 1] < (1u << 29);
+
+template <class P>
 KZ_DEV Fp<P> fp_mul_lazy(const Fp<P>& a, const Fp<P>& b) {
-  constexpr int N = P::N;
-  uint32_t m[N];
-  Fp<P> t;
-  uint64_t acc = 0;
-  uint32_t top = 0;
-  _Pragma("unroll") for (int k = 0; k < N; ++k) {
-    _Pragma("unroll") for (int i = 0; i < k; ++i) {
-      mac32(acc, top, a.v[i], b.v[k - i]);
-      mac32s(acc, top, m[i], P::MOD[k - i]);
-    }
-    mac32(acc, top, a.v[k], b.v[0]);
-    m[k] = (uint32_t)acc * P::INV;
-    mac32s(acc, top, m[k], P::MOD[0]);
-    acc = (acc >> 32) | ((uint64_t)top << 32);
-    top = 0;
-  }
-  _Pragma("unroll") for (int k = N; k < 2 * N - 1; ++k) {
-    _Pragma("unroll") for (int i = k - N + 1; i < N; ++i) {
-      mac32(acc, top, a.v[i], b.v[k - i]);
-      mac32s(acc, top, m[i], P::MOD[k - i]);
-    }
-    t.v[k - N] = (uint32_t)acc;
-    acc = (acc >> 32) | ((uint64_t)top << 32);
-    top = 0;
-  }
-  t.v[N - 1] = (uint32_t)acc;
-  return t;  // < 2p
+  static_assert(kFourPBelowR<P>, "lazy reduction needs 4p < R");
+  return mont_scan<P, false>(a, b, a, b);  // < 2p
 }
 
-// (a b + c d) R^-1 with ONE Montgomery reduction: the columns of the product scan take the
-// a b, c d and m p terms together (<= 36 limb products per column, within the 96-bit column
-// accumulator).  Lazy inputs <= 2p: (ab + cd + mp)/R < p (8p/R + 1), < 2p when 8p < R
-// (BLS12-381: 8p/R = 0.82); BN254 (8p/R = 1.51, result < 2.51p) folds 2p once more.
-// Replaces two products + an addition: 432 instead of 576 multiply-adds.
+// (a b + c d) R^-1, lazy inputs <= 2p: < p (8p/R + 1), i.e. < 2p when 8p < R (BLS12-381:
+// 8p/R = 0.82); BN254 (8p/R = 1.51, < 2.51p) folds 2p once more.  Replaces two products and an
+// addition: 432 instead of 576 multiply-adds.
 template <class P>
 KZ_DEV Fp<P> fp_mul2_lazy(const Fp<P>& a, const Fp<P>& b, const Fp<P>& c, const Fp<P>& d) {
-  constexpr int N = P::N;
-  uint32_t m[N];
-  Fp<P> t;
-  uint64_t acc = 0;
-  uint32_t top = 0;
-  _Pragma("unroll") for (int k = 0; k < N; ++k) {
-    _Pragma("unroll") for (int i = 0; i < k; ++i) {
-      mac32(acc, top, a.v[i], b.v[k - i]);
-      mac32(acc, top, c.v[i], d.v[k - i]);
-      mac32s(acc, top, m[i], P::MOD[k - i]);
-    }
-    mac32(acc, top, a.v[k], b.v[0]);
-    mac32(acc, top, c.v[k], d.v[0]);
-    m[k] = (uint32_t)acc * P::INV;
-    mac32s(acc, top, m[k], P::MOD[0]);
-    acc = (acc >> 32) | ((uint64_t)top << 32);
-    top = 0;
-  }
-  _Pragma("unroll") for (int k = N; k < 2 * N - 1; ++k) {
-    _Pragma("unroll") for (int i = k - N + 1; i < N; ++i) {
-      mac32(acc, top, a.v[i], b.v[k - i]);
-      mac32(acc, top, c.v[i], d.v[k - i]);
-      mac32s(acc, top, m[i], P::MOD[k - i]);
-    }
-    t.v[k - N] = (uint32_t)acc;
-    acc = (acc >> 32) | ((uint64_t)top << 32);
-    top = 0;
-  }
-  t.v[N - 1] = (uint32_t)acc;
-  if constexpr (P::MOD[N - 1] >= (1u << 29)) {  // 8p >= R (BN254: 8p/R = 1.51): t < 2.51p, fold once
-    Fp<P> u;
-    uint32_t bw = 0;
-    _Pragma("unroll") for (int i = 0; i < N; ++i) u.v[i] = __builtin_subc(t.v[i], P::MOD2[i], bw, &bw);
-    _Pragma("unroll") for (int i = 0; i < N; ++i) t.v[i] = bw ? t.v[i] : u.v[i];
-  }
-  return t;  // < 2p
+  static_assert(kFourPBelowR<P>, "lazy reduction needs 4p < R");
+  const Fp<P> t = mont_scan<P, true>(a, b, c, d);
+  if constexpr (kEightPBelowR<P>) return t;
+  else return fp_csub<P>(t, P::MOD2);  // < 2p
 }
 
 template <class P>
@@ -320,11 +285,7 @@ KZ_DEV bool fp_is_zero_lazy(const Fp<P>& a) {  // a < 2p: a = 0 mod p <=> a in {
 
 template <class P>
 KZ_DEV Fp<P> fp_canon(const Fp<P>& a) {  // a < 2p -> a mod p
-  Fp<P> d;
-  uint32_t bw = 0;
-  _Pragma("unroll") for (int i = 0; i < P::N; ++i) d.v[i] = __builtin_subc(a.v[i], P::MOD[i], bw, &bw);
-  _Pragma("unroll") for (int i = 0; i < P::N; ++i) d.v[i] = bw ? a.v[i] : d.v[i];
-  return d;
+  return fp_csub<P>(a, P::MOD);
 }
 
 // Default multiplication used by every kernel.
