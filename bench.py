@@ -130,7 +130,7 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20, help="tuples per GPU")
     ap.add_argument("--curve", default="bls12_381", choices=["bls12_381", "bn254"])
     ap.add_argument("--slots", type=int, default=0,
-                    help="batches in flight (default 12 single-GPU; sharded 6 + 2 combine lanes)")
+                    help="batches in flight (default 12 single-GPU; sharded 8 + 2 combine lanes)")
     ap.add_argument("--msm-steps", type=int, default=24)
     ap.add_argument("--trusted-steps", type=int, default=36,
                     help="secondary: pipelined batches with KZGMI_FLAG_TRUSTED_G1 (GLV on BLS12-381; 0 = skip)")
@@ -151,6 +151,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("warning: WORLD_SIZE=%d but --gpus=%d; using WORLD_SIZE" % (world, args.gpus))
+    if os.environ.get("KZGMI_DIST_BACKEND", "nccl") != "nccl":  # rehearsal: ranks share the GPUs
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     sharded = world > 1 or args.sharded
     if sharded:
@@ -158,11 +160,18 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # KZGMI_DIST_BACKEND=gloo: rehearsal of the N>1 orchestration with several ranks on
+        # one GPU (RCCL refuses two ranks on one device); the driver's N>1 runs use RCCL
+        backend = os.environ.get("KZGMI_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     curve, n = args.curve, args.n
-    # measured (profiles/r01/slots_sweep.txt): single 12 slots 105.6/s; sharded 6+2 lanes
-    # 103.6/s, 10+2 101.8/s, 12+2 70.5/s (more streams than hardware queues)
-    slots = args.slots if args.slots else (6 if sharded else 12)
+    # measured (profiles/r01/slots_sweep.txt, sharded_sweep.txt): single 12 slots; sharded at
+    # world 1 over RCCL, 6/8/10 slots + 2 combine lanes: 135.0/136.3/134.3 batch-verifies/s,
+    # MSM 193/217/220 M pts/s (12+2 streams exceed the hardware queues: 70/s)
+    slots = args.slots if args.slots else (8 if sharded else 12)
     lanes = 2 if sharded else 0
     ctx = kzgmi.Context(local, slots + lanes)  # + the combine lanes
     g2 = kzgmi.G2_GENERATOR[curve]
