@@ -117,6 +117,35 @@ KZ_DEV Xyzz<Cv> xyzz_add_affine_lazy(const Xyzz<Cv>& p, const Affine<Cv>& q) {
   return r;
 }
 
+// In-place form for the bucket-accumulation loop: `inf` tracks acc = O (set by the loop at a
+// bucket start, by this function when P + (-P) cancels), so the common path skips the ZZ = 0
+// test of xyzz_add_affine_lazy.  acc is undefined while inf is set.
+template <class Cv>
+KZ_DEV void xyzz_acc_affine_lazy(Xyzz<Cv>& acc, bool& inf, const Affine<Cv>& q) {
+  if (inf) {
+    acc = xyzz_from_affine(q);
+    inf = false;
+    return;
+  }
+  auto U2 = fp_mul_lazy(q.x, acc.zz);
+  auto S2 = fp_mul_lazy(q.y, acc.zzz);
+  auto P = fp_sub_lazy(U2, acc.x);
+  auto R = fp_sub_lazy(S2, acc.y);
+  if (fp_is_zero_lazy(P)) {
+    if (fp_is_zero_lazy(R)) acc = xyzz_dbl_affine(Affine<Cv>{fp_canon(q.x), fp_canon(q.y)});
+    else inf = true;
+    return;
+  }
+  auto PP = fp_mul_lazy(P, P);
+  auto PPP = fp_mul_lazy(P, PP);
+  auto Q = fp_mul_lazy(acc.x, PP);
+  const auto X3 = fp_sub_lazy(fp_sub_lazy(fp_mul_lazy(R, R), PPP), fp_add_lazy(Q, Q));
+  acc.y = fp_mul2_lazy(R, fp_sub_lazy(Q, X3), acc.y, fp_neg_lazy(PPP));  // R (Q - X3) - Y1 PPP
+  acc.x = X3;
+  acc.zz = fp_mul_lazy(acc.zz, PP);
+  acc.zzz = fp_mul_lazy(acc.zzz, PPP);
+}
+
 // P + Q, both XYZZ.  add-2008-s with the exceptional cases.
 template <class Cv>
 KZ_DEV Xyzz<Cv> xyzz_add(const Xyzz<Cv>& p, const Xyzz<Cv>& q) {

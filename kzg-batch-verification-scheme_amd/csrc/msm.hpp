@@ -356,12 +356,13 @@ template <class Cv>
 KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_t start, uint32_t len,
                       const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
                       Xyzz<Cv>* __restrict__ buckets, Xyzz<Cv>* __restrict__ part_first,
-                      Xyzz<Cv>* __restrict__ part_last) {
+                      Xyzz<Cv>* __restrict__ part_last, bool inf = false) {
   uint32_t o = off[key];
   bool started_before = o < start;
   bool ends_after = o + cnt[key] > start + len;
   Xyzz<Cv>* dst = started_before ? &part_first[chunk] : ends_after ? &part_last[chunk] : &buckets[key];
-  store_xyzz(dst, xyzz_canon(acc));  // the loop keeps coordinates lazily reduced (< 2p)
+  // the loop keeps coordinates lazily reduced (< 2p)
+  store_xyzz(dst, inf ? Xyzz<Cv>::inf() : xyzz_canon(acc));
 }
 
 template <class Cv>
@@ -382,6 +383,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
   const uint32_t end = min(start + len, total);
   Xyzz<Cv> acc = Xyzz<Cv>::inf();
   uint32_t cur = sorted_key[start];
+#ifdef KZ_ACC_OLD  // A/B reference: ZZ = 0 test per addition, canonical conditional negation
   for (uint32_t e = start; e < end; ++e) {
     uint32_t key = sorted_key[e];
     if (key != cur) {
@@ -390,14 +392,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
       cur = key;
     }
     uint32_t v = sorted_val[e];
-#ifdef KZ_EXPERIMENT_LOCAL_PTS  // timing experiment only: gathers hit 1024 cache-resident points
-    v &= 2047u;
-#endif
     Affine<Cv> p = load_affine(pts, v >> 1);
     p.y = fp_cneg(p.y, (v & 1) != 0);
     acc = xyzz_add_affine_lazy(acc, p);
   }
   acc_flush(acc, cur, chunk, start, len, off, cnt, buckets, part_first, part_last);
+#else
+  bool inf = true;  // acc = O: at every bucket start, and after P + (-P)
+  for (uint32_t e = start; e < end; ++e) {
+    uint32_t key = sorted_key[e];
+    if (key != cur) {
+      acc_flush(acc, cur, chunk, start, len, off, cnt, buckets, part_first, part_last, inf);
+      inf = true;
+      cur = key;
+    }
+    uint32_t v = sorted_val[e];
+#ifdef KZ_EXPERIMENT_LOCAL_PTS  // timing experiment only: gathers hit 1024 cache-resident points
+    v &= 2047u;
+#endif
+    Affine<Cv> p = load_affine(pts, v >> 1);
+    // -y as p - y: y != 0 for every point of odd order (no 2-torsion on either curve), and the
+    // lazy range [0, 2p) holds p - y either way -- no zero test, no canonical negation
+    p.y = fp_select((v & 1) != 0, fp_rsub_mod(p.y), p.y);
+    xyzz_acc_affine_lazy(acc, inf, p);
+  }
+  acc_flush(acc, cur, chunk, start, len, off, cnt, buckets, part_first, part_last, inf);
+#endif
 }
 
 // joins the pieces of buckets that cross chunk boundaries (launched with the same grid as

@@ -14,7 +14,7 @@ import sys
 
 src, dst = sys.argv[1], sys.argv[2]
 os.makedirs(dst, exist_ok=True)
-stats = glob.glob(os.path.join(src, "**", "*kernel_stats.csv"), recursive=True)[0]
+stats = sorted(glob.glob(os.path.join(src, "**", "*kernel_stats.csv"), recursive=True))[0]
 shutil.copy(stats, os.path.join(dst, "kernel_stats_single_batch.csv"))
 rows = sorted(csv.DictReader(open(stats)), key=lambda r: -float(r["TotalDurationNs"]))
 with open(os.path.join(dst, "kernel_stats_top.txt"), "w") as f:
@@ -36,3 +36,43 @@ out = {"command": "rocprofv3 --kernel-trace --stats -- python3 tools/phase_timin
        "k_accumulate_avg_ms": acc / 1e6, "k_fixup_avg_ms": fix / 1e6, "accumulate_phase_avg_ms": (acc + fix) / 1e6}
 json.dump(out, open(os.path.join(dst, "kernel_single.json"), "w"), indent=1)
 print(json.dumps(out))
+
+
+# ---- PMC passes of tools/profile_single.sh (absent for the plain kt_single.sh trace)
+def per_launch(kind, counter=None):
+    files = glob.glob(os.path.join(src, kind, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        return None
+    vals = {}
+    for r in csv.DictReader(open(files[0])):
+        if r["Kernel_Name"].startswith("void kzgmi::k_accumulate<kzgmi::Bls12_381>") and \
+                (counter is None or r["Counter_Name"] == counter):
+            vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return list(vals.values())
+
+
+fetch, write = per_launch("fetch_size"), per_launch("write_size")
+if fetch and write:
+    n = 1 << 20
+    entries = 32 * n  # window terms of one batch
+    fetch_kib, write_kib = sum(fetch) / len(fetch), sum(write) / len(write)
+    hit, miss = per_launch("tcc_hit_sum", "TCC_HIT_sum"), per_launch("tcc_hit_sum", "TCC_MISS_sum")
+    pmc = {
+        "kernel": "k_accumulate<Bls12_381>",
+        "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | TCC_HIT_sum TCC_MISS_sum (separate passes) "
+                   "-- python3 tools/phase_timing.py --reps 2 (n = 2^20, single batches)",
+        "launches_fetch": len(fetch), "launches_write": len(write),
+        "FETCH_SIZE_KiB_per_launch_raw": fetch_kib,
+        "WRITE_SIZE_KiB_per_launch": write_kib,
+        "traffic_bytes_per_launch": (2 * fetch_kib + write_kib) * 1024,
+        "correction": "FETCH_SIZE x 2 (gfx950 tallies 128-B read requests at 64 B, MI355X_MICROARCH.md HBM); "
+                      "Infinity-Cache hits are counted, so this is L2-miss traffic, an upper bound on HBM bytes",
+        "algorithmic_bytes_per_launch": 256 * n,
+        "gather_model_bytes_per_launch": entries * (96 + 8),
+        "gather_model": "every window term gathers its 96-B affine point and reads its 8-B sorted entry "
+                        "(32 terms per tuple): the traffic Pippenger accumulation touches by construction",
+        "tcc_hit_rate": (sum(hit) / (sum(hit) + sum(miss))) if hit and miss else None,
+        "k_accumulate_avg_ms": acc / 1e6,
+    }
+    json.dump(pmc, open(os.path.join(dst, "pmc_accumulate_single.json"), "w"), indent=1)
+    print(json.dumps(pmc, indent=1))
