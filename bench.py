@@ -467,14 +467,18 @@ def main():
     acc_fpmuls = 32 * n * 10
     # PMC traffic of the same kernel and config from the committed profile (tools/profile.sh:
     # separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE x 2 as MI355X_MICROARCH.md prescribes)
-    traffic, traffic_src, rocprof_ms, rocprof_src = None, None, None, None
-    pmc_path = os.path.join(ROOT, "profiles", "r01", "rocprof", "pmc_accumulate.json")
+    traffic, traffic_src, rocprof_ms, rocprof_src, gather_bytes = None, None, None, None, None
+    pmc_path = os.path.join(ROOT, "profiles", "r01", "rocprof_single", "pmc_accumulate_single.json")
     single_path = os.path.join(ROOT, "profiles", "r01", "rocprof_single", "kernel_single.json")
     if curve == "bls12_381" and n == 1 << 20 and os.path.exists(pmc_path):
         with open(pmc_path) as f:
             pmc = json.load(f)
-        traffic = pmc["traffic_bytes_per_launch"]
-        traffic_src = "profiles/r01/rocprof/pmc_accumulate.json (%s)" % pmc["command"]
+        # FETCH_SIZE as counted (x1): the kernel's loads are 16-B-per-lane gathers of scattered
+        # 128-B points, not the wide streaming reads the guide's x2 correction was calibrated on
+        # (x2 would exceed the two 128-B lines a point can touch)
+        traffic = (pmc["FETCH_SIZE_KiB_per_launch_raw"] + pmc["WRITE_SIZE_KiB_per_launch"]) * 1024
+        traffic_src = "profiles/r01/rocprof_single/pmc_accumulate_single.json (%s; FETCH_SIZE + WRITE_SIZE)" % pmc["command"]
+        gather_bytes = pmc.get("gather_model_bytes_per_launch")
     if curve == "bls12_381" and n == 1 << 20 and os.path.exists(single_path):
         with open(single_path) as f:
             ks = json.load(f)
@@ -488,6 +492,10 @@ def main():
         "frac": (achieved / HBM_PEAK) if achieved else None,
         "traffic": traffic,
         "traffic_source": traffic_src,
+        "gather_model_bytes": gather_bytes,
+        "gather_note": "Pippenger accumulation gathers one 96-B point (stored at a 128-B stride) and one 8-B "
+                       "sorted entry per window term, 32 terms per tuple: traffic above the 256 B/tuple of "
+                       "unique input is inherent to the bucket method, not a re-read to fix",
         "rocprof_kernel_avg_ms": rocprof_ms,
         "rocprof_source": rocprof_src,
         "timing_note": "kernel_ms = HIP events around k_accumulate + k_fixup of a non-pipelined batch in "

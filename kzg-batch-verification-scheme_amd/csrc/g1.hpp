@@ -10,8 +10,15 @@
 
 namespace kzgmi {
 
+// In HBM, affine points are padded to a power-of-two stride (BLS12-381: 96 -> 128 B, BN254
+// 64 B as is) so that each bucket-accumulation gather touches exactly one 128-B line instead
+// of 1.5 on average: L2-miss traffic of k_accumulate measured 211 B per window term with
+// 96-B points (profiles/r01/rocprof_single/pmc_accumulate_single.json).
 template <class Cv>
-struct Affine {
+constexpr int kAffineAlign = 2 * Cv::FpP::N * 4 == 96 ? 128 : 2 * Cv::FpP::N * 4;
+
+template <class Cv>
+struct alignas(kAffineAlign<Cv>) Affine {
   using F = Fp<typename Cv::FpP>;
   F x, y;
 };
