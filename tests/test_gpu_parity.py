@@ -131,6 +131,38 @@ def test_msm_skewed_buckets(ctx, curve):
 
 
 @pytest.mark.parametrize("curve", CURVES)
+def test_msm_cancelling_buckets(ctx, curve):
+    """Buckets whose running sum returns to infinity mid-chunk (P + (-P)), then keeps adding
+    (the accumulation's infinity flag, csrc/g1.hpp xyzz_acc_affine_lazy), doubling (P + P),
+    pieces that cancel across chunk boundaries (k_fixup), and an all-cancelling MSM (result
+    infinity).  Equal scalars put every term of a window into one bucket."""
+    C = pc.CURVES[curve]
+    rng = random.Random(29)
+    ks = [rng.randrange(1, C.r) for _ in range(6)]
+    allk = ks + [C.r - k for k in ks]  # P_j, then -P_j
+    base = O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(k) for k in allk), len(allk))
+    g1b = 2 * C.fp_bytes
+    pt = lambda j: base[j * g1b:(j + 1) * g1b]  # noqa: E731
+    cases = [
+        [pt(0), pt(6)] * 1500 + [pt(1), pt(2)],                      # +-P0 pairs, then two survivors
+        [pt(0), pt(0), pt(6), pt(6), pt(1)] * 700,                   # P0 + P0 doublings, -P0 cancels
+        [pt(j % 6) for j in range(2000)] + [pt(6 + j % 6) for j in range(2000)],  # all cancel: O
+        [pt(3), pt(9)] * 40 + [pt(4)],                               # short: single chunk
+    ]
+    try:
+        for trusted in (False, True):  # True: points declared G1 members -> GLV split path
+            ctx.set_trusted_g1(trusted)
+            for terms in cases:
+                n = len(terms)
+                pts = b"".join(terms)
+                for s in [5, C.r - 3, 0x10000]:
+                    sc = b"".join(pk.fr_to_bytes(s) for _ in range(n))
+                    assert ctx.msm_g1(curve, pts, sc) == O.msm_g1(curve, pts, sc, n), (trusted, n, s)
+    finally:
+        ctx.set_trusted_g1(False)
+
+
+@pytest.mark.parametrize("curve", CURVES)
 def test_gen_g1_vs_oracle(ctx, curve, torch_dev):
     torch = torch_dev
     C = pc.CURVES[curve]
