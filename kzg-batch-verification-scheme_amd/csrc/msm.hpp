@@ -499,6 +499,31 @@ KZ_DEV Xyzz<Cv> xyzz_mul_pow2(Xyzz<Cv> p, int k) {
   return p;
 }
 
+// 2^k P for the Horner steps of the window combination: the k doublings run in a = 0 Jacobian
+// coordinates (dbl-2009-l, 2M + 5S = 7 products) instead of XYZZ (6M + 3S = 9).  Entering
+// costs 6 products -- with ZZ = Z^2, ZZZ = Z^3 take Z' = ZZ ZZZ = Z^5, X' = X ZZ ZZZ^2 = X Z^8,
+// Y' = Y ZZZ^4 = Y Z^12 -- and leaving 2 (ZZ = Z'^2, ZZZ = Z'^3): 120 instead of 144 products for
+// k = 16.  Infinity (ZZ = 0) gives Z' = 0, which doubling keeps and which maps back to ZZ = 0.
+template <class Cv>
+__device__ __noinline__ Xyzz<Cv> xyzz_mul_pow2_jac(const Xyzz<Cv>& p, int k) {
+  const auto Z3sq = fp_sqr(p.zzz);
+  auto X = fp_mul(p.x, fp_mul(p.zz, Z3sq));
+  auto Y = fp_mul(p.y, fp_sqr(Z3sq));
+  auto Z = fp_mul(p.zz, p.zzz);
+  for (int i = 0; i < k; ++i) {
+    const auto A = fp_sqr(X);
+    const auto B = fp_sqr(Y);
+    const auto C = fp_sqr(B);
+    const auto D = fp_dbl(fp_sub(fp_sub(fp_sqr(fp_add(X, B)), A), C));
+    const auto E = fp_mul3(A);
+    Z = fp_dbl(fp_mul(Y, Z));
+    X = fp_sub(fp_sqr(E), fp_dbl(D));
+    Y = fp_sub(fp_mul(E, fp_sub(D, X)), fp_mul8(C));
+  }
+  const auto ZZ = fp_sqr(Z);
+  return {X, Y, ZZ, fp_mul(ZZ, Z)};
+}
+
 // One 256-thread workgroup per window (set).  Window sum
 //   W = sum_b (b+1) S_b = sum_g (R_g + U_g) + SEG * sum_g g U_g.
 // sum_g g U_g (2048 terms) is itself split into 16-term segments twice (in LDS scratch).
@@ -550,6 +575,59 @@ __global__ void __launch_bounds__(256) k_reduce_finish(const Xyzz<Cv>* __restric
   }
 }
 
+// Latency form of the window sums (replaces k_reduce_finish's three serial segment levels,
+// ~130 dependent point operations on one lane per set, by ~40):
+//   W = sum_g (R_g + U_g) + SEG * sum_g g U_g,   sum_g g U_g = sum_j 2^j B_j,
+//   B_j = sum of the 1024 U_g whose index g has bit j set (j < 11, NSEG = 2^11).
+// k_reduce_bits: RB_PARTS workgroups per set -- 11 compute B_j, 4 compute quarter sums of
+// R_g + U_g -- each 4 points per thread + an 8-level LDS tree.  k_reduce_bits_finish: one thread
+// per set, Horner over the 11 bit sums (10 doublings + 10 additions) + 4 doublings.
+constexpr int RB_PARTS = 15;
+
+template <class Cv>
+__global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict__ R, const Xyzz<Cv>* __restrict__ U,
+                                                     Xyzz<Cv>* __restrict__ parts) {
+  constexpr uint32_t NSEG = NBUCKETS / SEG;  // 2048 = 2^11
+  static_assert(NSEG == 2048 && RB_PARTS == 15, "bit decomposition assumes 2^11 segments per set");
+  __shared__ __attribute__((aligned(16))) Xyzz<Cv> lds[128];
+  const uint32_t set = blockIdx.x / RB_PARTS, j = blockIdx.x % RB_PARTS;
+  const Xyzz<Cv>* Rs = R + (size_t)set * NSEG;
+  const Xyzz<Cv>* Us = U + (size_t)set * NSEG;
+  const uint32_t t = threadIdx.x;
+  Xyzz<Cv> s = Xyzz<Cv>::inf();
+  if (j < 11) {
+#pragma unroll 1
+    for (uint32_t i = 0; i < 4; ++i) {  // q: 10-bit rank among the g with bit j set
+      const uint32_t q = t + 256 * i;
+      const uint32_t g = ((q >> j) << (j + 1)) | (1u << j) | (q & ((1u << j) - 1));
+      s = xyzz_add_c(s, load_xyzz(&Us[g]));
+    }
+  } else {
+    const uint32_t base = (j - 11) * (NSEG / 4);
+#pragma unroll 1
+    for (uint32_t i = 0; i < 2; ++i) {
+      const uint32_t g = base + t + 256 * i;
+      s = xyzz_add_c(s, load_xyzz(&Rs[g]));
+      s = xyzz_add_c(s, load_xyzz(&Us[g]));
+    }
+  }
+  const Xyzz<Cv> v = block_sum256(s, lds);
+  if (t == 0) store_xyzz(&parts[(size_t)set * RB_PARTS + j], v);
+}
+
+template <class Cv>
+__global__ void __launch_bounds__(64) k_reduce_bits_finish(uint32_t nsets, const Xyzz<Cv>* __restrict__ parts,
+                                                           Xyzz<Cv>* __restrict__ winsum) {
+  const uint32_t set = blockIdx.x * blockDim.x + threadIdx.x;
+  if (set >= nsets) return;
+  const Xyzz<Cv>* P = parts + (size_t)set * RB_PARTS;
+  Xyzz<Cv> V = load_xyzz(&P[10]);
+  for (int j = 9; j >= 0; --j) V = xyzz_add_c(xyzz_dbl_c(V), load_xyzz(&P[j]));
+  Xyzz<Cv> W = xyzz_add_c(xyzz_add_c(load_xyzz(&P[11]), load_xyzz(&P[12])),
+                          xyzz_add_c(load_xyzz(&P[13]), load_xyzz(&P[14])));
+  store_xyzz(&winsum[set], xyzz_add_c(W, xyzz_mul_pow2(V, 4)));
+}
+
 // Horner over windows for each MSM: res[m] = sum_w 2^(16 w) winsum[set_base_m + w]
 struct MsmWindows {
   uint32_t nmsm;
@@ -563,7 +641,11 @@ __global__ void k_window_combine(MsmWindows mw, const Xyzz<Cv>* __restrict__ win
   const Xyzz<Cv>* W = winsum + mw.set_base[m];
   Xyzz<Cv> acc = load_xyzz(&W[mw.nwin[m] - 1]);
   for (int w = (int)mw.nwin[m] - 2; w >= 0; --w) {
+#ifdef KZ_COMBINE_OLD  // A/B reference: XYZZ doublings
     acc = xyzz_mul_pow2(acc, WBITS);
+#else
+    acc = xyzz_mul_pow2_jac(acc, WBITS);
+#endif
     acc = xyzz_add_c(acc, load_xyzz(&W[w]));
   }
   store_xyzz(&res[m], acc);
