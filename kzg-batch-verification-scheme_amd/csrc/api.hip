@@ -462,7 +462,7 @@ int kzgmi_ctx_create(kzgmi_ctx** out, int device_id, int pipeline_slots) {
   c->device = device_id;
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_id) == hipSuccess && ncu > 0)
-    c->acc_threads = (size_t)ncu * 4 * 3 * 64;
+    c->acc_threads = (size_t)ncu * 4 * ACC_WAVES * 64;
   if (const char* e = getenv("KZGMI_ACC_THREADS")) c->acc_threads = (size_t)strtoull(e, nullptr, 10);
   c->slots.resize(pipeline_slots);
   for (auto& s : c->slots) {

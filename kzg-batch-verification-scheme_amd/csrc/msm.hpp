@@ -365,8 +365,16 @@ KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_
   store_xyzz(dst, inf ? Xyzz<Cv>::inf() : xyzz_canon(acc));
 }
 
+// Waves per SIMD the accumulation is compiled for (VGPR budget 512 / ACC_WAVES per lane); the
+// host caps the grid at one resident round of CUs x 4 SIMDs x ACC_WAVES waves (api.hip).
+#ifndef KZ_ACC_REGS
+constexpr int ACC_WAVES = 4;  // ZZ/ZZZ staged in LDS (below)
+#else
+constexpr int ACC_WAVES = 3;  // A/B reference: the whole running sum in registers (168 VGPRs)
+#endif
+
 template <class Cv>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_accumulate(const uint32_t* __restrict__ total_p,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ACC_WAVES))) k_accumulate(const uint32_t* __restrict__ total_p,
                                                     const uint32_t* __restrict__ sorted_val,
                                                     const uint32_t* __restrict__ sorted_key,
                                                     const uint32_t* __restrict__ off,
@@ -381,9 +389,81 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
   const uint32_t start = chunk * len;
   if (start >= total) return;
   const uint32_t end = min(start + len, total);
-  Xyzz<Cv> acc = Xyzz<Cv>::inf();
   uint32_t cur = sorted_key[start];
-#ifdef KZ_ACC_OLD  // A/B reference: ZZ = 0 test per addition, canonical conditional negation
+#ifndef KZ_ACC_REGS
+  // ZZ and ZZZ of the running bucket sum live in LDS (word-major per thread: conflict-free
+  // 32-bit accesses), X and Y in registers.  ZZ/ZZZ are read only at the start (U2, S2) and the
+  // end (ZZ3, ZZZ3) of an addition, so taking them out of the register file keeps the loop
+  // within 128 VGPRs: 4 waves per SIMD instead of 3.  The empty asm with a memory clobber in
+  // every access keeps them real LDS accesses (no forwarding of a stored value through
+  // registers across iterations).
+  using F = Fp<typename Cv::FpP>;
+  constexpr int N = Cv::FpP::N;
+  __shared__ uint32_t s_zz[N][256], s_zzz[N][256];
+  const uint32_t tx = threadIdx.x;
+  auto ld = [tx](uint32_t (&a)[N][256]) {
+    asm volatile("" ::: "memory");
+    F r;
+    _Pragma("unroll") for (int k = 0; k < N; ++k) r.v[k] = a[k][tx];
+    return r;
+  };
+  auto st = [tx](uint32_t (&a)[N][256], const F& v) {
+    _Pragma("unroll") for (int k = 0; k < N; ++k) a[k][tx] = v.v[k];
+    asm volatile("" ::: "memory");
+  };
+#define zzp s_zz
+#define zzzp s_zzz
+  F x, y;
+  bool inf = true;
+  for (uint32_t e = start; e < end; ++e) {
+    uint32_t key = sorted_key[e];
+    if (key != cur) {
+      acc_flush(Xyzz<Cv>{x, y, ld(zzp), ld(zzzp)}, cur, chunk, start, len, off, cnt, buckets, part_first, part_last,
+                inf);
+      inf = true;
+      cur = key;
+    }
+    uint32_t v = sorted_val[e];
+    Affine<Cv> q = load_affine(pts, v >> 1);
+    q.y = fp_select((v & 1) != 0, fp_rsub_mod(q.y), q.y);  // -y as p - y (see below)
+    if (inf) {
+      x = q.x;
+      y = q.y;
+      st(zzp, F::one());
+      st(zzzp, F::one());
+      inf = false;
+      continue;
+    }
+    const F U2 = fp_mul_lazy(q.x, ld(zzp));
+    const F S2 = fp_mul_lazy(q.y, ld(zzzp));
+    const F P = fp_sub_lazy(U2, x);
+    const F R = fp_sub_lazy(S2, y);
+    if (fp_is_zero_lazy(P)) {
+      if (fp_is_zero_lazy(R)) {
+        const Xyzz<Cv> d = xyzz_dbl_affine(Affine<Cv>{fp_canon(q.x), fp_canon(q.y)});
+        x = d.x;
+        y = d.y;
+        st(zzp, d.zz);
+        st(zzzp, d.zzz);
+      } else {
+        inf = true;
+      }
+      continue;
+    }
+    const F PP = fp_mul_lazy(P, P);
+    const F PPP = fp_mul_lazy(P, PP);
+    st(zzp, fp_mul_lazy(ld(zzp), PP));
+    st(zzzp, fp_mul_lazy(ld(zzzp), PPP));
+    const F Q = fp_mul_lazy(x, PP);
+    const F X3 = fp_sub_lazy(fp_sub_lazy(fp_mul_lazy(R, R), PPP), fp_add_lazy(Q, Q));
+    y = fp_mul2_lazy(R, fp_sub_lazy(Q, X3), y, fp_neg_lazy(PPP));  // R (Q - X3) - Y1 PPP
+    x = X3;
+  }
+  acc_flush(Xyzz<Cv>{x, y, ld(zzp), ld(zzzp)}, cur, chunk, start, len, off, cnt, buckets, part_first, part_last, inf);
+#undef zzp
+#undef zzzp
+#elif defined(KZ_ACC_OLD)  // A/B reference: ZZ = 0 test per addition, canonical conditional negation
+  Xyzz<Cv> acc = Xyzz<Cv>::inf();
   for (uint32_t e = start; e < end; ++e) {
     uint32_t key = sorted_key[e];
     if (key != cur) {
@@ -398,6 +478,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
   }
   acc_flush(acc, cur, chunk, start, len, off, cnt, buckets, part_first, part_last);
 #else
+  Xyzz<Cv> acc = Xyzz<Cv>::inf();
   bool inf = true;  // acc = O: at every bucket start, and after P + (-P)
   for (uint32_t e = start; e < end; ++e) {
     uint32_t key = sorted_key[e];
