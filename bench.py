@@ -33,9 +33,11 @@ sys.path.insert(0, os.path.join(ROOT, "kzg-batch-verification-scheme_amd"))
 
 # HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default).  The slot
 # pipeline needs about one queue per batch in flight -- batches whose streams share a queue
-# serialise (measured: 12 slots on 4 queues 77/s, on 12-16 queues 106/s).  Read by the HIP
+# serialise (measured: 12 slots on 4 queues 77/s, on 12-16 queues 106/s; after the latency-tail
+# work 12 slots x 16 queues 139-140/s, 16 x 24 142-145/s, 24 x 32 134/s: profiles/r01/
+# prio_sweep.txt).  Read by the HIP
 # runtime when it initialises, so set before torch touches the GPU.
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("KZGMI_HW_QUEUES", "16")
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("KZGMI_HW_QUEUES", "24")
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -130,7 +132,7 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20, help="tuples per GPU")
     ap.add_argument("--curve", default="bls12_381", choices=["bls12_381", "bn254"])
     ap.add_argument("--slots", type=int, default=0,
-                    help="batches in flight (default 12 single-GPU; sharded 8 + 2 combine lanes)")
+                    help="batches in flight (default 16 single-GPU; sharded 8 + 2 combine lanes)")
     ap.add_argument("--msm-steps", type=int, default=24)
     ap.add_argument("--trusted-steps", type=int, default=36,
                     help="secondary: pipelined batches with KZGMI_FLAG_TRUSTED_G1 (GLV on BLS12-381; 0 = skip)")
@@ -171,7 +173,7 @@ def main():
     # measured (profiles/r01/slots_sweep.txt, sharded_sweep.txt): single 12 slots; sharded at
     # world 1 over RCCL, 6/8/10 slots + 2 combine lanes: 135.0/136.3/134.3 batch-verifies/s,
     # MSM 193/217/220 M pts/s (12+2 streams exceed the hardware queues: 70/s)
-    slots = args.slots if args.slots else (8 if sharded else 12)
+    slots = args.slots if args.slots else (8 if sharded else 16)
     lanes = 2 if sharded else 0
     ctx = kzgmi.Context(local, slots + lanes)  # + the combine lanes
     g2 = kzgmi.G2_GENERATOR[curve]

@@ -77,7 +77,7 @@ const char* kzgmi_last_error(void);
 
 /* SURVEY.md 8b kzgmi_ctx_create: bind device `device_id` (>= 0).  `pipeline_slots` >= 1 is
  * the number of independent workspaces/streams for the async batch API (1 is enough for
- * the synchronous calls). */
+ * the synchronous calls), at most 64; each holds ~1 GiB at n = 2^20. */
 int kzgmi_ctx_create(kzgmi_ctx** out, int device_id, int pipeline_slots);
 void kzgmi_ctx_destroy(kzgmi_ctx* ctx);
 

@@ -452,7 +452,7 @@ const char* kzgmi_last_error(void) { return g_err.c_str(); }
 const char* kzgmi_phase_names(void) { return kPhaseNames; }
 
 int kzgmi_ctx_create(kzgmi_ctx** out, int device_id, int pipeline_slots) {
-  if (!out || device_id < 0 || pipeline_slots < 1 || pipeline_slots > 16) return fail(KZGMI_ERR_ARG, "bad ctx args");
+  if (!out || device_id < 0 || pipeline_slots < 1 || pipeline_slots > 64) return fail(KZGMI_ERR_ARG, "bad ctx args");
   *out = nullptr;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device_id)

@@ -13,6 +13,16 @@ enum : uint32_t { DERR_NONE = 0, DERR_ENCODING = 1, DERR_NOT_ON_CURVE = 2, DERR_
 
 KZ_DEV void raise_err(uint32_t* err, uint32_t code) { atomicMax(err, code); }
 
+// Latency-critical tail kernels (bucket-sum reduction, window combination, pairing, fix-ups)
+// run one to a few waves per CU beside the accumulation of other pipelined batches (4 waves
+// per SIMD).  Raising their wave priority lets the SIMD's issue arbiter pick them first, so a
+// batch's tail is not stretched ~4x while full-chip work shares its SIMDs.
+#ifdef KZ_NO_TAIL_PRIO
+#define KZ_TAIL_PRIO() ((void)0)
+#else
+#define KZ_TAIL_PRIO() __builtin_amdgcn_s_setprio(3)
+#endif
+
 // Fiat-Shamir transcript geometry (fs.hpp)
 constexpr uint32_t FS_CHUNK = 4096;  // leaves per shard-alignment subtree
 constexpr int FS_POW_BITS = 32;      // r^(2^k), k < 32: any global index < 2^32

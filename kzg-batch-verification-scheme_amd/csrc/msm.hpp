@@ -511,6 +511,7 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
                                                const Xyzz<Cv>* __restrict__ part_first,
                                                const Xyzz<Cv>* __restrict__ part_last,
                                                Xyzz<Cv>* __restrict__ buckets) {
+  KZ_TAIL_PRIO();
   const uint32_t total = *total_p;
   const uint32_t len = acc_chunk_len(total, gridDim.x * blockDim.x);
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x + 1;
@@ -534,6 +535,7 @@ template <class Cv>
 __global__ void __launch_bounds__(256) k_reduce_segments(uint32_t nseg, const uint32_t* __restrict__ cnt,
                                                          const Xyzz<Cv>* __restrict__ buckets,
                                                          Xyzz<Cv>* __restrict__ R, Xyzz<Cv>* __restrict__ U) {
+  KZ_TAIL_PRIO();
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nseg) return;
   Xyzz<Cv> run = Xyzz<Cv>::inf(), acc = Xyzz<Cv>::inf();
@@ -668,6 +670,7 @@ constexpr int RB_PARTS = 15;
 template <class Cv>
 __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict__ R, const Xyzz<Cv>* __restrict__ U,
                                                      Xyzz<Cv>* __restrict__ parts) {
+  KZ_TAIL_PRIO();
   constexpr uint32_t NSEG = NBUCKETS / SEG;  // 2048 = 2^11
   static_assert(NSEG == 2048 && RB_PARTS == 15, "bit decomposition assumes 2^11 segments per set");
   __shared__ __attribute__((aligned(16))) Xyzz<Cv> lds[128];
@@ -699,6 +702,7 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
 template <class Cv>
 __global__ void __launch_bounds__(64) k_reduce_bits_finish(uint32_t nsets, const Xyzz<Cv>* __restrict__ parts,
                                                            Xyzz<Cv>* __restrict__ winsum) {
+  KZ_TAIL_PRIO();
   const uint32_t set = blockIdx.x * blockDim.x + threadIdx.x;
   if (set >= nsets) return;
   const Xyzz<Cv>* P = parts + (size_t)set * RB_PARTS;
@@ -717,6 +721,7 @@ struct MsmWindows {
 };
 template <class Cv>
 __global__ void k_window_combine(MsmWindows mw, const Xyzz<Cv>* __restrict__ winsum, Xyzz<Cv>* __restrict__ res) {
+  KZ_TAIL_PRIO();
   uint32_t m = threadIdx.x;
   if (m >= mw.nmsm) return;
   const Xyzz<Cv>* W = winsum + mw.set_base[m];

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Sharded (world-1 RCCL) pipeline: batch and MSM rates vs slots in flight.
+# Sharded (world-1 RCCL) pipeline: batch and MSM rates vs slots in flight (+ 2 combine lanes).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 for s in ${SLOTS:-6 8 10}; do
