@@ -134,11 +134,11 @@ def main():
     ap.add_argument("--slots", type=int, default=0,
                     help="batches in flight (default 16 single-GPU; sharded 8 + 2 combine lanes)")
     ap.add_argument("--msm-steps", type=int, default=24)
-    ap.add_argument("--trusted-steps", type=int, default=36,
+    ap.add_argument("--trusted-steps", type=int, default=96,
                     help="secondary: pipelined batches with KZGMI_FLAG_TRUSTED_G1 (GLV on BLS12-381; 0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--fs-steps", type=int, default=36,
+    ap.add_argument("--fs-steps", type=int, default=96,
                     help="secondary: pipelined batches in Fiat-Shamir mode (r_i = r^i, 0 = skip)")
     ap.add_argument("--commit-steps", type=int, default=24,
                     help="secondary: fixed-base prover commits of n coefficients (0 = skip)")
