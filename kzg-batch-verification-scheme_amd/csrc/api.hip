@@ -212,7 +212,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   CHK(s.plast.ensure(nchunks * sizeof(XY)));
   CHK(s.R.ensure((size_t)NB / SEG * sizeof(XY)));
   CHK(s.U.ensure((size_t)NB / SEG * sizeof(XY)));
-  CHK(s.scratch.ensure((size_t)nsets * 288 * sizeof(XY)));
+  CHK(s.scratch.ensure((size_t)nsets * RB_PARTS * sizeof(XY)));  // k_reduce_bits partial sums
   CHK(s.winsum.ensure((size_t)nsets * sizeof(XY)));
   CHK(s.res.ensure(2 * sizeof(XY)));
   hipStream_t st = s.stream;

@@ -83,15 +83,6 @@ KZ_DEV Fp<P> fp_neg(const Fp<P>& a) {
   return d;
 }
 
-// conditional negation (branch-free): neg ? -a : a
-template <class P>
-KZ_DEV Fp<P> fp_cneg(const Fp<P>& a, bool neg) {
-  Fp<P> n = fp_neg(a);
-  Fp<P> r;
-  _Pragma("unroll") for (int i = 0; i < P::N; ++i) r.v[i] = neg ? n.v[i] : a.v[i];
-  return r;
-}
-
 template <class P>
 KZ_DEV Fp<P> fp_select(bool c, const Fp<P>& a, const Fp<P>& b) {
   Fp<P> r;

@@ -94,63 +94,11 @@ KZ_DEV Xyzz<Cv> xyzz_add_affine(const Xyzz<Cv>& p, const Affine<Cv>& q) {
   return r;
 }
 
-// Lazy-reduced form of xyzz_add_affine for the bucket-accumulation loop (field.hpp "lazy
-// reduction"): p's coordinates in [0, 2p), q canonical; result in [0, 2p).  The exceptional
-// cases canonicalise and use the canonical formulas (they do not occur for distinct points).
+// Canonical coordinates of a lazily reduced ([0, 2p), field.hpp "lazy reduction") point: the
+// bucket-accumulation loop (msm.hpp k_accumulate) keeps its running sum that way.
 template <class Cv>
 KZ_DEV Xyzz<Cv> xyzz_canon(const Xyzz<Cv>& p) {
   return {fp_canon(p.x), fp_canon(p.y), fp_canon(p.zz), fp_canon(p.zzz)};
-}
-
-template <class Cv>
-KZ_DEV Xyzz<Cv> xyzz_add_affine_lazy(const Xyzz<Cv>& p, const Affine<Cv>& q) {
-  if (fp_is_zero_lazy(p.zz)) return xyzz_from_affine(q);
-  auto U2 = fp_mul_lazy(q.x, p.zz);
-  auto S2 = fp_mul_lazy(q.y, p.zzz);
-  auto P = fp_sub_lazy(U2, p.x);
-  auto R = fp_sub_lazy(S2, p.y);
-  if (fp_is_zero_lazy(P)) {
-    if (fp_is_zero_lazy(R)) return xyzz_dbl_affine(q);
-    return Xyzz<Cv>::inf();
-  }
-  auto PP = fp_mul_lazy(P, P);
-  auto PPP = fp_mul_lazy(P, PP);
-  auto Q = fp_mul_lazy(p.x, PP);
-  Xyzz<Cv> r;
-  r.x = fp_sub_lazy(fp_sub_lazy(fp_mul_lazy(R, R), PPP), fp_add_lazy(Q, Q));
-  r.y = fp_mul2_lazy(R, fp_sub_lazy(Q, r.x), p.y, fp_neg_lazy(PPP));  // R (Q - X3) - Y1 PPP
-  r.zz = fp_mul_lazy(p.zz, PP);
-  r.zzz = fp_mul_lazy(p.zzz, PPP);
-  return r;
-}
-
-// In-place form for the bucket-accumulation loop: `inf` tracks acc = O (set by the loop at a
-// bucket start, by this function when P + (-P) cancels), so the common path skips the ZZ = 0
-// test of xyzz_add_affine_lazy.  acc is undefined while inf is set.
-template <class Cv>
-KZ_DEV void xyzz_acc_affine_lazy(Xyzz<Cv>& acc, bool& inf, const Affine<Cv>& q) {
-  if (inf) {
-    acc = xyzz_from_affine(q);
-    inf = false;
-    return;
-  }
-  auto U2 = fp_mul_lazy(q.x, acc.zz);
-  auto S2 = fp_mul_lazy(q.y, acc.zzz);
-  auto P = fp_sub_lazy(U2, acc.x);
-  auto R = fp_sub_lazy(S2, acc.y);
-  if (fp_is_zero_lazy(P)) {
-    if (fp_is_zero_lazy(R)) acc = xyzz_dbl_affine(Affine<Cv>{fp_canon(q.x), fp_canon(q.y)});
-    else inf = true;
-    return;
-  }
-  auto PP = fp_mul_lazy(P, P);
-  auto PPP = fp_mul_lazy(P, PP);
-  auto Q = fp_mul_lazy(acc.x, PP);
-  const auto X3 = fp_sub_lazy(fp_sub_lazy(fp_mul_lazy(R, R), PPP), fp_add_lazy(Q, Q));
-  acc.y = fp_mul2_lazy(R, fp_sub_lazy(Q, X3), acc.y, fp_neg_lazy(PPP));  // R (Q - X3) - Y1 PPP
-  acc.x = X3;
-  acc.zz = fp_mul_lazy(acc.zz, PP);
-  acc.zzz = fp_mul_lazy(acc.zzz, PPP);
 }
 
 // P + Q, both XYZZ.  add-2008-s with the exceptional cases.

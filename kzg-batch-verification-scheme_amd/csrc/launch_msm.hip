@@ -36,12 +36,9 @@ void Launch<Cv>::reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, con
                         XY* scratch, XY* winsum) {
   const uint32_t nseg = nsets * (NBUCKETS / SEG);
   k_reduce_segments<Cv><<<grid_for(nseg, 256), 256, 0, st>>>(nseg, cnt, buckets, R, U);
-#ifdef KZ_REDUCE_OLD  // A/B reference: one workgroup per set, three serial segment levels
-  k_reduce_finish<Cv><<<nsets, 256, 0, st>>>(R, U, scratch, winsum);
-#else  // scratch holds nsets * RB_PARTS partial sums (the workspace sizes it nsets * 288)
+  // scratch: nsets * RB_PARTS partial sums
   k_reduce_bits<Cv><<<nsets * RB_PARTS, 256, 0, st>>>(R, U, scratch);
   k_reduce_bits_finish<Cv><<<grid_for(nsets, 64), 64, 0, st>>>(nsets, scratch, winsum);
-#endif
 }
 
 template <class Cv>

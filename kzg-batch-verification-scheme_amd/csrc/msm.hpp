@@ -8,7 +8,7 @@
 //                     sizes do not diverge a wavefront; bucket pieces cut by a chunk
 //                     boundary go to partial slots and are joined by k_fixup.
 //   k_reduce_segments sum_b b*S_b per window: 16-bucket segments (running sums) ...
-//   k_reduce_finish   ... combined per window by one workgroup with LDS tree sums
+//   k_reduce_bits     ... combined per window by bit decomposition of the segment index
 //   k_window_combine  Horner over the 16-bit windows (2^16 * acc + W_w)
 //
 // A "term list" generalises the two MSMs of batch verification (BASELINE.json:5,
@@ -367,11 +367,9 @@ KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_
 
 // Waves per SIMD the accumulation is compiled for (VGPR budget 512 / ACC_WAVES per lane); the
 // host caps the grid at one resident round of CUs x 4 SIMDs x ACC_WAVES waves (api.hip).
-#ifndef KZ_ACC_REGS
-constexpr int ACC_WAVES = 4;  // ZZ/ZZZ staged in LDS (below)
-#else
-constexpr int ACC_WAVES = 3;  // A/B reference: the whole running sum in registers (168 VGPRs)
-#endif
+// ZZ/ZZZ staged in LDS (below) make 4 fit; the all-register loop needed 168 VGPRs (3 waves,
+// 7.53 vs 7.28 ms: profiles/r01/acc_lds_ab.txt).
+constexpr int ACC_WAVES = 4;
 
 template <class Cv>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ACC_WAVES))) k_accumulate(const uint32_t* __restrict__ total_p,
@@ -390,7 +388,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ACC_WA
   if (start >= total) return;
   const uint32_t end = min(start + len, total);
   uint32_t cur = sorted_key[start];
-#ifndef KZ_ACC_REGS
   // ZZ and ZZZ of the running bucket sum live in LDS (word-major per thread: conflict-free
   // 32-bit accesses), X and Y in registers.  ZZ/ZZZ are read only at the start (U2, S2) and the
   // end (ZZ3, ZZZ3) of an addition, so taking them out of the register file keeps the loop
@@ -462,43 +459,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ACC_WA
   acc_flush(Xyzz<Cv>{x, y, ld(zzp), ld(zzzp)}, cur, chunk, start, len, off, cnt, buckets, part_first, part_last, inf);
 #undef zzp
 #undef zzzp
-#elif defined(KZ_ACC_OLD)  // A/B reference: ZZ = 0 test per addition, canonical conditional negation
-  Xyzz<Cv> acc = Xyzz<Cv>::inf();
-  for (uint32_t e = start; e < end; ++e) {
-    uint32_t key = sorted_key[e];
-    if (key != cur) {
-      acc_flush(acc, cur, chunk, start, len, off, cnt, buckets, part_first, part_last);
-      acc = Xyzz<Cv>::inf();
-      cur = key;
-    }
-    uint32_t v = sorted_val[e];
-    Affine<Cv> p = load_affine(pts, v >> 1);
-    p.y = fp_cneg(p.y, (v & 1) != 0);
-    acc = xyzz_add_affine_lazy(acc, p);
-  }
-  acc_flush(acc, cur, chunk, start, len, off, cnt, buckets, part_first, part_last);
-#else
-  Xyzz<Cv> acc = Xyzz<Cv>::inf();
-  bool inf = true;  // acc = O: at every bucket start, and after P + (-P)
-  for (uint32_t e = start; e < end; ++e) {
-    uint32_t key = sorted_key[e];
-    if (key != cur) {
-      acc_flush(acc, cur, chunk, start, len, off, cnt, buckets, part_first, part_last, inf);
-      inf = true;
-      cur = key;
-    }
-    uint32_t v = sorted_val[e];
-#ifdef KZ_EXPERIMENT_LOCAL_PTS  // timing experiment only: gathers hit 1024 cache-resident points
-    v &= 2047u;
-#endif
-    Affine<Cv> p = load_affine(pts, v >> 1);
-    // -y as p - y: y != 0 for every point of odd order (no 2-torsion on either curve), and the
-    // lazy range [0, 2p) holds p - y either way -- no zero test, no canonical negation
-    p.y = fp_select((v & 1) != 0, fp_rsub_mod(p.y), p.y);
-    xyzz_acc_affine_lazy(acc, inf, p);
-  }
-  acc_flush(acc, cur, chunk, start, len, off, cnt, buckets, part_first, part_last, inf);
-#endif
 }
 
 // joins the pieces of buckets that cross chunk boundaries (launched with the same grid as
@@ -563,19 +523,6 @@ KZ_DEV Xyzz<Cv> block_sum256(Xyzz<Cv> v, Xyzz<Cv>* lds) {
   return v;  // valid in thread 0
 }
 
-// sum_{i<16} i*X_i and sum X_i for X_i = src[base + i*stride .. ] (serial, one thread)
-template <class Cv>
-KZ_DEV void weighted16(const Xyzz<Cv>* src, uint32_t count, Xyzz<Cv>& R, Xyzz<Cv>& U) {
-  Xyzz<Cv> run = Xyzz<Cv>::inf(), acc = Xyzz<Cv>::inf();
-  for (int i = (int)count - 1; i >= 1; --i) {
-    run = xyzz_add_c(run, load_xyzz(&src[i]));
-    acc = xyzz_add_c(acc, run);
-  }
-  if (count) run = xyzz_add_c(run, load_xyzz(&src[0]));
-  R = acc;
-  U = run;
-}
-
 template <class Cv>
 KZ_DEV Xyzz<Cv> xyzz_mul_pow2(Xyzz<Cv> p, int k) {
   for (int i = 0; i < k; ++i) p = xyzz_dbl_c(p);
@@ -607,59 +554,8 @@ __device__ __noinline__ Xyzz<Cv> xyzz_mul_pow2_jac(const Xyzz<Cv>& p, int k) {
   return {X, Y, ZZ, fp_mul(ZZ, Z)};
 }
 
-// One 256-thread workgroup per window (set).  Window sum
-//   W = sum_b (b+1) S_b = sum_g (R_g + U_g) + SEG * sum_g g U_g.
-// sum_g g U_g (2048 terms) is itself split into 16-term segments twice (in LDS scratch).
-template <class Cv>
-__global__ void __launch_bounds__(256) k_reduce_finish(const Xyzz<Cv>* __restrict__ R, const Xyzz<Cv>* __restrict__ U,
-                                                       Xyzz<Cv>* __restrict__ scratch, Xyzz<Cv>* __restrict__ winsum) {
-  constexpr uint32_t NSEG = NBUCKETS / SEG;  // 2048
-  __shared__ __attribute__((aligned(16))) Xyzz<Cv> lds[128];
-  const uint32_t set = blockIdx.x;
-  const Xyzz<Cv>* Rs = R + (size_t)set * NSEG;
-  const Xyzz<Cv>* Us = U + (size_t)set * NSEG;
-  Xyzz<Cv>* R2 = scratch + (size_t)set * 2 * (NSEG / SEG + 16);  // 128 + 8
-  Xyzz<Cv>* U2 = R2 + NSEG / SEG + 8;
-  const int t = threadIdx.x;
-  // (1) sum_g (R_g + U_g)
-  Xyzz<Cv> s = Xyzz<Cv>::inf();
-  for (uint32_t g = t; g < NSEG; g += 256) s = xyzz_add_c(xyzz_add_c(s, load_xyzz(&Rs[g])), load_xyzz(&Us[g]));
-  Xyzz<Cv> part1 = block_sum256(s, lds);
-  // (2) level 2: 128 threads, 16 U's each -> R2_j, U2_j
-  if (t < (int)(NSEG / SEG)) {
-    Xyzz<Cv> r, u;
-    weighted16(&Us[t * SEG], SEG, r, u);
-    store_xyzz(&R2[t], r);
-    store_xyzz(&U2[t], u);
-  }
-  __threadfence_block();
-  __syncthreads();
-  // sum_j R2_j (128 items): tree
-  Xyzz<Cv> v = (t < (int)(NSEG / SEG)) ? load_xyzz(&R2[t]) : Xyzz<Cv>::inf();
-  Xyzz<Cv> sumR2 = block_sum256(v, lds);
-  // (3) level 3: 8 threads over U2 (128 items) -> R3_j, U3_j (8 items); then serial
-  __shared__ __attribute__((aligned(16))) Xyzz<Cv> r3[8], u3[8];
-  if (t < 8) {
-    Xyzz<Cv> r, u;
-    weighted16(&U2[t * SEG], SEG, r, u);
-    store_xyzz(&r3[t], r);
-    store_xyzz(&u3[t], u);
-  }
-  __syncthreads();
-  if (t == 0) {
-    Xyzz<Cv> sumR3 = Xyzz<Cv>::inf();
-    for (int j = 0; j < 8; ++j) sumR3 = xyzz_add_c(sumR3, load_xyzz(&r3[j]));
-    Xyzz<Cv> r, u;
-    weighted16(u3, 8, r, u);                      // W3 = sum_j j U3_j
-    Xyzz<Cv> W2 = xyzz_add_c(sumR3, xyzz_mul_pow2(r, 4));   // sum_j j U2_j
-    Xyzz<Cv> V = xyzz_add_c(sumR2, xyzz_mul_pow2(W2, 4));   // sum_g g U_g
-    Xyzz<Cv> W = xyzz_add_c(part1, xyzz_mul_pow2(V, 4));
-    store_xyzz(&winsum[set], W);
-  }
-}
-
-// Latency form of the window sums (replaces k_reduce_finish's three serial segment levels,
-// ~130 dependent point operations on one lane per set, by ~40):
+// Window sums with a short dependency chain (~40 point operations per set; the earlier one
+// workgroup per set with three serial 16-term segment levels needed ~130, 3.8 vs 1.2 ms):
 //   W = sum_g (R_g + U_g) + SEG * sum_g g U_g,   sum_g g U_g = sum_j 2^j B_j,
 //   B_j = sum of the 1024 U_g whose index g has bit j set (j < 11, NSEG = 2^11).
 // k_reduce_bits: RB_PARTS workgroups per set -- 11 compute B_j, 4 compute quarter sums of
@@ -727,11 +623,7 @@ __global__ void k_window_combine(MsmWindows mw, const Xyzz<Cv>* __restrict__ win
   const Xyzz<Cv>* W = winsum + mw.set_base[m];
   Xyzz<Cv> acc = load_xyzz(&W[mw.nwin[m] - 1]);
   for (int w = (int)mw.nwin[m] - 2; w >= 0; --w) {
-#ifdef KZ_COMBINE_OLD  // A/B reference: XYZZ doublings
-    acc = xyzz_mul_pow2(acc, WBITS);
-#else
     acc = xyzz_mul_pow2_jac(acc, WBITS);
-#endif
     acc = xyzz_add_c(acc, load_xyzz(&W[w]));
   }
   store_xyzz(&res[m], acc);
