@@ -68,6 +68,7 @@ struct Slot {
   hipStream_t stream = nullptr;
   DevBuf pts, inf, scal_r, scal_s, scal_t, tpart, cnt, off, coarse, ent, total, sval, skey;
   DevBuf buckets, pfirst, plast, R, U, scratch, winsum, res, flags, stage, outb;
+  DevBuf acc29;                                  // radix-29 bucket records (BLS12-381, msm.hpp)
   DevBuf fs_leaves, fs_tmp, fs_top, pow, chal;  // Fiat-Shamir / powers-of-r randomisers
   DevBuf glv_r, glv_s, glv_t;                    // GLV half scalars (glv.hpp): [h0 x n | h1 x n]
   DevBuf digits;                                 // signed window digit codes of every term (msm.hpp)
@@ -94,10 +95,11 @@ struct kzgmi_ctx {
   bool glv_msm = true;      // enable knobs (kzgmi_set_glv; A/B measurements)
   bool glv_batch = true;
   bool msm_trusted_g1 = false;
-  // accumulation grid cap: one resident round (CUs x 4 SIMDs x 3 waves x 64 lanes at the
-  // kernel's 161 VGPRs) of equal chunks instead of 64-entry chunks in 2-3 partial rounds:
-  // 113 -> 116 batch-verifies/s pipelined (tools/ab_env.sh).  0 = uncapped.
-  size_t acc_threads = 0;
+  // accumulation grid cap: one resident round (CUs x 4 SIMDs x kAccWaves<Cv> waves x 64 lanes)
+  // of equal chunks instead of 64-entry chunks in 2-3 partial rounds: 113 -> 116
+  // batch-verifies/s pipelined when introduced (tools/ab_env.sh).
+  int ncu = 0;                // compute units: the accumulation grid cap (kAccWaves, msm.hpp)
+  size_t acc_threads_env = 0;  // KZGMI_ACC_THREADS override of that cap (0 = none)
   double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
   int phase_calls = 0;
   DevBuf table[2], table_base[2];
@@ -184,6 +186,9 @@ int map_device_err(uint32_t e) {
 template <class Cv>
 int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, size_t emax, const MsmWindows& mw,
                  const Affine<Cv>* pts = nullptr, const uint8_t* inf = nullptr) {
+  // pts == nullptr: the slot's freshly converted points, put into the accumulation's format
+  // here; explicit pts (commit-key rows) are stored in that format already (kzgmi_ck_load)
+  const bool own_pts = pts == nullptr;
   TermList tl = tl_in;  // + each class's offset in the digit array
   size_t ndig = 0;
   for (uint32_t k = 0; k < tl.nclass; ++k) {
@@ -198,7 +203,8 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   const uint32_t NB = nsets * NBUCKETS;
   // accumulation threads: 64-entry chunks, at most acc_threads of them (then equal longer chunks)
   size_t nchunks = (emax + ACC_CHUNK - 1) / ACC_CHUNK + 1;
-  if (c->acc_threads && nchunks > c->acc_threads) nchunks = c->acc_threads;
+  const size_t cap = c->acc_threads_env ? c->acc_threads_env : (size_t)c->ncu * 4 * kAccWaves<Cv> * 64;
+  if (cap && nchunks > cap) nchunks = cap;
   nchunks = (nchunks + 255) / 256 * 256;  // = the launched thread count (part arrays indexed by thread)
   CHK(s.cnt.ensure((size_t)NB * 4));
   CHK(s.off.ensure((size_t)NB * 4));
@@ -210,6 +216,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   CHK(s.buckets.ensure((size_t)NB * sizeof(XY)));
   CHK(s.pfirst.ensure(nchunks * sizeof(XY)));
   CHK(s.plast.ensure(nchunks * sizeof(XY)));
+  if constexpr (kAcc29<Cv>) CHK(s.acc29.ensure(((size_t)NB + 2 * nchunks) * W29 * 4));
   CHK(s.R.ensure((size_t)NB / SEG * sizeof(XY)));
   CHK(s.U.ensure((size_t)NB / SEG * sizeof(XY)));
   CHK(s.scratch.ensure((size_t)nsets * RB_PARTS * sizeof(XY)));  // k_reduce_bits partial sums
@@ -217,13 +224,20 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   CHK(s.res.ensure(2 * sizeof(XY)));
   hipStream_t st = s.stream;
   using L = Launch<Cv>;
+  if (own_pts) {
+    uint32_t npts = 0;
+    for (uint32_t k = 0; k < tl.nclass; ++k)
+      if (tl.c[k].count) npts = std::max(npts, tl.c[k].pt_base + tl.c[k].count);
+    L::pts_to29(st, s.pts.template as<Affine<Cv>>(), npts);
+  }
   L::sort(st, tl, nsets, inf, s.digits.template as<uint32_t>(), s.coarse.template as<uint32_t>(), s.ent.template as<uint64_t>(),
           s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.total.template as<uint32_t>(),
           s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>());
   mark(c, s, PH_SORT + 1);
   L::accumulate(st, nchunks, s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
                 s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts,
-                s.buckets.template as<XY>(), s.pfirst.template as<XY>(), s.plast.template as<XY>());
+                s.buckets.template as<XY>(), s.pfirst.template as<XY>(), s.plast.template as<XY>(),
+                s.acc29.template as<uint32_t>(), NB);
   mark(c, s, PH_ACCUM + 1);
   L::reduce(st, nsets, s.cnt.template as<uint32_t>(), s.buckets.template as<XY>(), s.R.template as<XY>(),
             s.U.template as<XY>(), s.scratch.template as<XY>(), s.winsum.template as<XY>());
@@ -462,8 +476,8 @@ int kzgmi_ctx_create(kzgmi_ctx** out, int device_id, int pipeline_slots) {
   c->device = device_id;
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_id) == hipSuccess && ncu > 0)
-    c->acc_threads = (size_t)ncu * 4 * ACC_WAVES * 64;
-  if (const char* e = getenv("KZGMI_ACC_THREADS")) c->acc_threads = (size_t)strtoull(e, nullptr, 10);
+    c->ncu = ncu;
+  if (const char* e = getenv("KZGMI_ACC_THREADS")) c->acc_threads_env = (size_t)strtoull(e, nullptr, 10);
   c->slots.resize(pipeline_slots);
   for (auto& s : c->slots) {
     if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
@@ -483,7 +497,7 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
   for (auto& s : c->slots) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     DevBuf* bufs[] = {&s.pts, &s.inf, &s.scal_r, &s.scal_s, &s.scal_t, &s.tpart, &s.cnt, &s.off, &s.coarse, &s.ent,
-                      &s.total, &s.sval, &s.skey, &s.buckets, &s.pfirst, &s.plast, &s.R, &s.U, &s.scratch,
+                      &s.total, &s.sval, &s.skey, &s.buckets, &s.pfirst, &s.plast, &s.acc29, &s.R, &s.U, &s.scratch,
                       &s.winsum, &s.res, &s.flags, &s.stage, &s.outb, &s.fs_leaves, &s.fs_tmp,
                       &s.fs_top, &s.pow, &s.chal, &s.glv_r, &s.glv_s, &s.glv_t, &s.digits};
     for (DevBuf* b : bufs) b->release();
@@ -753,6 +767,7 @@ int kzgmi_ck_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1_powers, siz
       for (int w = 1; w < CK_ROWS; ++w)
         L::shift_points(st, pts + (size_t)(w - 1) * n, inf + (size_t)(w - 1) * n, (uint32_t)n, pts + (size_t)w * n,
                         inf + (size_t)w * n);
+      L::pts_to29(st, pts, (uint32_t)(CK_ROWS * n));  // resident in the accumulation's format
       okk = hipGetLastError() == hipSuccess &&
             hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
             hipStreamSynchronize(st) == hipSuccess;

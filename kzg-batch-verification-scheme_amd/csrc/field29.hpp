@@ -1,0 +1,190 @@
+// Radix-2^29 Montgomery arithmetic for the BLS12-381 bucket accumulation (msm.hpp
+// k_accumulate).  14 limbs of 29 bits in 32-bit VGPRs, R29 = 2^406.
+//
+// Why: the accumulation is VALU-issue bound, and in the 32-bit-limb product (field.hpp) every
+// limb product costs TWO issue slots, the v_mad_u64_u32 and the v_addc_co_u32 folding its
+// carry-out (tools/probes/mad_rate.hip: both full rate).  With 29-bit limbs every column of
+// the product -- at most 28 (a b) + 14 (m p) products < 2^58 plus the carry -- fits the 64-bit
+// accumulator, so a limb product is ONE v_mad_u64_u32: 392 mads + ~4 column ops x 27 instead
+// of 288 x 2 + column moves.  Additions and subtractions pay a carry pass instead (sub29:
+// a + B - b with B a multiple of p whose limbs are biased into [2^29, 2^30), so no limb goes
+// negative).  Measured in one harness (tools/probes/radix29/acc29.hip): the mixed addition
+// runs 1.17-1.22x faster than the 32-bit lazy form, and it fits 108 VGPRs without spills.
+//
+// Value bounds (all values are normalised: limbs 0..12 < 2^29): a product of inputs below
+// 2^12 p returns < 2p (R29 > 2^24 p); callers track the bounds of sums and differences and
+// pick the bias B_k with k p >= the subtrahend's bound (msm.hpp documents them per step).
+// Reference: none (LICENSE only); checked bit-exactly against the C oracle through the MSM and
+// batch parity tests, which all run through this path on BLS12-381.
+#pragma once
+#include "field.hpp"
+#include "params29_gen.hpp"
+
+namespace kzgmi {
+
+constexpr uint32_t M29 = (1u << 29) - 1;
+
+template <class Q>
+struct F29 {
+  static constexpr int N = Q::N;
+  uint32_t v[N];
+  KZ_DEV static F29 zero() { F29 r; _Pragma("unroll") for (int i = 0; i < N; ++i) r.v[i] = 0; return r; }
+  KZ_DEV static F29 from_const(const uint32_t (&c)[N]) {
+    F29 r;
+    _Pragma("unroll") for (int i = 0; i < N; ++i) r.v[i] = c[i];
+    return r;
+  }
+};
+
+KZ_DEV void mad29(uint64_t& acc, uint32_t a, uint32_t b) {
+  uint64_t cc;  // carry-out unused: column sums stay below 2^64
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
+}
+KZ_DEV void mad29s(uint64_t& acc, uint32_t a, uint32_t b_uniform) {
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "s"(b_uniform));
+}
+
+// (a b [+ c d] + m p) / R29 -- product scanning, one 64-bit accumulator per column
+template <class Q, bool TWO>
+KZ_DEV F29<Q> mont29(const F29<Q>& a, const F29<Q>& b, const F29<Q>& c, const F29<Q>& d) {
+  constexpr int N = Q::N;
+  uint32_t m[N];
+  F29<Q> t;
+  uint64_t acc = 0;
+  _Pragma("unroll") for (int k = 0; k < N; ++k) {
+    _Pragma("unroll") for (int i = 0; i < k; ++i) {
+      mad29(acc, a.v[i], b.v[k - i]);
+      if constexpr (TWO) mad29(acc, c.v[i], d.v[k - i]);
+      mad29s(acc, m[i], Q::MOD[k - i]);
+    }
+    mad29(acc, a.v[k], b.v[0]);
+    if constexpr (TWO) mad29(acc, c.v[k], d.v[0]);
+    m[k] = ((uint32_t)acc * Q::INV) & M29;
+    mad29s(acc, m[k], Q::MOD[0]);  // low 29 bits become 0
+    acc >>= 29;
+  }
+  _Pragma("unroll") for (int k = N; k < 2 * N - 1; ++k) {
+    _Pragma("unroll") for (int i = k - N + 1; i < N; ++i) {
+      mad29(acc, a.v[i], b.v[k - i]);
+      if constexpr (TWO) mad29(acc, c.v[i], d.v[k - i]);
+      mad29s(acc, m[i], Q::MOD[k - i]);
+    }
+    t.v[k - N] = (uint32_t)acc & M29;
+    acc >>= 29;
+  }
+  t.v[N - 1] = (uint32_t)acc;
+  return t;
+}
+template <class Q>
+KZ_DEV F29<Q> mul29(const F29<Q>& a, const F29<Q>& b) { return mont29<Q, false>(a, b, a, b); }
+template <class Q>
+KZ_DEV F29<Q> mul2_29(const F29<Q>& a, const F29<Q>& b, const F29<Q>& c, const F29<Q>& d) {
+  return mont29<Q, true>(a, b, c, d);
+}
+
+// a + B - b, normalised (B: biased k p, k p >= b)
+template <class Q>
+KZ_DEV F29<Q> sub29(const F29<Q>& a, const F29<Q>& b, const uint32_t (&B)[Q::N]) {
+  F29<Q> r;
+  uint32_t c = 0;
+  _Pragma("unroll") for (int i = 0; i < Q::N; ++i) {
+    const uint32_t x = a.v[i] + B[i] + c - b.v[i];
+    if (i < Q::N - 1) {
+      r.v[i] = x & M29;
+      c = x >> 29;
+    } else {
+      r.v[i] = x;
+    }
+  }
+  return r;
+}
+
+// a + b + e, normalised
+template <class Q>
+KZ_DEV F29<Q> add3_29(const F29<Q>& a, const F29<Q>& b, const F29<Q>& e) {
+  F29<Q> r;
+  uint32_t c = 0;
+  _Pragma("unroll") for (int i = 0; i < Q::N; ++i) {
+    const uint32_t x = a.v[i] + b.v[i] + e.v[i] + c;
+    if (i < Q::N - 1) {
+      r.v[i] = x & M29;
+      c = x >> 29;
+    } else {
+      r.v[i] = x;
+    }
+  }
+  return r;
+}
+
+// a == 0 mod p for a < NKP p.  a = k p forces k = low limb x p^-1 mod 2^29 (p is odd), so one
+// multiply filters; only k < NKP is compared limb by limb (no table of multiples stays live in
+// registers across the accumulation loop)
+template <class Q>
+KZ_DEV bool is_zero29(const F29<Q>& a) {
+  bool hit = false;
+  _Pragma("unroll") for (int k = 0; k < Q::NKP; ++k) hit |= a.v[0] == Q::KP_LO[k];
+  if (!hit) return false;
+  for (int k = 0; k < Q::NKP; ++k) {
+    uint32_t d = 0;
+    for (int i = 0; i < Q::N; ++i) d |= a.v[i] ^ Q::KP[k][i];
+    if (d == 0) return true;
+  }
+  return false;
+}
+
+// a < 2p -> a mod p
+template <class Q>
+KZ_DEV F29<Q> canon29(const F29<Q>& a) {
+  F29<Q> d;
+  int32_t c = 0;
+  _Pragma("unroll") for (int i = 0; i < Q::N; ++i) {
+    const int32_t x = (int32_t)a.v[i] - (int32_t)Q::MOD[i] + c;
+    if (i < Q::N - 1) {
+      d.v[i] = (uint32_t)x & M29;
+      c = x >> 29;
+    } else {
+      d.v[i] = (uint32_t)x;
+    }
+  }
+  const bool neg = (int32_t)d.v[Q::N - 1] < 0;
+  F29<Q> r;
+  _Pragma("unroll") for (int i = 0; i < Q::N; ++i) r.v[i] = neg ? a.v[i] : d.v[i];
+  return r;
+}
+
+// 32-bit words (value < 2^(32 NW)) <-> 29-bit limbs of the same integer
+template <class Q, int NW>
+KZ_DEV F29<Q> limbs29(const uint32_t (&w)[NW]) {
+  F29<Q> r;
+  _Pragma("unroll") for (int i = 0; i < Q::N; ++i) {
+    const int bit = 29 * i, wi = bit >> 5, sh = bit & 31;
+    const uint64_t lo = (wi < NW ? (uint64_t)w[wi] : 0) | (wi + 1 < NW ? (uint64_t)w[wi + 1] << 32 : 0);
+    r.v[i] = (uint32_t)(lo >> sh) & (i < Q::N - 1 ? M29 : 0xffffffffu);
+  }
+  return r;
+}
+template <class Q, int NW>
+KZ_DEV void words32(const F29<Q>& a, uint32_t (&w)[NW]) {  // a normalised, < 2^(32 NW)
+  _Pragma("unroll") for (int j = 0; j < NW; ++j) {
+    const int bit = 32 * j, li = bit / 29, sh = bit % 29;
+    uint64_t x = (uint64_t)a.v[li] >> sh;
+    if (li + 1 < Q::N) x |= (uint64_t)a.v[li + 1] << (29 - sh);
+    if (li + 2 < Q::N && 58 - sh < 32) x |= (uint64_t)a.v[li + 2] << (58 - sh);
+    w[j] = (uint32_t)x;
+  }
+}
+
+// 32-bit Montgomery (x 2^384, canonical) -> radix-29 Montgomery (x R29), and back (canonical)
+template <class Q, class P>
+KZ_DEV F29<Q> fp_to29(const Fp<P>& a) {
+  return mul29(limbs29<Q>(a.v), F29<Q>::from_const(Q::TO29));
+}
+template <class Q, class P>
+KZ_DEV Fp<P> fp_from29(const F29<Q>& a) {  // a < 2^12 p
+  Fp<P> r;
+  words32<Q>(canon29(mul29(a, F29<Q>::from_const(Q::TO32))), r.v);
+  return r;
+}
+
+}  // namespace kzgmi

@@ -16,9 +16,12 @@ struct Launch {
   static void sort(hipStream_t st, const TermList& tl, uint32_t nsets, const uint8_t* inf, uint32_t* digits,
                    uint32_t* coarse, uint64_t* ent, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
                    uint32_t* skey);
+  // BLS12-381 accumulates in radix 2^29: pts converted by pts_to29 first, acc29 = (nb + 2 x
+  // launched threads) records of W29 words; BN254 ignores acc29
   static void accumulate(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* sval,
                          const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts, XY* buckets,
-                         XY* pfirst, XY* plast);
+                         XY* pfirst, XY* plast, uint32_t* acc29, uint32_t nb);
+  static void pts_to29(hipStream_t st, AF* pts, uint32_t n);  // in place; no-op for BN254
   static void reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const XY* buckets, XY* R, XY* U,
                      XY* scratch, XY* winsum);
   static void window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res);

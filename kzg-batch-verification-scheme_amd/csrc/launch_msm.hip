@@ -23,12 +23,23 @@ void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const 
 template <class Cv>
 void Launch<Cv>::accumulate(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* sval,
                             const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts, XY* buckets,
-                            XY* pfirst, XY* plast) {
+                            XY* pfirst, XY* plast, uint32_t* acc29, uint32_t nb) {
   // nchunks threads (rounded up to whole 256-thread blocks); both kernels derive the chunk
   // length from the same grid
   const unsigned blocks = grid_for(nchunks, 256);
-  k_accumulate<Cv><<<blocks, 256, 0, st>>>(total, sval, skey, off, cnt, pts, buckets, pfirst, plast);
+  k_accumulate<Cv><<<blocks, 256, 0, st>>>(total, sval, skey, off, cnt, pts, buckets, pfirst, plast, acc29, nb);
+  if constexpr (kAcc29<Cv>) {  // radix-29 records -> 32-bit XYZZ buckets and pieces
+    const uint32_t nthreads = blocks * 256u;
+    k_from29<Cv><<<grid_for(nb + 2 * nthreads, 256), 256, 0, st>>>(acc29, nb, nthreads, cnt, buckets, pfirst, plast);
+  }
   k_fixup<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, pfirst, plast, buckets);
+}
+
+template <class Cv>
+void Launch<Cv>::pts_to29(hipStream_t st, AF* pts, uint32_t n) {
+  if constexpr (kAcc29<Cv>) {
+    if (n) k_pts_to29<Cv><<<grid_for(n, 256), 256, 0, st>>>(pts, n);
+  }
 }
 
 template <class Cv>
@@ -50,7 +61,9 @@ template void Launch<KZ_CURVE_T>::sort(hipStream_t, const TermList&, uint32_t, c
                                        uint64_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*);
 template void Launch<KZ_CURVE_T>::accumulate(hipStream_t, size_t, const uint32_t*, const uint32_t*, const uint32_t*,
                                              const uint32_t*, const uint32_t*, const Affine<KZ_CURVE_T>*,
-                                             Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*);
+                                             Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, uint32_t*,
+                                             uint32_t);
+template void Launch<KZ_CURVE_T>::pts_to29(hipStream_t, Affine<KZ_CURVE_T>*, uint32_t);
 template void Launch<KZ_CURVE_T>::reduce(hipStream_t, uint32_t, const uint32_t*, const Xyzz<KZ_CURVE_T>*,
                                          Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*);
 template void Launch<KZ_CURVE_T>::window_combine(hipStream_t, const MsmWindows&, const Xyzz<KZ_CURVE_T>*,

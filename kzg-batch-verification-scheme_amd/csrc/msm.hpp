@@ -17,6 +17,7 @@
 // Reference: none (LICENSE only); parity vs the C oracle in tests/test_gpu_parity.py.
 #pragma once
 #include "common.hpp"
+#include "field29.hpp"
 
 namespace kzgmi {
 
@@ -365,14 +366,196 @@ KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_
   store_xyzz(dst, inf ? Xyzz<Cv>::inf() : xyzz_canon(acc));
 }
 
-// Waves per SIMD the accumulation is compiled for (VGPR budget 512 / ACC_WAVES per lane); the
-// host caps the grid at one resident round of CUs x 4 SIMDs x ACC_WAVES waves (api.hip).
-// ZZ/ZZZ staged in LDS (below) make 4 fit; the all-register loop needed 168 VGPRs (3 waves,
-// 7.53 vs 7.28 ms: profiles/r01/acc_lds_ab.txt).
-constexpr int ACC_WAVES = 4;
+// ---- radix-2^29 accumulation (BLS12-381; field29.hpp) ------------------------------------
+// Points arrive converted in place by k_pts_to29 (x in words 0..13, y in 14..27 of each 128-B
+// slot).  Finished bucket pieces are written as radix-29 records of W29 words (x, y, zz, zzz;
+// zz = 0 marks infinity) to `acc29` = [nb bucket records | nthreads first pieces | nthreads
+// last pieces]; k_from29 converts them to the 32-bit XYZZ arrays that k_fixup and the
+// reduction read.  Converting at each flush instead (4 products) would run on most
+// iterations of a wavefront, since some lane changes bucket in almost every step.
+#ifndef KZ_NO_ACC29
+template <class Cv>
+constexpr bool kAcc29 = Cv::FpP::N == 12;
+#else  // A/B reference: the 32-bit-limb loop for both curves
+template <class Cv>
+constexpr bool kAcc29 = false;
+#endif
+constexpr int W29 = 4 * Bls12_381Fp29::N;  // 56 words, 224 B
 
 template <class Cv>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ACC_WAVES))) k_accumulate(const uint32_t* __restrict__ total_p,
+__global__ void __launch_bounds__(256) k_pts_to29(Affine<Cv>* __restrict__ pts, uint32_t n) {
+  using Q = Bls12_381Fp29;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Affine<Cv> a = pts[i];
+  const F29<Q> x = fp_to29<Q>(a.x), y = fp_to29<Q>(a.y);
+  uint32_t w[2 * Q::N];
+#pragma unroll
+  for (int k = 0; k < Q::N; ++k) { w[k] = x.v[k]; w[Q::N + k] = y.v[k]; }
+  uint4* d = reinterpret_cast<uint4*>(pts + i);
+#pragma unroll
+  for (int k = 0; k < Q::N / 2; ++k) d[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+}
+
+template <class Cv>
+__global__ void __launch_bounds__(256) k_from29(const uint32_t* __restrict__ acc29, uint32_t nb, uint32_t nthreads,
+                                                const uint32_t* __restrict__ cnt, Xyzz<Cv>* __restrict__ buckets,
+                                                Xyzz<Cv>* __restrict__ part_first, Xyzz<Cv>* __restrict__ part_last) {
+  using Q = Bls12_381Fp29;
+  using P = typename Cv::FpP;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nb + 2 * nthreads) return;
+  if (r < nb && cnt[r] == 0) return;  // never written, never read
+  const uint4* s4 = reinterpret_cast<const uint4*>(acc29 + (size_t)r * W29);
+  uint32_t w[W29];
+#pragma unroll
+  for (int k = 0; k < W29 / 4; ++k) {
+    const uint4 q = s4[k];
+    w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w;
+  }
+  F29<Q> c[4];
+  uint32_t zz_or = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < Q::N; ++k) c[j].v[k] = w[j * Q::N + k];
+#pragma unroll
+  for (int k = 0; k < Q::N; ++k) zz_or |= c[2].v[k];
+  Xyzz<Cv> o = Xyzz<Cv>::inf();
+  if (zz_or) o = {fp_from29<Q, P>(c[0]), fp_from29<Q, P>(c[1]), fp_from29<Q, P>(c[2]), fp_from29<Q, P>(c[3])};
+  Xyzz<Cv>* dst = r < nb ? &buckets[r] : r < nb + nthreads ? &part_first[r - nb] : &part_last[r - nb - nthreads];
+  store_xyzz(dst, o);
+}
+
+// 2Q for an affine Q (rare path: the running sum equals the incoming point), bounds: qx < p,
+// qy < 8p in; x < 10p, y < 10p, zz, zzz < 2p out
+template <class Q>
+struct Xyzz29 {
+  F29<Q> x, y, zz, zzz;
+};
+// out of line: its temporaries would otherwise raise the loop's register peak
+template <class Q>
+__device__ __noinline__ Xyzz29<Q> dbl_affine29(const F29<Q> qx, const F29<Q> qy) {
+  using G = F29<Q>;
+  G x, y, zz, zzz;
+  const G U = add3_29(qy, qy, G::zero());                             // < 16p
+  const G V = mul29(U, U);
+  const G W = mul29(U, V);
+  const G S = mul29(qx, V);
+  const G X2 = mul29(qx, qx);
+  const G M = add3_29(X2, X2, X2);                                    // < 6p
+  x = sub29(mul29(M, M), add3_29(S, S, G::zero()), Q::B8);           // < 10p
+  y = sub29(mul29(M, sub29(S, x, Q::B16)), mul29(W, qy), Q::B8);      // < 10p
+  zz = V;
+  zzz = W;
+  return {x, y, zz, zzz};
+}
+
+// The mixed-addition loop.  Bounds (values, all normalised): q.x < p, q.y < 8p; x < 10p;
+// y < 16p; zz, zzz < 2p; products < 2p.  Only two biased multiples of p (8p, 16p) are used, so
+// few constants stay live across the loop.  ZZ/ZZZ in LDS as in the 32-bit loop below.
+template <class Cv>
+KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t len, uint32_t chunk, uint32_t cur,
+                       const uint32_t* __restrict__ sorted_val, const uint32_t* __restrict__ sorted_key,
+                       const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
+                       const uint32_t* __restrict__ pts29, uint32_t* __restrict__ acc29, uint32_t nb) {
+  using Q = Bls12_381Fp29;
+  using G = F29<Q>;
+  constexpr int N = Q::N;
+  __shared__ uint32_t s_zz[N][256], s_zzz[N][256];
+  const uint32_t tx = threadIdx.x;
+  const uint32_t nthreads = gridDim.x * blockDim.x;
+  auto ld = [tx](uint32_t (&a)[N][256]) {
+    asm volatile("" ::: "memory");
+    G r;
+    _Pragma("unroll") for (int k = 0; k < N; ++k) r.v[k] = a[k][tx];
+    return r;
+  };
+  auto st = [tx](uint32_t (&a)[N][256], const G& v) {
+    _Pragma("unroll") for (int k = 0; k < N; ++k) a[k][tx] = v.v[k];
+    asm volatile("" ::: "memory");
+  };
+  // one coordinate at a time (8-B stores: a coordinate is 14 words), zz = 0 marks infinity
+  auto put = [](uint32_t* d, const G& a) {
+    _Pragma("unroll") for (int k = 0; k < N / 2; ++k) reinterpret_cast<uint2*>(d)[k] = make_uint2(a.v[2 * k], a.v[2 * k + 1]);
+  };
+  auto flush = [&](const G& x, const G& y, uint32_t key, bool inf) {
+    const uint32_t o = off[key];
+    const bool started_before = o < start;
+    const bool ends_after = o + cnt[key] > start + len;
+    const size_t rec = started_before ? (size_t)nb + chunk : ends_after ? (size_t)nb + nthreads + chunk : key;
+    uint32_t* d = acc29 + rec * W29;
+    put(d, x);
+    put(d + N, y);
+    put(d + 2 * N, inf ? G::zero() : ld(s_zz));
+    put(d + 3 * N, ld(s_zzz));
+  };
+  G x = G::zero(), y = G::zero();
+  bool inf = true;  // running sum = O: at every bucket start, and after P + (-P)
+  for (uint32_t e = start; e < end; ++e) {
+    const uint32_t key = sorted_key[e];
+    if (key != cur) {
+      flush(x, y, cur, inf);
+      inf = true;
+      cur = key;
+    }
+    const uint32_t v = sorted_val[e];
+    const uint4* s4 = reinterpret_cast<const uint4*>(pts29 + (size_t)(v >> 1) * (sizeof(Affine<Cv>) / 4));
+    uint32_t w[2 * N];
+    _Pragma("unroll") for (int k = 0; k < N / 2; ++k) {
+      const uint4 q = s4[k];
+      w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w;
+    }
+    G qx, qy;
+    _Pragma("unroll") for (int k = 0; k < N; ++k) { qx.v[k] = w[k]; qy.v[k] = w[N + k]; }
+    if (v & 1) qy = sub29(G::zero(), qy, Q::B8);  // -y as 8p - y
+    if (inf) {
+      x = qx;
+      y = qy;
+      st(s_zz, G::from_const(Q::ONE));
+      st(s_zzz, G::from_const(Q::ONE));
+      inf = false;
+      continue;
+    }
+    const G U2 = mul29(qx, ld(s_zz));
+    const G S2 = mul29(qy, ld(s_zzz));
+    const G P = sub29(U2, x, Q::B16);  // < 18p
+    const G R = sub29(S2, y, Q::B16);  // < 18p
+    if (is_zero29(P)) {
+      if (is_zero29(R)) {
+        const Xyzz29<Q> d = dbl_affine29<Q>(qx, qy);
+        x = d.x;
+        y = d.y;
+        st(s_zz, d.zz);
+        st(s_zzz, d.zzz);
+      } else {
+        inf = true;
+      }
+      continue;
+    }
+    const G PP = mul29(P, P);
+    const G PPP = mul29(P, PP);
+    st(s_zz, mul29(ld(s_zz), PP));
+    st(s_zzz, mul29(ld(s_zzz), PPP));
+    const G Q2 = mul29(x, PP);
+    const G X3 = sub29(mul29(R, R), add3_29(PPP, Q2, Q2), Q::B8);  // < 10p
+    y = mul2_29(R, sub29(Q2, X3, Q::B16), y, sub29(G::zero(), PPP, Q::B8));  // R (Q - X3) - Y1 PPP
+    x = X3;
+  }
+  flush(x, y, cur, inf);
+}
+
+// Waves per SIMD the accumulation is compiled for (VGPR budget 512 / waves per lane); the host
+// caps the grid at one resident round of CUs x 4 SIMDs x kAccWaves waves (api.hip).
+// 32-bit limbs (BN254): ZZ/ZZZ staged in LDS make 4 waves fit (128 VGPRs; the all-register
+// loop needed 168: 7.53 vs 7.28 ms, profiles/r01/acc_lds_ab.txt).  Radix 2^29 (BLS12-381):
+// 3 waves, 167 VGPRs and no spills -- forced to 128 the compiler spills ~48 VGPRs inside the
+// products (profiles/r01/acc29_ab.txt).
+template <class Cv>
+constexpr int kAccWaves = kAcc29<Cv> ? 3 : 4;
+
+template <class Cv>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWaves<Cv>))) k_accumulate(const uint32_t* __restrict__ total_p,
                                                     const uint32_t* __restrict__ sorted_val,
                                                     const uint32_t* __restrict__ sorted_key,
                                                     const uint32_t* __restrict__ off,
@@ -380,7 +563,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ACC_WA
                                                     const Affine<Cv>* __restrict__ pts,
                                                     Xyzz<Cv>* __restrict__ buckets,
                                                     Xyzz<Cv>* __restrict__ part_first,
-                                                    Xyzz<Cv>* __restrict__ part_last) {
+                                                    Xyzz<Cv>* __restrict__ part_last,
+                                                    uint32_t* __restrict__ acc29, uint32_t nb) {
   const uint32_t total = *total_p;
   const uint32_t len = acc_chunk_len(total, gridDim.x * blockDim.x);
   const uint32_t chunk = blockIdx.x * blockDim.x + threadIdx.x;
@@ -388,6 +572,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ACC_WA
   if (start >= total) return;
   const uint32_t end = min(start + len, total);
   uint32_t cur = sorted_key[start];
+  if constexpr (kAcc29<Cv>) {
+    acc_loop29<Cv>(start, end, len, chunk, cur, sorted_val, sorted_key, off, cnt,
+                   reinterpret_cast<const uint32_t*>(pts), acc29, nb);
+  } else {  // BN254: 32-bit limbs (8 x 32 bits; radix 2^29 would need 9 limbs)
   // ZZ and ZZZ of the running bucket sum live in LDS (word-major per thread: conflict-free
   // 32-bit accesses), X and Y in registers.  ZZ/ZZZ are read only at the start (U2, S2) and the
   // end (ZZ3, ZZZ3) of an addition, so taking them out of the register file keeps the loop
@@ -459,6 +647,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ACC_WA
   acc_flush(Xyzz<Cv>{x, y, ld(zzp), ld(zzzp)}, cur, chunk, start, len, off, cnt, buckets, part_first, part_last, inf);
 #undef zzp
 #undef zzzp
+  }
 }
 
 // joins the pieces of buckets that cross chunk boundaries (launched with the same grid as
