@@ -492,13 +492,8 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t len, uint32_t chun
   };
   G x = G::zero(), y = G::zero();
   bool inf = true;  // running sum = O: at every bucket start, and after P + (-P)
-  for (uint32_t e = start; e < end; ++e) {
-    const uint32_t key = sorted_key[e];
-    if (key != cur) {
-      flush(x, y, cur, inf);
-      inf = true;
-      cur = key;
-    }
+  // loads entry e's point (sign applied: -y as 8p - y)
+  auto load_q = [&](uint32_t e, G& qx, G& qy) {
     const uint32_t v = sorted_val[e];
     const uint4* s4 = reinterpret_cast<const uint4*>(pts29 + (size_t)(v >> 1) * (sizeof(Affine<Cv>) / 4));
     uint32_t w[2 * N];
@@ -506,41 +501,62 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t len, uint32_t chun
       const uint4 q = s4[k];
       w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w;
     }
-    G qx, qy;
     _Pragma("unroll") for (int k = 0; k < N; ++k) { qx.v[k] = w[k]; qy.v[k] = w[N + k]; }
-    if (v & 1) qy = sub29(G::zero(), qy, Q::B8);  // -y as 8p - y
-    if (inf) {
-      x = qx;
-      y = qy;
-      st(s_zz, G::from_const(Q::ONE));
-      st(s_zzz, G::from_const(Q::ONE));
-      inf = false;
-      continue;
-    }
-    const G U2 = mul29(qx, ld(s_zz));
-    const G S2 = mul29(qy, ld(s_zzz));
-    const G P = sub29(U2, x, Q::B16);  // < 18p
-    const G R = sub29(S2, y, Q::B16);  // < 18p
-    if (is_zero29(P)) {
-      if (is_zero29(R)) {
-        const Xyzz29<Q> d = dbl_affine29<Q>(qx, qy);
-        x = d.x;
-        y = d.y;
-        st(s_zz, d.zz);
-        st(s_zzz, d.zzz);
-      } else {
+    if (v & 1) qy = sub29(G::zero(), qy, Q::B8);
+  };
+  // The rare doubling (running sum == incoming point) leaves the hot loop: a call or the
+  // doubling's temporaries inside it would raise the loop's register peak (a call there cost
+  // ~48 spilled VGPRs at 4 waves); the outer loop does it and resumes at the next entry.
+  uint32_t e = start;
+  for (;;) {
+    bool dbl = false;
+    for (; e < end; ++e) {
+      const uint32_t key = sorted_key[e];
+      if (key != cur) {
+        flush(x, y, cur, inf);
         inf = true;
+        cur = key;
       }
-      continue;
+      G qx, qy;
+      load_q(e, qx, qy);
+      if (inf) {
+        x = qx;
+        y = qy;
+        st(s_zz, G::from_const(Q::ONE));
+        st(s_zzz, G::from_const(Q::ONE));
+        inf = false;
+        continue;
+      }
+      const G U2 = mul29(qx, ld(s_zz));
+      const G S2 = mul29(qy, ld(s_zzz));
+      const G P = sub29(U2, x, Q::B16);  // < 18p
+      const G R = sub29(S2, y, Q::B16);  // < 18p
+      if (is_zero29(P)) {
+        if (is_zero29(R)) {
+          dbl = true;
+          break;
+        }
+        inf = true;
+        continue;
+      }
+      const G PP = mul29(P, P);
+      const G PPP = mul29(P, PP);
+      st(s_zz, mul29(ld(s_zz), PP));
+      st(s_zzz, mul29(ld(s_zzz), PPP));
+      const G Q2 = mul29(x, PP);
+      const G X3 = sub29(mul29(R, R), add3_29(PPP, Q2, Q2), Q::B8);  // < 10p
+      y = mul2_29(R, sub29(Q2, X3, Q::B16), y, sub29(G::zero(), PPP, Q::B8));  // R (Q - X3) - Y1 PPP
+      x = X3;
     }
-    const G PP = mul29(P, P);
-    const G PPP = mul29(P, PP);
-    st(s_zz, mul29(ld(s_zz), PP));
-    st(s_zzz, mul29(ld(s_zzz), PPP));
-    const G Q2 = mul29(x, PP);
-    const G X3 = sub29(mul29(R, R), add3_29(PPP, Q2, Q2), Q::B8);  // < 10p
-    y = mul2_29(R, sub29(Q2, X3, Q::B16), y, sub29(G::zero(), PPP, Q::B8));  // R (Q - X3) - Y1 PPP
-    x = X3;
+    if (!dbl) break;
+    G qx, qy;  // entry e: running sum := 2 q
+    load_q(e, qx, qy);
+    const Xyzz29<Q> d = dbl_affine29<Q>(qx, qy);
+    x = d.x;
+    y = d.y;
+    st(s_zz, d.zz);
+    st(s_zzz, d.zzz);
+    ++e;
   }
   flush(x, y, cur, inf);
 }
@@ -549,10 +565,13 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t len, uint32_t chun
 // caps the grid at one resident round of CUs x 4 SIMDs x kAccWaves waves (api.hip).
 // 32-bit limbs (BN254): ZZ/ZZZ staged in LDS make 4 waves fit (128 VGPRs; the all-register
 // loop needed 168: 7.53 vs 7.28 ms, profiles/r01/acc_lds_ab.txt).  Radix 2^29 (BLS12-381):
-// 3 waves, 167 VGPRs and no spills -- forced to 128 the compiler spills ~48 VGPRs inside the
-// products (profiles/r01/acc29_ab.txt).
+// 4 waves at 128 VGPRs once the rare doubling left the hot loop (7 VGPRs spilled outside it);
+// 3 waves / 167 VGPRs measured 6.94 vs 6.63 ms (profiles/r01/acc29_ab.txt).
+#ifndef KZ_ACC29_WAVES
+#define KZ_ACC29_WAVES 4
+#endif
 template <class Cv>
-constexpr int kAccWaves = kAcc29<Cv> ? 3 : 4;
+constexpr int kAccWaves = kAcc29<Cv> ? KZ_ACC29_WAVES : 4;
 
 template <class Cv>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWaves<Cv>))) k_accumulate(const uint32_t* __restrict__ total_p,
