@@ -32,8 +32,10 @@ def avg_ns(prefix):
 
 acc = avg_ns("void kzgmi::k_accumulate<kzgmi::Bls12_381>")
 fix = avg_ns("void kzgmi::k_fixup<kzgmi::Bls12_381>")
+f29 = avg_ns("void kzgmi::k_from29<kzgmi::Bls12_381>")  # radix-29 records -> 32-bit buckets
 out = {"command": "rocprofv3 --kernel-trace --stats -- python3 tools/phase_timing.py --reps 4 (n = 2^20)",
-       "k_accumulate_avg_ms": acc / 1e6, "k_fixup_avg_ms": fix / 1e6, "accumulate_phase_avg_ms": (acc + fix) / 1e6}
+       "k_accumulate_avg_ms": acc / 1e6, "k_from29_avg_ms": f29 / 1e6, "k_fixup_avg_ms": fix / 1e6,
+       "accumulate_phase_avg_ms": (acc + f29 + fix) / 1e6}
 json.dump(out, open(os.path.join(dst, "kernel_single.json"), "w"), indent=1)
 print(json.dumps(out))
 
@@ -71,9 +73,10 @@ if fetch and write:
                       "two 128-B lines a gathered point can touch.  Infinity-Cache hits are counted, so this is "
                       "L2-miss traffic, an upper bound on HBM bytes",
         "algorithmic_bytes_per_launch": 256 * n,
-        "gather_model_bytes_per_launch": entries * (96 + 8),
-        "gather_model": "every window term gathers its 96-B affine point and reads its 8-B sorted entry "
-                        "(32 terms per tuple): the traffic Pippenger accumulation touches by construction",
+        "gather_model_bytes_per_launch": entries * (112 + 8),
+        "gather_model": "every window term gathers its 112-B radix-2^29 affine point (x, y: 2 x 14 words "
+                        "of a 128-B slot) and reads its 8-B sorted entry (32 terms per tuple): the traffic "
+                        "Pippenger accumulation touches by construction",
         "tcc_hit_rate": (sum(hit) / (sum(hit) + sum(miss))) if hit and miss else None,
         "k_accumulate_avg_ms": acc / 1e6,
     }
