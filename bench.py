@@ -538,7 +538,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32-limb Montgomery Fp (%d-bit modular integer)" % (381 if curve == "bls12_381" else 254),
+        "dtype": ("Montgomery Fp, 381-bit modular integer (u32 limbs; radix-2^29 limbs in the bucket accumulation)"
+                  if curve == "bls12_381" else "Montgomery Fp, 254-bit modular integer (u32 limbs)"),
         "data": "synthetic: valid toy-tau KZG openings generated on the GPU (kzgmi_gen_tuples), HBM-resident",
         "config": {
             "workload": "batch_verify (configs[2]): n=%d %s tuples per GPU, two G1 MSMs + 2-pairing check" % (n, curve),
