@@ -94,3 +94,30 @@ def test_sharded_msm_cfg4_shape(ctx):
     ctx.msm_partial(curve, Cm[h * g1b:], z[h * 32:], h, parts[pb:])
     got = ctx.msm_combine(curve, parts, 2)
     assert got == O.msm_g1(curve, _host(Cm), _host(z), n)
+
+
+@pytest.mark.parametrize("curve,n,trusted", [("bls12_381", 300007, False), ("bls12_381", 262143, True),
+                                             ("bn254", 524289, False)])
+def test_ragged_batch_vs_oracle(ctx, curve, n, trusted):
+    """Non-power-of-two batches: the accumulation's per-thread runs, the last partial round and
+    the bucket pieces joined by k_fixup do not divide evenly.  A, B and the verdict bit-exact vs
+    the oracle (with and without the GLV split that trusted_g1 enables), then one corrupted
+    proof flips the verdict."""
+    C = pc.CURVES[curve]
+    tau = 0xBADC0DE + n
+    Cm, z, y, P = _gen_batch(ctx, curve, n, tau, hashlib.sha256(b"ragged%d" % n).digest())
+    g2 = pk.g2_to_bytes(C.g2, C)
+    tg2 = O.g2_mul(curve, g2, tau)
+    srs = ctx.load_srs(curve, g2, tg2)
+    vseed = hashlib.sha256(b"ragged-verify%d" % n).digest()
+    assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n, trusted_g1=trusted) is True
+    A, B = ctx.last_combination(curve)
+    hb = [_host(t) for t in (Cm, z, y, P)]
+    ok, Ao, Bo = O.batch_verify(curve, hb[0], hb[1], hb[2], hb[3], n, g2, tg2, vseed, want_ab=True)
+    assert ok is True and A == Ao and B == Bo
+    # swap two proofs (both stay valid curve points): the check must fail
+    g1b = 2 * C.fp_bytes
+    P2 = P.clone()
+    P2[:g1b] = P[(n - 1) * g1b:]
+    P2[(n - 1) * g1b:] = P[:g1b]
+    assert ctx.batch_verify(srs, Cm, z, y, P2, seed=vseed, n=n, trusted_g1=trusted) is False
