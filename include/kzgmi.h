@@ -20,6 +20,13 @@
  *   - Return value 0 = OK, negative = error (see KZGMI_ERR_*).  Invalid input is an error,
  *     never "ok = 0".  kzgmi_last_error() gives a thread-local message.
  *   - Threading: one ctx per host thread; calls on one ctx are serialised by the caller.
+ *   - Device-memory ordering: the library runs on its own non-blocking HIP streams (one per
+ *     pipeline slot).  A caller that produced device inputs on another stream (e.g. a torch
+ *     stream) must order the slot after it -- kzgmi_stream_wait(ctx, slot, stream) (no host
+ *     sync), or synchronise that stream -- before the call that reads them.  Device outputs
+ *     (partials, digests, generated points) are complete when the call, or the
+ *     kzgmi_slot_wait / kzgmi_msm_wait that completes it, returns.  Device buffers passed to
+ *     an async call must stay allocated until its wait returns.
  *   - Randomisers: r_i = int_be(SHA256(seed || le64(i))[0:16]) >> 1 (1 if zero); 127-bit,
  *     counter mode, so a shard [off, off+n) derives its own r_i with no communication.
  *     seed == NULL draws 32 bytes from the OS CSPRNG (verifier-private randomness).
@@ -66,7 +73,7 @@ typedef enum { KZGMI_BLS12_381 = 0, KZGMI_BN254 = 1 } kzgmi_curve;
                                         GLV endomorphism, which is exact only on G1 (kzgmi_set_glv).
                                         Results for inputs outside G1 are then unspecified. */
 
-typedef struct kzgmi_ctx kzgmi_ctx; /* one GPU, its streams and workspaces */
+typedef struct kzgmi_ctx kzgmi_ctx; /* one GPU (or a device list), its streams and workspaces */
 typedef struct kzgmi_srs kzgmi_srs; /* {G1, [1]_2, [tau]_2} + precomputed Miller lines */
 typedef struct kzgmi_ck kzgmi_ck;   /* prover commit key: [tau^i]_1 + fixed-base tables */
 
@@ -75,16 +82,34 @@ const char* kzgmi_version(void);
 /* Thread-local description of the last error. */
 const char* kzgmi_last_error(void);
 
-/* SURVEY.md 8b kzgmi_ctx_create: bind device `device_id` (>= 0).  `pipeline_slots` >= 1 is
+/* SURVEY.md 8b kzgmi_ctx_create, single device: bind device `device_id` (>= 0).  `pipeline_slots` >= 1 is
  * the number of independent workspaces/streams for the async batch API (1 is enough for
  * the synchronous calls), at most 64; each holds ~1 GiB at n = 2^20. */
 int kzgmi_ctx_create(kzgmi_ctx** out, int device_id, int pipeline_slots);
 void kzgmi_ctx_destroy(kzgmi_ctx* ctx);
 
-/* SURVEY.md 8b kzgmi_srs_load (BASELINE.json:5 "srs"): G2 generator and [tau]_2 (host
- * encodings).  Precomputes the Miller-loop line coefficients on the device. */
-int kzgmi_srs_load(kzgmi_ctx* ctx, kzgmi_curve curve, const uint8_t* g2, const uint8_t* tau_g2,
-                   kzgmi_srs** out);
+/* SURVEY.md 8b kzgmi_ctx_create(out, device_ids, n_devices): one context over a device list
+ * (one process driving several GPUs; a device id may repeat).  device_ids[0] is the primary
+ * device: every single-device entry point below runs there.  The host-buffer entry points
+ * kzgmi_batch_verify / kzgmi_batch_verify_ex / kzgmi_msm_g1 split their input by point range
+ * over all devices (balanced, in units of 4096), run the shards concurrently and combine the
+ * partial sums on the primary; kzgmi_batch_verify_multi_device / kzgmi_msm_g1_multi_device take
+ * shards already resident on each device.  The exchange is 2 (batch) or 1 (MSM) partial
+ * records per device, copied to the primary with hipMemcpyPeer (xGMI); processes that own one
+ * GPU each instead all-gather kzgmi_batch_partial_device records over RCCL. */
+int kzgmi_ctx_create_multi(kzgmi_ctx** out, const int* device_ids, int n_devices, int pipeline_slots);
+int kzgmi_ctx_num_devices(const kzgmi_ctx* ctx);
+
+/* Order slot `slot`'s stream after all work enqueued so far on `hip_stream` (a hipStream_t of
+ * the ctx's primary device, passed as void*; NULL = the null stream), without a host sync. */
+int kzgmi_stream_wait(kzgmi_ctx* ctx, int slot, void* hip_stream);
+
+/* SURVEY.md 8b kzgmi_srs_load (BASELINE.json:5 "srs" = {G1, [1]_2, [tau]_2}): host encodings
+ * of the SRS's G1 element g1 (the base of the -t G1 term; validated, must be a G1 member
+ * other than infinity; g1 == NULL means the standard generator), the G2 generator and
+ * [tau]_2.  Precomputes the Miller-loop line coefficients on the device(s). */
+int kzgmi_srs_load(kzgmi_ctx* ctx, kzgmi_curve curve, const uint8_t* g1, const uint8_t* g2,
+                   const uint8_t* tau_g2, kzgmi_srs** out);
 void kzgmi_srs_free(kzgmi_srs* srs);
 
 /* BASELINE.json:5 batch_verify(commitments, zs, ys, proofs, srs) -- host buffers (copied to
@@ -117,6 +142,15 @@ int kzgmi_batch_verify_device_ex_async(kzgmi_ctx* ctx, const kzgmi_srs* srs, int
                                        const void* d_commitments, const void* d_zs,
                                        const void* d_ys, const void* d_proofs, size_t n,
                                        const uint8_t* seed32, uint32_t flags);
+
+/* Multi-device context (kzgmi_ctx_create_multi): device d holds n_per_device[d] tuples
+ * (global indices follow device order) at d_*[d], device pointers on device_ids[d].  flags as
+ * kzgmi_batch_verify_ex; with KZGMI_FLAG_FIAT_SHAMIR every non-empty shard but the last must
+ * hold a multiple of 4096 tuples.  Synchronous. */
+int kzgmi_batch_verify_multi_device(kzgmi_ctx* ctx, const kzgmi_srs* srs, const void* const* d_commitments,
+                                    const void* const* d_zs, const void* const* d_ys,
+                                    const void* const* d_proofs, const size_t* n_per_device,
+                                    const uint8_t* seed32, uint32_t flags, int* ok_out);
 
 /* Fiat-Shamir challenge of KZGMI_FLAG_FIAT_SHAMIR for a device-resident batch (flags:
  * KZGMI_FLAG_COMPRESSED): r as 32 big-endian bytes. */
@@ -166,6 +200,10 @@ int kzgmi_msm_wait(kzgmi_ctx* ctx, int slot, uint8_t* out);
  * partial (A_k, B_k) as 2 opaque partial-point records (kzgmi_partial_bytes() each) to
  * device memory; the records are all-gathered over RCCL and any rank combines them. */
 size_t kzgmi_partial_bytes(kzgmi_curve curve);
+/* Encode `count` device-resident partial records (e.g. a shard's A_k, B_k) as G1 encodings
+ * (count x G1 bytes, host) -- for checking partials against a CPU reference. */
+int kzgmi_partial_encode_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_records, size_t count,
+                                uint8_t* out);
 int kzgmi_batch_partial_device(kzgmi_ctx* ctx, const kzgmi_srs* srs, const void* d_commitments,
                                const void* d_zs, const void* d_ys, const void* d_proofs, size_t n,
                                uint64_t index_offset, const uint8_t* seed32, void* d_partial_out);
@@ -184,6 +222,10 @@ int kzgmi_msm_partial_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_po
                              const void* d_scalars, size_t n, void* d_partial_out);
 int kzgmi_msm_combine_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* d_partials,
                              int n_parts, uint8_t* out);
+/* sum k_i P_i over shards resident on each device of a multi-device context (see
+ * kzgmi_batch_verify_multi_device); out = G1 encoding. */
+int kzgmi_msm_g1_multi_device(kzgmi_ctx* ctx, kzgmi_curve curve, const void* const* d_points,
+                              const void* const* d_scalars, const size_t* n_per_device, uint8_t* out);
 /* Pipelined forms: the partial completes with kzgmi_slot_wait, the combine (sum of the
  * gathered records, encoded) with kzgmi_msm_wait. */
 int kzgmi_msm_partial_device_async(kzgmi_ctx* ctx, kzgmi_curve curve, int slot, const void* d_points,

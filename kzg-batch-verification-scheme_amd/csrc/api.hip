@@ -75,6 +75,7 @@ struct Slot {
   int* host_flags = nullptr;  // pinned: [ok, err]
   uint8_t* host_out = nullptr;  // pinned: encoded MSM result of an async MSM job
   hipEvent_t ev[kNumPhases + 1] = {};
+  hipEvent_t order_ev = nullptr;  // kzgmi_stream_wait: the caller's stream -> this slot's stream
   bool ev_used[kNumPhases + 1] = {};
   bool pending = false;
   bool partial_job = false;  // pending job produces a partial record, not a verdict
@@ -105,6 +106,9 @@ struct kzgmi_ctx {
   DevBuf table[2], table_base[2];
   bool table_ready[2] = {false, false};
   DevBuf lines_tmp, tmp;
+  DevBuf gath;                       // multi-device: partial records gathered from every device
+  DevBuf mdig, mdig_all;             // multi-device Fiat-Shamir: this device's / every device's subtree roots
+  std::vector<kzgmi_ctx*> peers;     // multi-device: contexts of device_ids[1..] (kzgmi_ctx_create_multi)
   std::vector<kzgmi_srs*> srs_list;  // live SRS objects: detached (device memory freed) on destroy
   std::vector<kzgmi_ck*> ck_list;    // live commit keys: same
 };
@@ -122,6 +126,8 @@ struct kzgmi_srs {
   int curve = 0;
   kzgmi_ctx* ctx = nullptr;
   DevBuf lines, q, q_inf;
+  DevBuf g1;                        // the SRS's [1]_1: Montgomery affine point + its infinity byte after it
+  std::vector<kzgmi_srs*> peers;    // multi-device context: the same SRS on each peer device
 };
 
 namespace {
@@ -332,7 +338,9 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
     L::convert_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err);
   }
   if (flags & KZGMI_FLAG_SUBGROUP_CHECK) L::subgroup_check(st, pts, inf, (uint32_t)(2 * n), err);
-  L::set_generator(st, pts + 2 * n, inf + 2 * n);
+  // the SRS's [1]_1 as the last term of MSM#1: -t [1]_1
+  HIPCHK(hipMemcpyAsync(pts + 2 * n, srs->g1.p, sizeof(Affine<Cv>), hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpyAsync(inf + 2 * n, srs->g1.template as<uint8_t>() + sizeof(Affine<Cv>), 1, hipMemcpyDeviceToDevice, st));
   if (glv) L::endo_points(st, pts, inf, (uint32_t)PH, pts + PH, inf + PH);
   mark(c, s, PH_CONVERT + 1);
   if (flags & KZGMI_FLAG_FIAT_SHAMIR) {  // r from the transcript of this (whole) batch
@@ -444,6 +452,18 @@ int check_ctx(kzgmi_ctx* c, int slot = 0) {
   return set_dev(c);
 }
 
+int batch_multi_host(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commitments, const uint8_t* zs,
+                     const uint8_t* ys, const uint8_t* proofs, size_t n, const uint8_t* seed32, uint32_t flags,
+                     int* ok_out);
+int msm_multi_host(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* points, const uint8_t* scalars, size_t n,
+                   uint8_t* out);
+
+// synchronous entry points that run on slot 0 must not overwrite a pending async job's
+// flags / result buffers (its later kzgmi_slot_wait would report theirs)
+int slot0_idle(kzgmi_ctx* c) {
+  return c->slots[0].pending ? fail(KZGMI_ERR_ARG, "slot 0 busy: complete its pending job (kzgmi_slot_wait / kzgmi_msm_wait) first") : 0;
+}
+
 template <class Cv>
 int ensure_table(kzgmi_ctx* c, hipStream_t st) {
   if (c->table_ready[Cv::ID]) return 0;
@@ -503,6 +523,7 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
     for (DevBuf* b : bufs) b->release();
     for (auto& e : s.ev)
       if (e) (void)hipEventDestroy(e);
+    if (s.order_ev) (void)hipEventDestroy(s.order_ev);
     if (s.host_flags) (void)hipHostFree(s.host_flags);
     if (s.host_out) (void)hipHostFree(s.host_out);
     if (s.stream) (void)hipStreamDestroy(s.stream);
@@ -519,40 +540,61 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
     srs->lines.release();
     srs->q.release();
     srs->q_inf.release();
+    srs->g1.release();
     srs->ctx = nullptr;
   }
+  c->gath.release();
+  std::vector<kzgmi_ctx*> peers;
+  peers.swap(c->peers);
   delete c;
+  for (kzgmi_ctx* p : peers) kzgmi_ctx_destroy(p);
 }
 
-int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g2, const uint8_t* tau_g2, kzgmi_srs** out) {
+int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uint8_t* g2, const uint8_t* tau_g2,
+                   kzgmi_srs** out) {
   CHK(check_ctx(c));
   if (!g2 || !tau_g2 || !out) return fail(KZGMI_ERR_ARG, "null srs argument");
-  return dispatch(curve, [&](auto cv) -> int {
+  *out = nullptr;
+  CHK(slot0_idle(c));
+  int rc = dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     Slot& s = c->slots[0];
-    const size_t gb = g2_bytes(Cv::ID);
+    const size_t gb = g2_bytes(Cv::ID), g1b = g1_bytes(Cv::ID);
     kzgmi_srs* srs = new kzgmi_srs();
     srs->curve = Cv::ID;
     srs->ctx = c;
     int r = 0;
-    if ((r = s.stage.ensure(2 * gb)) || (r = s.flags.ensure(16)) || (r = srs->q.ensure(2 * sizeof(G2Aff<Cv>))) ||
-        (r = srs->q_inf.ensure(16)) || (r = srs->lines.ensure(2 * Launch<Cv>::num_lines() * sizeof(Line<Cv>)))) {
+    if ((r = s.stage.ensure(2 * gb + g1b)) || (r = s.flags.ensure(16)) || (r = srs->q.ensure(2 * sizeof(G2Aff<Cv>))) ||
+        (r = srs->q_inf.ensure(16)) || (r = srs->lines.ensure(2 * Launch<Cv>::num_lines() * sizeof(Line<Cv>))) ||
+        (r = srs->g1.ensure(sizeof(Affine<Cv>) + 16))) {
       delete srs;
       return r;
     }
-    // slot 0 = [tau]_2, slot 1 = [1]_2
-    std::vector<uint8_t> h(2 * gb);
+    // slot 0 = [tau]_2, slot 1 = [1]_2, then [1]_1
+    std::vector<uint8_t> h(2 * gb + g1b);
     memcpy(h.data(), tau_g2, gb);
     memcpy(h.data() + gb, g2, gb);
+    if (g1) memcpy(h.data() + 2 * gb, g1, g1b);
     hipStream_t st = s.stream;
-    bool okk = hipMemcpyAsync(s.stage.p, h.data(), 2 * gb, hipMemcpyHostToDevice, st) == hipSuccess &&
+    Affine<Cv>* g1p = srs->g1.template as<Affine<Cv>>();
+    uint8_t* g1inf = srs->g1.template as<uint8_t>() + sizeof(Affine<Cv>);
+    uint8_t g1inf_h = 0;
+    bool okk = hipMemcpyAsync(s.stage.p, h.data(), h.size(), hipMemcpyHostToDevice, st) == hipSuccess &&
                hipMemsetAsync(s.flags.p, 0, 16, st) == hipSuccess;
     if (okk) {
+      uint32_t* err = s.flags.template as<uint32_t>() + 1;
       Launch<Cv>::convert_g2(st, s.stage.template as<uint8_t>(), 2, srs->q.template as<G2Aff<Cv>>(), srs->q_inf.template as<uint8_t>(),
-                                         s.flags.template as<uint32_t>() + 1);
+                                         err);
       Launch<Cv>::precompute_lines(st, srs->q.template as<G2Aff<Cv>>(), srs->lines.template as<Line<Cv>>());
+      if (g1) {  // validated like any input point, and it must be in G1 (GLV and the check rely on it)
+        Launch<Cv>::convert_points(st, s.stage.template as<uint8_t>() + 2 * gb, 1, g1p, g1inf, err);
+        Launch<Cv>::subgroup_check(st, g1p, g1inf, 1, err);
+      } else {   // NULL: the standard generator
+        Launch<Cv>::set_generator(st, g1p, g1inf);
+      }
       okk = hipGetLastError() == hipSuccess &&
             hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
+            hipMemcpyAsync(&g1inf_h, g1inf, 1, hipMemcpyDeviceToHost, st) == hipSuccess &&
             hipStreamSynchronize(st) == hipSuccess;
     }
     if (!okk) {
@@ -560,6 +602,7 @@ int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g2, const uin
       return fail(KZGMI_ERR_DEVICE, "srs upload/precompute failed");
     }
     int e = map_device_err((uint32_t)s.host_flags[1]);
+    if (!e && g1inf_h) e = fail(KZGMI_ERR_ARG, "SRS G1 element is the point at infinity");
     if (e) {
       kzgmi_srs_free(srs);
       return e;
@@ -568,10 +611,23 @@ int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g2, const uin
     *out = srs;
     return 0;
   });
+  if (rc) return rc;
+  for (kzgmi_ctx* p : c->peers) {  // multi-device context: the same SRS on every device
+    kzgmi_srs* ps = nullptr;
+    if (int r = kzgmi_srs_load(p, curve, g1, g2, tau_g2, &ps)) {
+      kzgmi_srs_free(*out);
+      *out = nullptr;
+      return r;
+    }
+    (*out)->peers.push_back(ps);
+  }
+  return set_dev(c);
 }
 
 void kzgmi_srs_free(kzgmi_srs* srs) {
   if (!srs) return;
+  for (kzgmi_srs* p : srs->peers) kzgmi_srs_free(p);
+  srs->peers.clear();
   if (kzgmi_ctx* c = srs->ctx) {  // still attached: free its device memory on its device
     (void)hipSetDevice(c->device);
     auto& v = c->srs_list;
@@ -579,6 +635,7 @@ void kzgmi_srs_free(kzgmi_srs* srs) {
     srs->lines.release();
     srs->q.release();
     srs->q_inf.release();
+    srs->g1.release();
   }
   delete srs;  // a detached SRS (its context already destroyed) owns no device memory
 }
@@ -642,7 +699,10 @@ int kzgmi_batch_verify_ex(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* com
                           int* ok_out) {
   CHK(check_ctx(c));
   if (!srs || !ok_out) return fail(KZGMI_ERR_ARG, "null argument");
+  if (srs->ctx != c) return fail(KZGMI_ERR_ARG, "srs does not belong to this context");
   if (n && (!commitments || !zs || !ys || !proofs)) return fail(KZGMI_ERR_ARG, "null input");
+  CHK(slot0_idle(c));
+  if (!c->peers.empty()) return batch_multi_host(c, srs, commitments, zs, ys, proofs, n, seed32, flags, ok_out);
   Slot& s = c->slots[0];
   uint8_t *dC = nullptr, *dpi = nullptr, *dz = nullptr, *dy = nullptr;
   if (n) {
@@ -665,6 +725,7 @@ int kzgmi_batch_verify_ex(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* com
 int kzgmi_last_combination(kzgmi_ctx* c, uint8_t* a_out, uint8_t* b_out) {
   CHK(check_ctx(c));
   if (!a_out || !b_out) return fail(KZGMI_ERR_ARG, "null output");
+  CHK(slot0_idle(c));
   Slot& s = c->slots[0];
   if (!s.res.p) return fail(KZGMI_ERR_ARG, "no batch has run on slot 0");
   return dispatch(s.curve, [&](auto cv) -> int {
@@ -856,6 +917,7 @@ int kzgmi_commit(kzgmi_ctx* c, const kzgmi_ck* ck, const uint8_t* coeffs, size_t
   CHK(check_ctx(c));
   if (!ck || (m && !coeffs)) return fail(KZGMI_ERR_ARG, "null argument");
   if (m == 0) return kzgmi_commit_device(c, ck, nullptr, 0, out);
+  CHK(slot0_idle(c));
   Slot& s = c->slots[0];
   CHK(s.stage.ensure(m * 32));
   HIPCHK(hipMemcpyAsync(s.stage.p, coeffs, m * 32, hipMemcpyHostToDevice, s.stream));
@@ -866,6 +928,7 @@ int kzgmi_msm_g1_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dpts, const
   CHK(check_ctx(c));
   if (!out || (n && (!dpts || !dsc))) return fail(KZGMI_ERR_ARG, "null argument");
   if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "MSM too large (max 2^26 points per call)");
+  CHK(slot0_idle(c));
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     Slot& s = c->slots[0];
@@ -933,6 +996,8 @@ int kzgmi_msm_g1(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* points, const u
   if (!out || (n && (!points || !scalars))) return fail(KZGMI_ERR_ARG, "null argument");
   if (curve != KZGMI_BLS12_381 && curve != KZGMI_BN254) return fail(KZGMI_ERR_ARG, "unknown curve");
   if (n == 0) return kzgmi_msm_g1_device(c, curve, nullptr, nullptr, 0, out);
+  CHK(slot0_idle(c));
+  if (!c->peers.empty()) return msm_multi_host(c, curve, points, scalars, n, out);
   Slot& s = c->slots[0];
   const size_t gb = g1_bytes(curve);
   CHK(s.stage.ensure(n * (gb + 32)));
@@ -954,6 +1019,10 @@ int kzgmi_batch_partial_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slo
   if (flags & ~kAllFlags) return fail(KZGMI_ERR_ARG, "unknown flags");
   if (flags & KZGMI_FLAG_FIAT_SHAMIR)
     return fail(KZGMI_ERR_ARG, "shards take the Fiat-Shamir r as seed32 (see kzgmi_fs_challenge_from_digests_device)");
+  // r^i is built from the FS_POW_BITS = 32 low bits of the global index (fs.hpp): indices at or
+  // above 2^32 would wrap and repeat randomisers
+  if ((flags & KZGMI_FLAG_POWERS) && (index_offset > (1ull << 32) || n > (1ull << 32) - index_offset))
+    return fail(KZGMI_ERR_ARG, "KZGMI_FLAG_POWERS needs index_offset + n <= 2^32");
   CHK(check_ctx(c, slot));
   if (!srs || srs->ctx != c || !d_partial_out) return fail(KZGMI_ERR_ARG, "bad argument");
   if (!seed32) return fail(KZGMI_ERR_ARG, "sharded verification needs an explicit shared seed");
@@ -1120,6 +1189,7 @@ int kzgmi_g1_compress_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_poin
   CHK(check_ctx(c));
   if (n && (!d_points || !d_out)) return fail(KZGMI_ERR_ARG, "null argument");
   if (n > (1u << 27)) return fail(KZGMI_ERR_ARG, "too many points (max 2^27 per call)");
+  CHK(slot0_idle(c));
   Slot& s = c->slots[0];
   return dispatch(curve, [&](auto cv) -> int {
     Launch<decltype(cv)>::compress_points(s.stream, (const uint8_t*)d_points, (uint32_t)n, (uint8_t*)d_out);
@@ -1133,6 +1203,8 @@ int kzgmi_msm_partial_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dpts, 
                              void* d_partial_out) {
   CHK(check_ctx(c));
   if (!d_partial_out || (n && (!dpts || !dsc))) return fail(KZGMI_ERR_ARG, "bad argument");
+  if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "MSM too large (max 2^26 points per call)");
+  CHK(slot0_idle(c));
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     Slot& s = c->slots[0];
@@ -1204,6 +1276,7 @@ int kzgmi_msm_combine_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, co
 int kzgmi_msm_combine_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_partials, int n_parts, uint8_t* out) {
   CHK(check_ctx(c));
   if (!d_partials || n_parts < 1 || !out) return fail(KZGMI_ERR_ARG, "bad argument");
+  CHK(slot0_idle(c));
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     using XY = Xyzz<Cv>;
@@ -1224,6 +1297,7 @@ int kzgmi_msm_combine_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_part
 int kzgmi_pairing(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uint8_t* g2, uint8_t* out) {
   CHK(check_ctx(c));
   if (!g1 || !g2 || !out) return fail(KZGMI_ERR_ARG, "null argument");
+  CHK(slot0_idle(c));
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     Slot& s = c->slots[0];
@@ -1262,6 +1336,7 @@ int kzgmi_pairing(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uint
 int kzgmi_gen_g1(kzgmi_ctx* c, kzgmi_curve curve, const void* d_scalars, size_t n, void* d_points_out) {
   CHK(check_ctx(c));
   if (n && (!d_scalars || !d_points_out)) return fail(KZGMI_ERR_ARG, "null argument");
+  CHK(slot0_idle(c));
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     Slot& s = c->slots[0];
@@ -1280,6 +1355,7 @@ int kzgmi_gen_tuples(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* tau32, cons
                      void* dC, void* dz, void* dy, void* dpi) {
   CHK(check_ctx(c));
   if (!tau32 || !seed32 || (n && (!dC || !dz || !dy || !dpi))) return fail(KZGMI_ERR_ARG, "null argument");
+  CHK(slot0_idle(c));
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     using FrF = Fp<typename Cv::FrP>;
@@ -1308,6 +1384,7 @@ int kzgmi_gen_tuples(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* tau32, cons
 int kzgmi_g2_mul(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g2, const uint8_t* k32, uint8_t* out) {
   CHK(check_ctx(c));
   if (!g2 || !k32 || !out) return fail(KZGMI_ERR_ARG, "null argument");
+  CHK(slot0_idle(c));
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     Slot& s = c->slots[0];
@@ -1341,6 +1418,7 @@ int kzgmi_g2_mul(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g2, const uint8
 int kzgmi_probe_fpmul(kzgmi_ctx* c, kzgmi_curve curve, double* muls_per_s) {
   CHK(check_ctx(c));
   if (!muls_per_s) return fail(KZGMI_ERR_ARG, "null argument");
+  CHK(slot0_idle(c));
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     Slot& s = c->slots[0];
@@ -1370,7 +1448,8 @@ int kzgmi_set_glv(kzgmi_ctx* c, int msm, int batch) {
     if (s.pending) return fail(KZGMI_ERR_ARG, "kzgmi_set_glv with jobs in flight");
   c->glv_msm = msm != 0;
   c->glv_batch = batch != 0;
-  return 0;
+  for (kzgmi_ctx* p : c->peers) CHK(kzgmi_set_glv(p, msm, batch));
+  return set_dev(c);
 }
 
 int kzgmi_set_trusted_g1(kzgmi_ctx* c, int on) {
@@ -1378,7 +1457,8 @@ int kzgmi_set_trusted_g1(kzgmi_ctx* c, int on) {
   for (auto& s : c->slots)
     if (s.pending) return fail(KZGMI_ERR_ARG, "kzgmi_set_trusted_g1 with jobs in flight");
   c->msm_trusted_g1 = on != 0;
-  return 0;
+  for (kzgmi_ctx* p : c->peers) CHK(kzgmi_set_trusted_g1(p, on));
+  return set_dev(c);
 }
 
 int kzgmi_set_profiling(kzgmi_ctx* c, int on) {
@@ -1394,6 +1474,272 @@ int kzgmi_get_phase_ms(kzgmi_ctx* c, double* out, int max_n) {
   int k = max_n < kNumPhases ? max_n : kNumPhases;
   for (int i = 0; i < k; ++i) out[i] = c->phase_calls ? c->phase_ms[i] / c->phase_calls : 0.0;
   return k;
+}
+
+// ------------------------------------------------------------------------------ stream order
+int kzgmi_stream_wait(kzgmi_ctx* c, int slot, void* stream) {
+  CHK(check_ctx(c, slot));
+  Slot& s = c->slots[slot];
+  if (!s.order_ev) HIPCHK(hipEventCreateWithFlags(&s.order_ev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(s.order_ev, (hipStream_t)stream));
+  HIPCHK(hipStreamWaitEvent(s.stream, s.order_ev, 0));
+  return 0;
+}
+
+int kzgmi_partial_encode_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_records, size_t count, uint8_t* out) {
+  CHK(check_ctx(c));
+  if (!d_records || !out || count == 0 || count > 4096) return fail(KZGMI_ERR_ARG, "bad argument");
+  CHK(slot0_idle(c));
+  return dispatch(curve, [&](auto cv) -> int {
+    using Cv = decltype(cv);
+    Slot& s = c->slots[0];
+    const size_t gb = g1_bytes(Cv::ID);
+    CHK(s.outb.ensure(count * gb));
+    Launch<Cv>::encode_points(s.stream, (const Xyzz<Cv>*)d_records, (uint32_t)count, s.outb.template as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, s.outb.p, count * gb, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipStreamSynchronize(s.stream));
+    return 0;
+  });
+}
+
+// ------------------------------------------------------------------------------ multi-device context
+int kzgmi_ctx_create_multi(kzgmi_ctx** out, const int* device_ids, int n_devices, int pipeline_slots) {
+  if (!out || !device_ids || n_devices < 1 || n_devices > 64) return fail(KZGMI_ERR_ARG, "bad multi-device ctx args");
+  *out = nullptr;
+  kzgmi_ctx* c = nullptr;
+  CHK(kzgmi_ctx_create(&c, device_ids[0], pipeline_slots));
+  for (int k = 1; k < n_devices; ++k) {
+    kzgmi_ctx* p = nullptr;
+    if (int r = kzgmi_ctx_create(&p, device_ids[k], pipeline_slots)) {
+      kzgmi_ctx_destroy(c);
+      return r;
+    }
+    c->peers.push_back(p);
+  }
+  CHK(set_dev(c));
+  *out = c;
+  return 0;
+}
+
+int kzgmi_ctx_num_devices(const kzgmi_ctx* c) { return c ? 1 + (int)c->peers.size() : 0; }
+
+}  // extern "C"
+
+// Shards run concurrently (one async partial per device on its slot 0), the partial records are
+// copied to the primary device (hipMemcpyPeer over xGMI: 2 XYZZ records per device), and the
+// primary sums them and runs the pairing check -- the single-process form of the RCCL
+// all-gather that kzgmi/distributed.py does across processes.
+namespace {
+
+kzgmi_ctx* dev_ctx(kzgmi_ctx* c, int d) { return d == 0 ? c : c->peers[d - 1]; }
+
+// wait every device's slot 0 (first error wins; every slot is completed either way)
+int wait_all(kzgmi_ctx* c, int started) {
+  int first = 0;
+  std::string msg;
+  for (int d = 0; d < started; ++d) {
+    int r = kzgmi_slot_wait(dev_ctx(c, d), 0, nullptr);
+    if (r && !first) {
+      first = r;
+      msg = g_err;
+    }
+  }
+  if (first) return fail(first, msg);
+  return 0;
+}
+
+// children's records (in their `gath`) -> c->gath[d]
+int gather_records(kzgmi_ctx* c, size_t rec) {
+  for (size_t d = 1; d <= c->peers.size(); ++d) {
+    kzgmi_ctx* p = c->peers[d - 1];
+    HIPCHK(hipMemcpyPeer((uint8_t*)c->gath.p + d * rec, c->device, p->gath.p, p->device, rec));
+  }
+  return set_dev(c);
+}
+
+int batch_multi(kzgmi_ctx* c, const kzgmi_srs* srs, const void* const* dC, const void* const* dz,
+                const void* const* dy, const void* const* dpi, const size_t* nd, const uint8_t* seed32,
+                uint32_t flags, int* ok_out) {
+  const int D = 1 + (int)c->peers.size();
+  if (srs->peers.size() != c->peers.size()) return fail(KZGMI_ERR_ARG, "srs was not loaded on this context");
+  const kzgmi_curve curve = (kzgmi_curve)srs->curve;
+  const size_t rec = 2 * kzgmi_partial_bytes(curve);
+  std::vector<uint64_t> off(D + 1, 0);
+  for (int d = 0; d < D; ++d) {
+    if (nd[d] && (!dC[d] || !dz[d] || !dy[d] || !dpi[d])) return fail(KZGMI_ERR_ARG, "null input");
+    if (nd[d] > (1u << 26)) return fail(KZGMI_ERR_ARG, "shard too large (max 2^26 tuples per device)");
+    off[d + 1] = off[d] + nd[d];
+  }
+  uint8_t sb[32];
+  if (flags & KZGMI_FLAG_FIAT_SHAMIR) {  // one transcript over the whole batch: subtree roots gathered
+    if (flags & KZGMI_FLAG_POWERS) return fail(KZGMI_ERR_ARG, "KZGMI_FLAG_POWERS and KZGMI_FLAG_FIAT_SHAMIR are exclusive");
+    const uint64_t ntot = off[D];
+    if (ntot == 0) {
+      *ok_out = 1;
+      return 0;
+    }
+    const size_t nch_tot = (ntot + FS_CHUNK - 1) / FS_CHUNK;
+    CHK(c->mdig_all.ensure(nch_tot * 32));
+    size_t at = 0;
+    for (int d = 0; d < D; ++d) {
+      if (!nd[d]) continue;
+      if (off[d] % FS_CHUNK) return fail(KZGMI_ERR_ARG, "Fiat-Shamir shards must start at multiples of 4096 tuples");
+      kzgmi_ctx* p = dev_ctx(c, d);
+      const size_t nch = (nd[d] + FS_CHUNK - 1) / FS_CHUNK;
+      CHK(set_dev(p));
+      CHK(p->mdig.ensure(nch * 32));
+      CHK(kzgmi_fs_chunk_digests_device(p, curve, dC[d], dz[d], dy[d], dpi[d], nd[d], off[d],
+                                        flags & KZGMI_FLAG_COMPRESSED, p->mdig.p));
+      HIPCHK(hipMemcpyPeer((uint8_t*)c->mdig_all.p + at * 32, c->device, p->mdig.p, p->device, nch * 32));
+      at += nch;
+    }
+    CHK(kzgmi_fs_challenge_from_digests_device(c, curve, c->mdig_all.p, nch_tot, ntot, sb));
+    seed32 = sb;
+    flags &= ~KZGMI_FLAG_FIAT_SHAMIR;
+  } else if (!seed32) {
+    uint8_t tmp[32];
+    make_seed(nullptr, tmp);  // one verifier-private seed shared by every shard
+    memcpy(sb, tmp, 32);
+    seed32 = sb;
+  }
+  CHK(set_dev(c));
+  CHK(c->gath.ensure(D * rec));
+  for (int d = 0; d < D; ++d) {
+    kzgmi_ctx* p = dev_ctx(c, d);
+    int r = 0;
+    if (d > 0) {
+      r = set_dev(p);
+      if (!r) r = p->gath.ensure(rec);
+    }
+    if (!r)
+      r = kzgmi_batch_partial_device_async(p, d == 0 ? srs : srs->peers[d - 1], 0, dC[d], dz[d], dy[d], dpi[d], nd[d],
+                                           off[d], seed32, flags, d == 0 ? c->gath.p : p->gath.p);
+    if (r) {
+      std::string msg = g_err;
+      (void)wait_all(c, d);
+      return fail(r, msg);
+    }
+  }
+  CHK(wait_all(c, D));
+  CHK(gather_records(c, rec));
+  return kzgmi_batch_combine_device(c, srs, c->gath.p, D, ok_out);
+}
+
+int msm_multi(kzgmi_ctx* c, kzgmi_curve curve, const void* const* dp, const void* const* ds, const size_t* nd,
+              uint8_t* out) {
+  const int D = 1 + (int)c->peers.size();
+  if (curve != KZGMI_BLS12_381 && curve != KZGMI_BN254) return fail(KZGMI_ERR_ARG, "unknown curve");
+  const size_t rec = kzgmi_partial_bytes(curve);
+  CHK(set_dev(c));
+  CHK(c->gath.ensure(D * rec));
+  for (int d = 0; d < D; ++d) {
+    kzgmi_ctx* p = dev_ctx(c, d);
+    int r = 0;
+    if (d > 0) {
+      r = set_dev(p);
+      if (!r) r = p->gath.ensure(rec);
+    }
+    if (!r) r = kzgmi_msm_partial_device_async(p, curve, 0, dp[d], ds[d], nd[d], d == 0 ? c->gath.p : p->gath.p);
+    if (r) {
+      std::string msg = g_err;
+      (void)wait_all(c, d);
+      return fail(r, msg);
+    }
+  }
+  CHK(wait_all(c, D));
+  CHK(gather_records(c, rec));
+  return kzgmi_msm_combine_device(c, curve, c->gath.p, D, out);
+}
+
+// balanced split of n tuples/points over the devices in units of 4096 (Fiat-Shamir subtrees)
+std::vector<size_t> split_units(size_t n, int D) {
+  const size_t units = (n + FS_CHUNK - 1) / FS_CHUNK;
+  std::vector<size_t> nd(D);
+  size_t lo = 0;
+  for (int d = 0; d < D; ++d) {
+    size_t u1 = units * (d + 1) / D;
+    size_t hi = std::min(n, u1 * FS_CHUNK);
+    nd[d] = hi - lo;
+    lo = hi;
+  }
+  return nd;
+}
+
+int batch_multi_host(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commitments, const uint8_t* zs,
+                     const uint8_t* ys, const uint8_t* proofs, size_t n, const uint8_t* seed32, uint32_t flags,
+                     int* ok_out) {
+  const int D = 1 + (int)c->peers.size();
+  const size_t gb = (flags & KZGMI_FLAG_COMPRESSED) ? g1_bytes(srs->curve) / 2 : g1_bytes(srs->curve);
+  std::vector<size_t> nd = split_units(n, D);
+  std::vector<const void*> pC(D), pz(D), py(D), ppi(D);
+  size_t lo = 0;
+  for (int d = 0; d < D; ++d) {
+    kzgmi_ctx* p = dev_ctx(c, d);
+    Slot& s = p->slots[0];
+    CHK(set_dev(p));
+    CHK(s.stage.ensure(nd[d] * (2 * gb + 64)));
+    uint8_t* base = s.stage.template as<uint8_t>();
+    pC[d] = base;
+    ppi[d] = base + nd[d] * gb;
+    pz[d] = base + 2 * nd[d] * gb;
+    py[d] = base + 2 * nd[d] * gb + 32 * nd[d];
+    if (nd[d]) {
+      HIPCHK(hipMemcpyAsync((void*)pC[d], commitments + lo * gb, nd[d] * gb, hipMemcpyHostToDevice, s.stream));
+      HIPCHK(hipMemcpyAsync((void*)ppi[d], proofs + lo * gb, nd[d] * gb, hipMemcpyHostToDevice, s.stream));
+      HIPCHK(hipMemcpyAsync((void*)pz[d], zs + lo * 32, nd[d] * 32, hipMemcpyHostToDevice, s.stream));
+      HIPCHK(hipMemcpyAsync((void*)py[d], ys + lo * 32, nd[d] * 32, hipMemcpyHostToDevice, s.stream));
+    }
+    lo += nd[d];
+  }
+  return batch_multi(c, srs, pC.data(), pz.data(), py.data(), ppi.data(), nd.data(), seed32, flags, ok_out);
+}
+
+int msm_multi_host(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* points, const uint8_t* scalars, size_t n,
+                   uint8_t* out) {
+  const int D = 1 + (int)c->peers.size();
+  const size_t gb = g1_bytes(curve);
+  std::vector<size_t> nd = split_units(n, D);
+  std::vector<const void*> pp(D), ps(D);
+  size_t lo = 0;
+  for (int d = 0; d < D; ++d) {
+    kzgmi_ctx* p = dev_ctx(c, d);
+    Slot& s = p->slots[0];
+    CHK(set_dev(p));
+    CHK(s.stage.ensure(nd[d] * (gb + 32)));
+    pp[d] = s.stage.p;
+    ps[d] = s.stage.template as<uint8_t>() + nd[d] * gb;
+    if (nd[d]) {
+      HIPCHK(hipMemcpyAsync((void*)pp[d], points + lo * gb, nd[d] * gb, hipMemcpyHostToDevice, s.stream));
+      HIPCHK(hipMemcpyAsync((void*)ps[d], scalars + lo * 32, nd[d] * 32, hipMemcpyHostToDevice, s.stream));
+    }
+    lo += nd[d];
+  }
+  return msm_multi(c, curve, pp.data(), ps.data(), nd.data(), out);
+}
+
+}  // namespace
+
+extern "C" {
+
+int kzgmi_batch_verify_multi_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* const* d_commitments,
+                                    const void* const* d_zs, const void* const* d_ys, const void* const* d_proofs,
+                                    const size_t* n_per_device, const uint8_t* seed32, uint32_t flags, int* ok_out) {
+  CHK(check_ctx(c));
+  if (!srs || srs->ctx != c || !ok_out || !d_commitments || !d_zs || !d_ys || !d_proofs || !n_per_device)
+    return fail(KZGMI_ERR_ARG, "bad argument");
+  if (flags & ~kAllFlags) return fail(KZGMI_ERR_ARG, "unknown flags");
+  if ((flags & KZGMI_FLAG_POWERS) && !seed32) return fail(KZGMI_ERR_ARG, "KZGMI_FLAG_POWERS needs r in seed32");
+  CHK(slot0_idle(c));
+  return batch_multi(c, srs, d_commitments, d_zs, d_ys, d_proofs, n_per_device, seed32, flags, ok_out);
+}
+
+int kzgmi_msm_g1_multi_device(kzgmi_ctx* c, kzgmi_curve curve, const void* const* d_points,
+                              const void* const* d_scalars, const size_t* n_per_device, uint8_t* out) {
+  CHK(check_ctx(c));
+  if (!d_points || !d_scalars || !n_per_device || !out) return fail(KZGMI_ERR_ARG, "bad argument");
+  CHK(slot0_idle(c));
+  return msm_multi(c, curve, d_points, d_scalars, n_per_device, out);
 }
 
 }  // extern "C"

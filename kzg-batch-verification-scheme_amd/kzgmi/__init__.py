@@ -26,7 +26,8 @@ CURVES = {"bls12_381": 0, "bn254": 1}
 FP_BYTES = {"bls12_381": 48, "bn254": 32}
 PHASES = ["convert", "scalars", "sort", "accumulate", "reduce", "combine", "pairing"]
 
-ERR_NAMES = {-1: "ARG", -2: "ENCODING", -3: "NOT_ON_CURVE", -4: "SCALAR", -5: "DEVICE", -6: "OOM"}
+ERR_NAMES = {-1: "ARG", -2: "ENCODING", -3: "NOT_ON_CURVE", -4: "SCALAR", -5: "DEVICE", -6: "OOM",
+             -7: "NOT_IN_SUBGROUP"}
 
 
 class KzgmiError(RuntimeError):
@@ -61,7 +62,14 @@ def lib():
         "kzgmi_phase_names": ([], c.c_char_p),
         "kzgmi_ctx_create": ([c.POINTER(vp), c.c_int, c.c_int], c.c_int),
         "kzgmi_ctx_destroy": ([vp], None),
-        "kzgmi_srs_load": ([vp, c.c_int, u8p, u8p, c.POINTER(vp)], c.c_int),
+        "kzgmi_srs_load": ([vp, c.c_int, u8p, u8p, u8p, c.POINTER(vp)], c.c_int),
+        "kzgmi_ctx_create_multi": ([c.POINTER(vp), c.POINTER(c.c_int), c.c_int, c.c_int], c.c_int),
+        "kzgmi_ctx_num_devices": ([vp], c.c_int),
+        "kzgmi_stream_wait": ([vp, c.c_int, vp], c.c_int),
+        "kzgmi_partial_encode_device": ([vp, c.c_int, vp, sz, u8p], c.c_int),
+        "kzgmi_batch_verify_multi_device": ([vp, vp, c.POINTER(vp), c.POINTER(vp), c.POINTER(vp), c.POINTER(vp),
+                                             c.POINTER(sz), u8p, c.c_uint32, ip], c.c_int),
+        "kzgmi_msm_g1_multi_device": ([vp, c.c_int, c.POINTER(vp), c.POINTER(vp), c.POINTER(sz), u8p], c.c_int),
         "kzgmi_srs_free": ([vp], None),
         "kzgmi_batch_verify": ([vp, vp, u8p, u8p, u8p, u8p, sz, u8p, ip], c.c_int),
         "kzgmi_batch_verify_device": ([vp, vp, vp, vp, vp, vp, sz, u8p, ip], c.c_int),
@@ -127,6 +135,8 @@ def exported_symbols():
         "kzgmi_batch_combine_device_async", "kzgmi_msm_partial_device",
         "kzgmi_msm_combine_device", "kzgmi_pairing", "kzgmi_gen_g1", "kzgmi_gen_tuples",
         "kzgmi_g2_mul", "kzgmi_probe_fpmul", "kzgmi_set_profiling", "kzgmi_get_phase_ms",
+        "kzgmi_ctx_create_multi", "kzgmi_ctx_num_devices", "kzgmi_stream_wait", "kzgmi_partial_encode_device",
+        "kzgmi_batch_verify_multi_device", "kzgmi_msm_g1_multi_device",
     ]
 
 
@@ -147,12 +157,25 @@ def _flags(compressed: bool = False, subgroup_check: bool = False, fiat_shamir: 
 
 
 def _challenge_seed(seed, challenge):
-    """KZGMI_FLAG_POWERS passes r (int or 32 big-endian bytes) in the seed argument."""
+    """The 32-byte seed argument of the C-ABI (the library reads exactly 32 bytes from it).
+    KZGMI_FLAG_POWERS passes r (int < 2^256 or 32 big-endian bytes) in its place."""
     if challenge is None:
-        return None if seed is None else bytes(seed)
+        if seed is None:
+            return None
+        sd = bytes(seed)
+        if len(sd) != 32:
+            raise ValueError("seed must be 32 bytes, got %d" % len(sd))
+        return sd
     if seed is not None:
         raise ValueError("pass either seed or challenge")
-    return int(challenge).to_bytes(32, "big") if isinstance(challenge, int) else bytes(challenge)
+    if isinstance(challenge, int):
+        if not 0 <= challenge < (1 << 256):
+            raise ValueError("challenge must be in [0, 2^256)")
+        return challenge.to_bytes(32, "big")
+    sd = bytes(challenge)
+    if len(sd) != 32:
+        raise ValueError("challenge must be 32 bytes, got %d" % len(sd))
+    return sd
 
 
 def _check(rc: int):
@@ -177,10 +200,18 @@ def _host_bytes(x) -> bytes:
     raise TypeError("unsupported buffer type %r" % type(x))
 
 
-def _dptr(x) -> int:
+def _dptr(x, nbytes: Optional[int] = None) -> int:
+    """Device pointer of a contiguous tensor holding at least `nbytes` bytes."""
     if not x.is_contiguous():
         raise ValueError("device tensors must be contiguous")
+    if nbytes is not None and x.numel() * x.element_size() < nbytes:
+        raise ValueError("device tensor holds %d bytes, the call reads %d" % (x.numel() * x.element_size(), nbytes))
     return x.data_ptr()
+
+
+def _current_stream(device: int):
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
 
 
 @dataclass
@@ -216,14 +247,33 @@ class CommitKey:
 
 
 class Context:
-    """One GPU (device_id) with `slots` independent workspaces/streams."""
+    """One GPU (device_id) with `slots` independent workspaces/streams; or, with
+    devices=[d0, d1, ...], one context over several GPUs (kzgmi_ctx_create_multi: host-buffer
+    batch_verify / msm_g1 are sharded over them; d0 is the primary device).
 
-    def __init__(self, device: int = 0, slots: int = 1):
+    Device-tensor arguments are read on the library's own streams: every call first orders
+    the slot's stream after torch's current stream (kzgmi_stream_wait), so tensors written by
+    torch just before the call are seen complete."""
+
+    def __init__(self, device: int = 0, slots: int = 1, devices=None):
         h = ctypes.c_void_p()
-        _check(lib().kzgmi_ctx_create(ctypes.byref(h), int(device), int(slots)))
+        if devices is not None:
+            devs = [int(d) for d in devices]
+            arr = (ctypes.c_int * len(devs))(*devs)
+            _check(lib().kzgmi_ctx_create_multi(ctypes.byref(h), arr, len(devs), int(slots)))
+            device = devs[0]
+        else:
+            _check(lib().kzgmi_ctx_create(ctypes.byref(h), int(device), int(slots)))
         self.handle = h
         self.device = device
         self.slots = slots
+
+    def num_devices(self) -> int:
+        return int(lib().kzgmi_ctx_num_devices(self.handle))
+
+    def _order(self, slot: int = 0):
+        """Order `slot`'s stream after torch's current stream (device inputs written by torch)."""
+        _check(lib().kzgmi_stream_wait(self.handle, int(slot), _current_stream(self.device)))
 
     def close(self):
         if getattr(self, "handle", None):
@@ -237,9 +287,11 @@ class Context:
             pass
 
     # ------------------------------------------------------------------ SRS
-    def load_srs(self, curve: str, g2: bytes, tau_g2: bytes) -> Srs:
+    def load_srs(self, curve: str, g2: bytes, tau_g2: bytes, g1: Optional[bytes] = None) -> Srs:
+        """srs = {G1, [1]_2, [tau]_2}; g1 None = the standard generator."""
         h = ctypes.c_void_p()
-        _check(lib().kzgmi_srs_load(self.handle, CURVES[curve], bytes(g2), bytes(tau_g2), ctypes.byref(h)))
+        _check(lib().kzgmi_srs_load(self.handle, CURVES[curve], None if g1 is None else bytes(g1), bytes(g2),
+                                    bytes(tau_g2), ctypes.byref(h)))
         return Srs(self, curve, h)
 
     # ------------------------------------------------------------------ batch verify
@@ -260,12 +312,12 @@ class Context:
         if _is_device_tensor(commitments):
             if n is None:
                 n = commitments.numel() // g1b
+            ptrs = (_dptr(commitments, n * g1b), _dptr(zs, 32 * n), _dptr(ys, 32 * n), _dptr(proofs, n * g1b))
+            self._order(0)
             if flags:
-                _check(lib().kzgmi_batch_verify_device_ex_async(self.handle, srs.handle, 0, _dptr(commitments),
-                                                                _dptr(zs), _dptr(ys), _dptr(proofs), n, sd, flags))
+                _check(lib().kzgmi_batch_verify_device_ex_async(self.handle, srs.handle, 0, *ptrs, n, sd, flags))
                 return self.wait(0)
-            _check(lib().kzgmi_batch_verify_device(self.handle, srs.handle, _dptr(commitments), _dptr(zs),
-                                                   _dptr(ys), _dptr(proofs), n, sd, ctypes.byref(ok)))
+            _check(lib().kzgmi_batch_verify_device(self.handle, srs.handle, *ptrs, n, sd, ctypes.byref(ok)))
         else:
             cb, zb, yb, pb = (_host_bytes(v) for v in (commitments, zs, ys, proofs))
             if n is None:
@@ -279,11 +331,60 @@ class Context:
     def batch_verify_async(self, srs: Srs, slot: int, commitments, zs, ys, proofs, n: int,
                            seed: Optional[bytes] = None, compressed: bool = False, subgroup_check: bool = False,
                            fiat_shamir: bool = False, challenge=None, trusted_g1: bool = False):
-        _check(lib().kzgmi_batch_verify_device_ex_async(self.handle, srs.handle, int(slot), _dptr(commitments),
-                                                        _dptr(zs), _dptr(ys), _dptr(proofs), n,
-                                                        _challenge_seed(seed, challenge),
+        g1b = (1 if compressed else 2) * FP_BYTES[srs.curve]
+        ptrs = (_dptr(commitments, n * g1b), _dptr(zs, 32 * n), _dptr(ys, 32 * n), _dptr(proofs, n * g1b))
+        sd = _challenge_seed(seed, challenge)
+        self._order(slot)
+        _check(lib().kzgmi_batch_verify_device_ex_async(self.handle, srs.handle, int(slot), *ptrs, n, sd,
                                                         _flags(compressed, subgroup_check, fiat_shamir, challenge,
                                                                trusted_g1)))
+
+    def batch_verify_multi(self, srs: Srs, shards, seed: Optional[bytes] = None, compressed: bool = False,
+                           subgroup_check: bool = False, fiat_shamir: bool = False, challenge=None,
+                           trusted_g1: bool = False) -> bool:
+        """Multi-device context: shards[d] = (commitments, zs, ys, proofs[, n]) device tensors on
+        device d of the context's list (global tuple order = shard order)."""
+        g1b = (1 if compressed else 2) * FP_BYTES[srs.curve]
+        D = len(shards)
+        if D != self.num_devices():
+            raise ValueError("need one shard per device (%d), got %d" % (self.num_devices(), D))
+        cols = [[], [], [], []]
+        ns = []
+        for sh in shards:
+            C, z, y, P = sh[:4]
+            n = sh[4] if len(sh) > 4 else C.numel() // g1b
+            ns.append(n)
+            for i, (t, nb) in enumerate(((C, n * g1b), (z, 32 * n), (y, 32 * n), (P, n * g1b))):
+                cols[i].append(_dptr(t, nb) if n else None)
+        import torch
+        for sh in shards:  # inputs written by torch on each device's current stream
+            torch.cuda.current_stream(sh[0].device).synchronize()
+        arr = [(ctypes.c_void_p * D)(*c) for c in cols]
+        nn = (ctypes.c_size_t * D)(*ns)
+        ok = ctypes.c_int(-1)
+        _check(lib().kzgmi_batch_verify_multi_device(self.handle, srs.handle, *arr, nn, _challenge_seed(seed, challenge),
+                                                     _flags(compressed, subgroup_check, fiat_shamir, challenge,
+                                                            trusted_g1), ctypes.byref(ok)))
+        return bool(ok.value)
+
+    def msm_g1_multi(self, curve: str, shards) -> bytes:
+        """Multi-device context: shards[d] = (points, scalars[, n]) device tensors on device d."""
+        g1b = 2 * FP_BYTES[curve]
+        D = len(shards)
+        if D != self.num_devices():
+            raise ValueError("need one shard per device (%d), got %d" % (self.num_devices(), D))
+        pp, ss, ns = [], [], []
+        import torch
+        for sh in shards:
+            n = sh[2] if len(sh) > 2 else sh[0].numel() // g1b
+            ns.append(n)
+            pp.append(_dptr(sh[0], n * g1b) if n else None)
+            ss.append(_dptr(sh[1], 32 * n) if n else None)
+            torch.cuda.current_stream(sh[0].device).synchronize()
+        out = ctypes.create_string_buffer(g1b)
+        _check(lib().kzgmi_msm_g1_multi_device(self.handle, CURVES[curve], (ctypes.c_void_p * D)(*pp),
+                                               (ctypes.c_void_p * D)(*ss), (ctypes.c_size_t * D)(*ns), out))
+        return out.raw
 
     # ------------------------------------------------------------------ prover commit
     def load_commit_key(self, curve: str, g1_powers: bytes, n: Optional[int] = None) -> CommitKey:
@@ -303,7 +404,9 @@ class Context:
         if _is_device_tensor(coeffs):
             if m is None:
                 m = coeffs.numel() // 32
-            _check(lib().kzgmi_commit_device(self.handle, ck.handle, _dptr(coeffs), m, out))
+            p = _dptr(coeffs, 32 * m)
+            self._order(0)
+            _check(lib().kzgmi_commit_device(self.handle, ck.handle, p, m, out))
         else:
             cb = _host_bytes(coeffs)
             if m is None:
@@ -317,36 +420,48 @@ class Context:
         msm_wait(slot) returns it."""
         self._msm_curve = getattr(self, "_msm_curve", {})
         self._msm_curve[slot] = ck.curve
-        _check(lib().kzgmi_commit_device_async(self.handle, ck.handle, int(slot), _dptr(coeffs), int(m)))
+        p = _dptr(coeffs, 32 * m)
+        self._order(slot)
+        _check(lib().kzgmi_commit_device_async(self.handle, ck.handle, int(slot), p, int(m)))
 
     def fs_challenge(self, curve: str, commitments, zs, ys, proofs, n: int, compressed: bool = False) -> int:
         """r of KZGMI_FLAG_FIAT_SHAMIR for device-resident inputs."""
         out = ctypes.create_string_buffer(32)
-        _check(lib().kzgmi_fs_challenge_device(self.handle, CURVES[curve], _dptr(commitments), _dptr(zs), _dptr(ys),
-                                               _dptr(proofs), n, _flags(compressed), out))
+        g1b = (1 if compressed else 2) * FP_BYTES[curve]
+        ptrs = (_dptr(commitments, n * g1b), _dptr(zs, 32 * n), _dptr(ys, 32 * n), _dptr(proofs, n * g1b))
+        self._order(0)
+        _check(lib().kzgmi_fs_challenge_device(self.handle, CURVES[curve], *ptrs, n, _flags(compressed), out))
         return int.from_bytes(out.raw, "big")
 
     def fs_chunk_digests(self, curve: str, commitments, zs, ys, proofs, n: int, index_offset: int, out,
                          compressed: bool = False):
         """Shard's 4096-leaf subtree roots (ceil(n / 4096) x 32 B) into device tensor `out`."""
-        _check(lib().kzgmi_fs_chunk_digests_device(self.handle, CURVES[curve], _dptr(commitments), _dptr(zs),
-                                                   _dptr(ys), _dptr(proofs), n, int(index_offset),
-                                                   _flags(compressed), _dptr(out)))
+        g1b = (1 if compressed else 2) * FP_BYTES[curve]
+        ptrs = (_dptr(commitments, n * g1b), _dptr(zs, 32 * n), _dptr(ys, 32 * n), _dptr(proofs, n * g1b))
+        po = _dptr(out, 32 * ((n + FS_CHUNK - 1) // FS_CHUNK))
+        self._order(0)
+        _check(lib().kzgmi_fs_chunk_digests_device(self.handle, CURVES[curve], *ptrs, n, int(index_offset),
+                                                   _flags(compressed), po))
 
     def fs_challenge_from_digests(self, curve: str, digests, nchunks: int, n_total: int) -> int:
         out = ctypes.create_string_buffer(32)
-        _check(lib().kzgmi_fs_challenge_from_digests_device(self.handle, CURVES[curve], _dptr(digests), nchunks,
+        p = _dptr(digests, 32 * nchunks)
+        self._order(0)
+        _check(lib().kzgmi_fs_challenge_from_digests_device(self.handle, CURVES[curve], p, nchunks,
                                                             int(n_total), out))
         return int.from_bytes(out.raw, "big")
 
     def g1_validate(self, curve: str, points, n: int, compressed: bool = False, subgroup_check: bool = False):
         """Raise KzgmiError unless all n device-resident G1 encodings are valid."""
-        _check(lib().kzgmi_g1_validate_device(self.handle, CURVES[curve], _dptr(points), n,
-                                              _flags(compressed, subgroup_check)))
+        p = _dptr(points, n * (1 if compressed else 2) * FP_BYTES[curve])
+        self._order(0)
+        _check(lib().kzgmi_g1_validate_device(self.handle, CURVES[curve], p, n, _flags(compressed, subgroup_check)))
 
     def g1_compress(self, curve: str, points, n: int, out):
         """Device utility: uncompressed G1 encodings -> compressed (no validation)."""
-        _check(lib().kzgmi_g1_compress_device(self.handle, CURVES[curve], _dptr(points), n, _dptr(out)))
+        pi, po = _dptr(points, 2 * n * FP_BYTES[curve]), _dptr(out, n * FP_BYTES[curve])
+        self._order(0)
+        _check(lib().kzgmi_g1_compress_device(self.handle, CURVES[curve], pi, n, po))
 
     def wait(self, slot: int) -> bool:
         ok = ctypes.c_int(-1)
@@ -367,7 +482,9 @@ class Context:
         if _is_device_tensor(points):
             if n is None:
                 n = points.numel() // g1b
-            _check(lib().kzgmi_msm_g1_device(self.handle, CURVES[curve], _dptr(points), _dptr(scalars), n, out))
+            pp, ps = _dptr(points, n * g1b), _dptr(scalars, 32 * n)
+            self._order(0)
+            _check(lib().kzgmi_msm_g1_device(self.handle, CURVES[curve], pp, ps, n, out))
         else:
             pb, sb = _host_bytes(points), _host_bytes(scalars)
             if n is None:
@@ -379,8 +496,9 @@ class Context:
         """Enqueue sum k_i P_i (device tensors) on workspace `slot`; msm_wait(slot) returns it."""
         self._msm_curve = getattr(self, "_msm_curve", {})
         self._msm_curve[slot] = curve
-        _check(lib().kzgmi_msm_g1_device_async(self.handle, CURVES[curve], int(slot), _dptr(points),
-                                               _dptr(scalars), int(n)))
+        pp, ps = _dptr(points, n * 2 * FP_BYTES[curve]), _dptr(scalars, 32 * n)
+        self._order(slot)
+        _check(lib().kzgmi_msm_g1_device_async(self.handle, CURVES[curve], int(slot), pp, ps, int(n)))
 
     def msm_wait(self, slot: int) -> bytes:
         g1b = 2 * FP_BYTES[self._msm_curve[slot]]
@@ -396,50 +514,76 @@ class Context:
     def partial_bytes(self, curve: str) -> int:
         return int(lib().kzgmi_partial_bytes(CURVES[curve]))
 
+    def _batch_ptrs(self, curve, commitments, zs, ys, proofs, n, compressed=False):
+        g1b = (1 if compressed else 2) * FP_BYTES[curve]
+        return (_dptr(commitments, n * g1b), _dptr(zs, 32 * n), _dptr(ys, 32 * n), _dptr(proofs, n * g1b))
+
     def batch_partial(self, srs: Srs, commitments, zs, ys, proofs, n: int, index_offset: int, seed: bytes, out):
-        _check(lib().kzgmi_batch_partial_device(self.handle, srs.handle, _dptr(commitments), _dptr(zs), _dptr(ys),
-                                                _dptr(proofs), n, int(index_offset), bytes(seed), _dptr(out)))
+        ptrs = self._batch_ptrs(srs.curve, commitments, zs, ys, proofs, n)
+        po = _dptr(out, 2 * self.partial_bytes(srs.curve))
+        sd = _challenge_seed(seed, None)
+        self._order(0)
+        _check(lib().kzgmi_batch_partial_device(self.handle, srs.handle, *ptrs, n, int(index_offset), sd, po))
 
     def batch_combine(self, srs: Srs, partials, n_parts: int) -> bool:
         ok = ctypes.c_int(-1)
-        _check(lib().kzgmi_batch_combine_device(self.handle, srs.handle, _dptr(partials), int(n_parts),
-                                                ctypes.byref(ok)))
+        p = _dptr(partials, 2 * n_parts * self.partial_bytes(srs.curve))
+        self._order(0)
+        _check(lib().kzgmi_batch_combine_device(self.handle, srs.handle, p, int(n_parts), ctypes.byref(ok)))
         return bool(ok.value)
+
+    def partial_encode(self, curve: str, records, count: int) -> list:
+        """G1 encodings of `count` device-resident partial records (e.g. a shard's [A_k, B_k])."""
+        g1b = 2 * FP_BYTES[curve]
+        p = _dptr(records, count * self.partial_bytes(curve))
+        out = ctypes.create_string_buffer(count * g1b)
+        self._order(0)
+        _check(lib().kzgmi_partial_encode_device(self.handle, CURVES[curve], p, int(count), out))
+        return [out.raw[i * g1b:(i + 1) * g1b] for i in range(count)]
 
     def batch_partial_async(self, srs: Srs, slot: int, commitments, zs, ys, proofs, n: int, index_offset: int,
                             seed, out, compressed: bool = False, subgroup_check: bool = False, challenge=None,
                             trusted_g1: bool = False):
         """Enqueue this shard's partial (A_k, B_k) on `slot`; complete with wait(slot).
         challenge: r_i = r^(index_offset + i) (pass seed=None)."""
-        _check(lib().kzgmi_batch_partial_device_async(self.handle, srs.handle, int(slot), _dptr(commitments),
-                                                      _dptr(zs), _dptr(ys), _dptr(proofs), n, int(index_offset),
-                                                      _challenge_seed(seed, challenge),
-                                                      _flags(compressed, subgroup_check, False, challenge,
-                                                             trusted_g1),
-                                                      _dptr(out)))
+        ptrs = self._batch_ptrs(srs.curve, commitments, zs, ys, proofs, n, compressed)
+        po = _dptr(out, 2 * self.partial_bytes(srs.curve))
+        sd = _challenge_seed(seed, challenge)
+        self._order(slot)
+        _check(lib().kzgmi_batch_partial_device_async(self.handle, srs.handle, int(slot), *ptrs, n, int(index_offset),
+                                                      sd, _flags(compressed, subgroup_check, False, challenge,
+                                                                 trusted_g1), po))
 
     def batch_combine_async(self, srs: Srs, slot: int, partials, n_parts: int):
         """Enqueue sum-of-partials + pairing check on `slot`; wait(slot) returns the verdict."""
-        _check(lib().kzgmi_batch_combine_device_async(self.handle, srs.handle, int(slot), _dptr(partials),
-                                                      int(n_parts)))
+        p = _dptr(partials, 2 * n_parts * self.partial_bytes(srs.curve))
+        self._order(slot)
+        _check(lib().kzgmi_batch_combine_device_async(self.handle, srs.handle, int(slot), p, int(n_parts)))
 
     def msm_partial(self, curve: str, points, scalars, n: int, out):
-        _check(lib().kzgmi_msm_partial_device(self.handle, CURVES[curve], _dptr(points), _dptr(scalars), n,
-                                              _dptr(out)))
+        pp, ps = _dptr(points, n * 2 * FP_BYTES[curve]), _dptr(scalars, 32 * n)
+        po = _dptr(out, self.partial_bytes(curve))
+        self._order(0)
+        _check(lib().kzgmi_msm_partial_device(self.handle, CURVES[curve], pp, ps, n, po))
 
     def msm_partial_async(self, curve: str, slot: int, points, scalars, n: int, out):
-        _check(lib().kzgmi_msm_partial_device_async(self.handle, CURVES[curve], int(slot), _dptr(points),
-                                                    _dptr(scalars), int(n), _dptr(out)))
+        pp, ps = _dptr(points, n * 2 * FP_BYTES[curve]), _dptr(scalars, 32 * n)
+        po = _dptr(out, self.partial_bytes(curve))
+        self._order(slot)
+        _check(lib().kzgmi_msm_partial_device_async(self.handle, CURVES[curve], int(slot), pp, ps, int(n), po))
 
     def msm_combine_async(self, curve: str, slot: int, partials, n_parts: int):
         self._msm_curve = getattr(self, "_msm_curve", {})
         self._msm_curve[slot] = curve
-        _check(lib().kzgmi_msm_combine_device_async(self.handle, CURVES[curve], int(slot), _dptr(partials),
-                                                    int(n_parts)))
+        p = _dptr(partials, n_parts * self.partial_bytes(curve))
+        self._order(slot)
+        _check(lib().kzgmi_msm_combine_device_async(self.handle, CURVES[curve], int(slot), p, int(n_parts)))
 
     def msm_combine(self, curve: str, partials, n_parts: int) -> bytes:
         out = ctypes.create_string_buffer(2 * FP_BYTES[curve])
-        _check(lib().kzgmi_msm_combine_device(self.handle, CURVES[curve], _dptr(partials), int(n_parts), out))
+        p = _dptr(partials, n_parts * self.partial_bytes(curve))
+        self._order(0)
+        _check(lib().kzgmi_msm_combine_device(self.handle, CURVES[curve], p, int(n_parts), out))
         return out.raw
 
     # ------------------------------------------------------------------ utilities
@@ -449,11 +593,15 @@ class Context:
         return out.raw
 
     def gen_g1(self, curve: str, scalars_dev, n: int, out_dev):
-        _check(lib().kzgmi_gen_g1(self.handle, CURVES[curve], _dptr(scalars_dev), n, _dptr(out_dev)))
+        ps, po = _dptr(scalars_dev, 32 * n), _dptr(out_dev, n * 2 * FP_BYTES[curve])
+        self._order(0)
+        _check(lib().kzgmi_gen_g1(self.handle, CURVES[curve], ps, n, po))
 
     def gen_tuples(self, curve: str, tau: int, seed: bytes, n: int, C, z, y, pi):
-        _check(lib().kzgmi_gen_tuples(self.handle, CURVES[curve], int(tau).to_bytes(32, "big"), bytes(seed), n,
-                                      _dptr(C), _dptr(z), _dptr(y), _dptr(pi)))
+        ptrs = self._batch_ptrs(curve, C, z, y, pi, n)
+        sd = _challenge_seed(seed, None)
+        self._order(0)
+        _check(lib().kzgmi_gen_tuples(self.handle, CURVES[curve], int(tau).to_bytes(32, "big"), sd, n, *ptrs))
 
     def g2_mul(self, curve: str, g2: bytes, k: int) -> bytes:
         out = ctypes.create_string_buffer(4 * FP_BYTES[curve])
@@ -512,8 +660,8 @@ def default_context() -> Context:
     return _default_ctx
 
 
-def load_srs(curve: str, g2: bytes, tau_g2: bytes, ctx: Optional[Context] = None) -> Srs:
-    return (ctx or default_context()).load_srs(curve, g2, tau_g2)
+def load_srs(curve: str, g2: bytes, tau_g2: bytes, ctx: Optional[Context] = None, g1: Optional[bytes] = None) -> Srs:
+    return (ctx or default_context()).load_srs(curve, g2, tau_g2, g1=g1)
 
 
 def batch_verify(commitments, zs, ys, proofs, srs: Srs, seed: Optional[bytes] = None, compressed: bool = False,

@@ -17,6 +17,13 @@ at the single-GPU pipelined rate plus one small all-gather per batch.
 
 `backend` is anything with the methods used below (a `kzgmi.Context` on the GPU; the
 CPU tests substitute a double built on the oracle to exercise this orchestration with gloo).
+
+Stream order: the collectives run on torch's streams, kzgmi on its own.  Every
+`kzgmi.Context` method that reads a device tensor first orders its slot's stream after
+torch's current stream (kzgmi_stream_wait), and every kzgmi output read here (partial
+records, subtree roots) is complete when the call or its wait() returns -- so gathered
+buffers are never read before the all-gather has written them, whatever buffer the caching
+allocator hands out.
 """
 from __future__ import annotations
 
@@ -128,16 +135,15 @@ class ShardedPipeline:
             self.lane_pending[lane] = False
 
     def _gather_and_combine(self, s: int, out):
-        import torch
         import torch.distributed as dist
         self.backend.wait(s)                                   # shard partial ready (errors raise here)
         self.pending[s] = False
         lane = self.j % self.lanes
         self.j += 1
         self._collect_lane(lane, out)                          # verdict of the batch `lanes` combines ago
+        # the combine lane's stream is ordered after torch's current stream (which waits for the
+        # collective) inside batch_combine_async (kzgmi_stream_wait): no host sync
         dist.all_gather_into_tensor(self.gathered[lane], self.local[s], group=self.group)
-        if str(self.dev).startswith("cuda"):
-            torch.cuda.current_stream().synchronize()          # gathered records visible to the lane stream
         self.backend.batch_combine_async(self.srs, self.slots + lane, self.gathered[lane], self.world)
         self.lane_pending[lane] = True
 
@@ -206,7 +212,6 @@ class ShardedMsmPipeline:
             self.lane_pending[lane] = False
 
     def _gather_and_combine(self, s: int, out):
-        import torch
         import torch.distributed as dist
         self.backend.wait(s)
         self.pending[s] = False
@@ -214,8 +219,6 @@ class ShardedMsmPipeline:
         self.j += 1
         self._collect_lane(lane, out)
         dist.all_gather_into_tensor(self.gathered[lane], self.local[s], group=self.group)
-        if str(self.dev).startswith("cuda"):
-            torch.cuda.current_stream().synchronize()
         self.backend.msm_combine_async(self.curve, self.slots + lane, self.gathered[lane], self.world)
         self.lane_pending[lane] = True
 

@@ -419,11 +419,17 @@ static void C_(pairing_check)(const C_(aff)* A, const C_(aff)* B, const C_(aff2)
 static int C_(batch_verify)(const uint8_t* cm, const uint8_t* zs, const uint8_t* ys, const uint8_t* pf,
                             size_t n, const uint8_t* g2b, const uint8_t* tg2b, const uint8_t* seed,
                             int* ok, uint8_t* a_out, uint8_t* b_out, uint64_t offset, int do_pairing,
-                            const uint8_t* pow_r) {
+                            const uint8_t* pow_r, const uint8_t* g1b) {
   C_(aff2) g2, tg2;
+  C_(aff) g1;
   int e;
   if ((e = C_(g2_decode)(&g2, g2b))) return e;
   if ((e = C_(g2_decode)(&tg2, tg2b))) return e;
+  if (g1b) {  /* the SRS's [1]_1 (SURVEY.md 8b srs = {G1, [1]_2, [tau]_2}); NULL = the standard generator */
+    if ((e = C_(g1_decode)(&g1, g1b))) return e;
+  } else {
+    C_(generator)(&g1);
+  }
   if (n == 0) {
     *ok = 1;
     C_(aff) inf; memset(&inf, 0, sizeof(inf)); inf.inf = 1;
@@ -480,7 +486,7 @@ static int C_(batch_verify)(const uint8_t* cm, const uint8_t* zs, const uint8_t*
     FR_(add)(&tsum, &tsum, &tloc);
   }
   if (err) { free(pts); free(sc); return err; }
-  C_(generator)(&pts[2 * n]);
+  pts[2 * n] = g1;
   FR nt; FR_(neg)(&nt, &tsum); FR_(from_mont)(sc + 4 * (2 * n), &nt);
   /* A = sum r_i pi_i ; B = sum r_i C_i + s_i pi_i - t G */
   uint64_t* sa = (uint64_t*)malloc(n * 4 * sizeof(uint64_t));

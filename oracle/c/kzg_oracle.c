@@ -256,8 +256,8 @@ int kzgo_batch_verify(int curve, const uint8_t* cm, const uint8_t* zs, const uin
                       size_t n, const uint8_t* g2, const uint8_t* tau_g2, const uint8_t* seed, int* ok,
                       uint8_t* a_out, uint8_t* b_out) {
   if (!ok || !seed || !g2 || !tau_g2 || (n && (!cm || !zs || !ys || !pf))) return KZGO_ERR_ARG;
-  return CURVE_DISPATCH(curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, 1, NULL),
-                        bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, 1, NULL));
+  return CURVE_DISPATCH(curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, 1, NULL, NULL),
+                        bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, 1, NULL, NULL));
 }
 
 /* Powers mode (Fiat-Shamir / caller-supplied challenge): r_i = r^(offset + i), r = int_be(r32) < r.
@@ -267,8 +267,8 @@ int kzgo_batch_verify_powers(int curve, const uint8_t* cm, const uint8_t* zs, co
                              int do_pairing, int* ok, uint8_t* a_out, uint8_t* b_out) {
   if (!ok || !r32 || !g2 || !tau_g2 || (n && (!cm || !zs || !ys || !pf))) return KZGO_ERR_ARG;
   return CURVE_DISPATCH(
-      curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, NULL, ok, a_out, b_out, offset, do_pairing, r32),
-      bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, NULL, ok, a_out, b_out, offset, do_pairing, r32));
+      curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, NULL, ok, a_out, b_out, offset, do_pairing, r32, NULL),
+      bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, NULL, ok, a_out, b_out, offset, do_pairing, r32, NULL));
 }
 
 /* A, B of tuples [offset, offset+n) of a global batch (no pairing): the shard partials */
@@ -277,8 +277,50 @@ int kzgo_batch_combination(int curve, const uint8_t* cm, const uint8_t* zs, cons
                            uint8_t* a_out, uint8_t* b_out) {
   int ok = -1;
   if (!seed || !g2 || !tau_g2 || !a_out || !b_out || (n && (!cm || !zs || !ys || !pf))) return KZGO_ERR_ARG;
-  return CURVE_DISPATCH(curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, &ok, a_out, b_out, offset, 0, NULL),
-                        bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, &ok, a_out, b_out, offset, 0, NULL));
+  return CURVE_DISPATCH(curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, &ok, a_out, b_out, offset, 0, NULL, NULL),
+                        bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, &ok, a_out, b_out, offset, 0, NULL, NULL));
+}
+
+/* Batch verification / shard partials against an SRS whose G1 element is g1 (NULL = the
+ * standard generator): the -t [1]_1 term uses it.  do_pairing = 0 gives A, B only. */
+int kzgo_batch_verify_g1(int curve, const uint8_t* cm, const uint8_t* zs, const uint8_t* ys, const uint8_t* pf,
+                         size_t n, uint64_t offset, const uint8_t* g1, const uint8_t* g2, const uint8_t* tau_g2,
+                         const uint8_t* seed, int do_pairing, int* ok, uint8_t* a_out, uint8_t* b_out) {
+  if (!ok || !seed || !g2 || !tau_g2 || (n && (!cm || !zs || !ys || !pf))) return KZGO_ERR_ARG;
+  return CURVE_DISPATCH(
+      curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, offset, do_pairing, NULL, g1),
+      bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, offset, do_pairing, NULL, g1));
+}
+
+/* sum_i a_i b_i mod r for canonical big-endian Fr values (the discrete-log side of the MSM
+ * identity sum_i b_i [a_i] G = [sum_i a_i b_i] G).  Non-canonical input -> error. */
+#define DEF_FRDOT(C, FRT)                                                                      \
+  static int C##_fr_dot_api(const uint8_t* a, const uint8_t* b, size_t n, uint8_t* out) {      \
+    FRT acc; FRT##_zero(&acc);                                                                 \
+    int err = 0;                                                                               \
+    _Pragma("omp parallel num_threads(kzgo_threads())")                                        \
+    {                                                                                          \
+      FRT loc; FRT##_zero(&loc);                                                               \
+      _Pragma("omp for schedule(static)")                                                      \
+      for (size_t i = 0; i < n; ++i) {                                                         \
+        uint64_t x[4], y[4];                                                                   \
+        FRT##_raw_from_be(x, a + 32 * i, 32); FRT##_raw_from_be(y, b + 32 * i, 32);            \
+        if (FRT##_geq_mod(x) || FRT##_geq_mod(y)) { err = KZGO_ERR_SCALAR; continue; }        \
+        FRT xm, ym, p; FRT##_to_mont(&xm, x); FRT##_to_mont(&ym, y);                           \
+        FRT##_mul(&p, &xm, &ym); FRT##_add(&loc, &loc, &p);                                    \
+      }                                                                                        \
+      _Pragma("omp critical")                                                                  \
+      FRT##_add(&acc, &acc, &loc);                                                             \
+    }                                                                                          \
+    uint64_t raw[4]; FRT##_from_mont(raw, &acc); FRT##_raw_to_be(out, raw, 32);                \
+    return err;                                                                                \
+  }
+DEF_FRDOT(bls, fr_bls)
+DEF_FRDOT(bn, fr_bn)
+
+int kzgo_fr_dot(int curve, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* out) {
+  if (!out || (n && (!a || !b))) return KZGO_ERR_ARG;
+  return CURVE_DISPATCH(curve, bls_fr_dot_api(a, b, n, out), bn_fr_dot_api(a, b, n, out));
 }
 
 int kzgo_pairing_check(int curve, const uint8_t* a, const uint8_t* b, const uint8_t* g2, const uint8_t* tau_g2, int* ok) {

@@ -47,6 +47,10 @@ def lib():
         L.kzgo_g2_mul.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p]
         L.kzgo_randomizer_bytes.argtypes = [c.c_char_p, c.c_uint64, c.c_char_p]
         L.kzgo_sha256.argtypes = [c.c_char_p, c.c_char_p, c.c_size_t]
+        L.kzgo_batch_verify_g1.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p, c.c_size_t,
+                                           c.c_uint64, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p, c.c_int,
+                                           c.POINTER(c.c_int), c.c_char_p, c.c_char_p]
+        L.kzgo_fr_dot.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_size_t, c.c_char_p]
         L.kzgo_set_threads.argtypes = [c.c_int]
         L.kzgo_get_threads.restype = c.c_int
         _lib = L
@@ -93,6 +97,26 @@ def batch_combination(curve, commitments, zs, ys, proofs, n, offset, g2, tau_g2,
     _check(lib().kzgo_batch_combination(CURVE_IDS[curve], commitments, zs, ys, proofs, n, offset, g2, tau_g2,
                                         seed, a, b))
     return a.raw, b.raw
+
+
+def batch_verify_g1(curve, commitments, zs, ys, proofs, n, g1, g2, tau_g2, seed, offset=0, pairing=True):
+    """Batch check against an SRS whose G1 element is `g1` (None = the standard generator).
+    Returns (ok or None, A, B); pairing=False gives the shard partials of [offset, offset + n)."""
+    g1b = 2 * FP_BYTES[curve]
+    ok = ctypes.c_int(-1)
+    a = ctypes.create_string_buffer(g1b)
+    b = ctypes.create_string_buffer(g1b)
+    _check(lib().kzgo_batch_verify_g1(CURVE_IDS[curve], commitments, zs, ys, proofs, n, offset, g1, g2, tau_g2, seed,
+                                      1 if pairing else 0, ctypes.byref(ok), a, b))
+    return (bool(ok.value) if pairing else None), a.raw, b.raw
+
+
+def fr_dot(curve, a: bytes, b: bytes, n: int) -> int:
+    """sum_i a_i b_i mod r (32-B big-endian canonical Fr values): with points a_i G1 and
+    scalars b_i, [fr_dot] G1 is the MSM (SURVEY.md 4.3 discrete-log identity)."""
+    out = ctypes.create_string_buffer(32)
+    _check(lib().kzgo_fr_dot(CURVE_IDS[curve], a, b, n, out))
+    return int.from_bytes(out.raw, "big")
 
 
 def pairing_check(curve, A: bytes, B: bytes, g2: bytes, tau_g2: bytes) -> bool:

@@ -1,0 +1,73 @@
+"""One rank of tests/test_gpu_boundary.py::test_two_rank_gloo_pipeline_on_gpu.
+
+Both ranks run on the box's one GPU and talk over gloo (RCCL refuses two ranks per device).
+Every rank generates the same global batch, verifies its half through the real HIP
+kzgmi.distributed.ShardedPipeline and checks, against the C oracle (test infrastructure):
+its own shard partial (A_k, B_k), the combined (A, B) of the one-shot sharded path, and the
+pipeline's verdicts in submission order.  Prints "RANK OK" on success.
+"""
+import hashlib
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "kzg-batch-verification-scheme_amd")):
+    sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import kzgmi  # noqa: E402
+from kzgmi.distributed import ShardedPipeline, shard_range, sharded_batch_verify  # noqa: E402
+from oracle import oracle as O  # noqa: E402  (checker only)
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    curve, n_total, tau = "bls12_381", 3001, 0x5EED
+    g1b = 96
+    ctx = kzgmi.Context(0, 3)  # 2 shard slots + 1 combine lane
+    Cm = torch.empty(n_total * g1b, dtype=torch.uint8, device="cuda")
+    P = torch.empty(n_total * g1b, dtype=torch.uint8, device="cuda")
+    z = torch.empty(n_total * 32, dtype=torch.uint8, device="cuda")
+    y = torch.empty(n_total * 32, dtype=torch.uint8, device="cuda")
+    ctx.gen_tuples(curve, tau, hashlib.sha256(b"gloo2").digest(), n_total, Cm, z, y, P)
+    g2 = kzgmi.G2_GENERATOR[curve]
+    tg2 = O.g2_mul(curve, g2, tau)
+    srs = ctx.load_srs(curve, g2, tg2)
+    seed = hashlib.sha256(b"gloo2-verify").digest()
+    off, n = shard_range(n_total, world, rank)
+    sl = lambda t, w: t[off * w:(off + n) * w]  # noqa: E731
+    Cs, zs, ys, Ps = sl(Cm, g1b), sl(z, 32), sl(y, 32), sl(P, g1b)
+    host = [t.cpu().numpy().tobytes() for t in (Cm, z, y, P)]
+    hs = [b[off * w:(off + n) * w] for b, w in zip(host, (g1b, 32, 32, g1b))]
+
+    # this rank's partial vs the oracle's combination of the same global index range
+    rec = torch.empty(2 * ctx.partial_bytes(curve), dtype=torch.uint8, device="cuda")
+    ctx.batch_partial(srs, Cs, zs, ys, Ps, n, off, seed, rec)
+    assert tuple(ctx.partial_encode(curve, rec, 2)) == O.batch_combination(curve, *hs, n, off, g2, tg2, seed), rank
+
+    # one-shot sharded check: combined A, B vs the oracle's unsharded batch
+    assert sharded_batch_verify(ctx, srs, Cs, zs, ys, Ps, n, off, seed) is True
+    ok, Ao, Bo = O.batch_verify(curve, *host, n_total, g2, tg2, seed, want_ab=True)
+    assert ok is True and ctx.last_combination(curve) == (Ao, Bo), rank
+
+    # pipelined: batches 1 and 3 carry a corrupted y on rank 1's shard only
+    ybad = ys.clone()
+    if rank == 1:
+        ybad[32 * (n - 1) + 31] ^= 1
+    pipe = ShardedPipeline(ctx, srs, slots=2, lanes=1)
+    out = []
+    for b in range(4):
+        out += pipe.submit(Cs, zs, ybad if b % 2 else ys, Ps, n, off, seed)
+    out += pipe.drain()
+    assert out == [True, False, True, False], (rank, out)
+    dist.barrier()
+    dist.destroy_process_group()
+    print("RANK OK", rank, flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -79,21 +79,85 @@ def test_full_msm_vs_oracle(ctx):
     assert got == O.msm_g1(curve, _host(pts), sc, n)
 
 
-def test_sharded_msm_cfg4_shape(ctx):
-    """cfg 4 shape on one device: two 2^21-point shards (msm_partial) + combine == one MSM."""
+def test_sharded_msm_cfg4(ctx):
+    """cfg 4 at its real size on one device: G1 MSM n = 2^24 as 8 shards of 2^21 points
+    (msm_partial, one per would-be GPU) + msm_combine, checked through the discrete-log
+    identity sum_i s_i [k_i] G1 = [sum_i k_i s_i mod r] G1: points k_i G1 from
+    the GPU generator (its restatement is checked in test_gpu_parity.py), the dot product
+    and the final scalar multiple on the oracle.  Every shard's partial is checked the same
+    way."""
+    import numpy as np
     import torch
     curve = "bls12_381"
     C = pc.CURVES[curve]
-    n = 1 << 22
-    Cm, z, _, _ = _gen_batch(ctx, curve, n, 77, hashlib.sha256(b"cfg4").digest())
+    shards, m = 8, 1 << 21
+    n = shards * m
+    rs = np.random.default_rng(4)
+    ks = rs.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    ks[:, 0] &= 0x3F                      # < 2^254: canonical Fr (r > 2^254)
+    sc = rs.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    sc[:, 0] &= 0x3F
     g1b = 2 * C.fp_bytes
     pb = ctx.partial_bytes(curve)
-    parts = torch.empty(2 * pb, dtype=torch.uint8, device="cuda")
-    h = n // 2
-    ctx.msm_partial(curve, Cm[: h * g1b], z[: h * 32], h, parts[:pb])
-    ctx.msm_partial(curve, Cm[h * g1b:], z[h * 32:], h, parts[pb:])
-    got = ctx.msm_combine(curve, parts, 2)
-    assert got == O.msm_g1(curve, _host(Cm), _host(z), n)
+    pts = torch.empty(n * g1b, dtype=torch.uint8, device="cuda")
+    d_k = torch.from_numpy(ks.reshape(-1)).cuda()
+    ctx.gen_g1(curve, d_k, n, pts)
+    del d_k
+    d_sc = torch.from_numpy(sc.reshape(-1)).cuda()
+    parts = torch.empty(shards * pb, dtype=torch.uint8, device="cuda")
+    for k in range(shards):
+        ctx.msm_partial(curve, pts[k * m * g1b:(k + 1) * m * g1b], d_sc[k * m * 32:(k + 1) * m * 32], m,
+                        parts[k * pb:(k + 1) * pb])
+    got = ctx.msm_combine(curve, parts, shards)
+    kb, sb = ks.tobytes(), sc.tobytes()
+    want = O.g1_mul_gen(curve, pk.fr_to_bytes(O.fr_dot(curve, kb, sb, n)), 1)
+    assert got == want
+    enc = ctx.partial_encode(curve, parts, shards)
+    for k in (0, shards - 1):
+        lo, hi = k * m * 32, (k + 1) * m * 32
+        assert enc[k] == O.g1_mul_gen(curve, pk.fr_to_bytes(O.fr_dot(curve, kb[lo:hi], sb[lo:hi], m)), 1), k
+
+
+def test_sharded_batch_cfg5_bn254(ctx):
+    """cfg 5 shape on one device: BN254 batch of 2^22 tuples as 8 shards of 2^19 (global index
+    offsets, one per would-be GPU): every shard's A_k, B_k equals the oracle's combination of
+    the same range, the combined A, B equal the oracle's unsharded batch, the verdict is True,
+    and a corrupted y in shard 5 flips it."""
+    import torch
+    curve = "bn254"
+    C = pc.CURVES[curve]
+    shards, m = 8, 1 << 19
+    n, tau = shards * m, 0xC0FFEE + 55
+    Cm, z, y, P = _gen_batch(ctx, curve, n, tau, hashlib.sha256(b"cfg5-sharded").digest())
+    g2 = pk.g2_to_bytes(C.g2, C)
+    tg2 = O.g2_mul(curve, g2, tau)
+    srs = ctx.load_srs(curve, g2, tg2)
+    seed = hashlib.sha256(b"cfg5-sharded-verify").digest()
+    g1b = 2 * C.fp_bytes
+    pb = ctx.partial_bytes(curve)
+    hb = [_host(t) for t in (Cm, z, y, P)]
+    parts = torch.empty(shards * 2 * pb, dtype=torch.uint8, device="cuda")
+
+    def run(yt):
+        for k in range(shards):
+            lo, hi = k * m, (k + 1) * m
+            ctx.batch_partial(srs, Cm[lo * g1b:hi * g1b], z[lo * 32:hi * 32], yt[lo * 32:hi * 32],
+                              P[lo * g1b:hi * g1b], m, lo, seed, parts[k * 2 * pb:(k + 1) * 2 * pb])
+        return ctx.batch_combine(srs, parts, shards)
+
+    assert run(y) is True
+    AB = ctx.last_combination(curve)
+    enc = ctx.partial_encode(curve, parts, 2 * shards)
+    for k in range(shards):
+        lo, hi = k * m, (k + 1) * m
+        want = O.batch_combination(curve, hb[0][lo * g1b:hi * g1b], hb[1][lo * 32:hi * 32], hb[2][lo * 32:hi * 32],
+                                   hb[3][lo * g1b:hi * g1b], m, lo, g2, tg2, seed)
+        assert (enc[2 * k], enc[2 * k + 1]) == want, k
+    ok, Ao, Bo = O.batch_verify(curve, hb[0], hb[1], hb[2], hb[3], n, g2, tg2, seed, want_ab=True)
+    assert ok is True and AB == (Ao, Bo)
+    y2 = y.clone()
+    y2[32 * (5 * m + 123) + 31] ^= 1
+    assert run(y2) is False
 
 
 @pytest.mark.parametrize("curve,n,trusted", [("bls12_381", 300007, False), ("bls12_381", 262143, True),

@@ -259,34 +259,6 @@ def test_async_msm_slots(ctx, curve, torch_dev):
     assert ctx.msm_wait(0) == O.msm_g1(curve, b"", b"", 0)
 
 
-def test_sharded_partials_equal_unsharded(ctx, torch_dev):
-    """Multi-GPU decomposition on one device: 3 shards + combine == single batch."""
-    torch = torch_dev
-    curve = "bls12_381"
-    C = pc.CURVES[curve]
-    n, tau = 2500, 4242
-    seed = hashlib.sha256(b"shard").digest()
-    Cm, z, y, P = _gen_batch(ctx, torch, curve, n, tau, seed)
-    g2 = pk.g2_to_bytes(C.g2, C)
-    srs = ctx.load_srs(curve, g2, O.g2_mul(curve, g2, tau))
-    pb = ctx.partial_bytes(curve)
-    bounds = [0, 1000, 1001, n]
-    parts = torch.empty(3 * 2 * pb, dtype=torch.uint8, device="cuda")
-    g1b = 2 * C.fp_bytes
-    for k in range(3):
-        lo, hi = bounds[k], bounds[k + 1]
-        ctx.batch_partial(srs, Cm[lo * g1b:hi * g1b], z[lo * 32:hi * 32], y[lo * 32:hi * 32], P[lo * g1b:hi * g1b],
-                          hi - lo, lo, seed, parts[k * 2 * pb:(k + 1) * 2 * pb])
-    assert ctx.batch_combine(srs, parts, 3) is True
-    # MSM sharding
-    pts = Cm[: 2000 * g1b]
-    sc = z[: 2000 * 32]
-    mp = torch.empty(2 * pb, dtype=torch.uint8, device="cuda")
-    ctx.msm_partial(curve, pts[: 700 * g1b], sc[: 700 * 32], 700, mp[:pb])
-    ctx.msm_partial(curve, pts[700 * g1b:], sc[700 * 32:], 1300, mp[pb:])
-    assert ctx.msm_combine(curve, mp, 2) == ctx.msm_g1(curve, pts, sc, n=2000)
-
-
 @pytest.mark.gpu
 def test_sharded_pipeline_rccl_world1(ctx, torch_dev):
     """kzgmi.distributed.ShardedPipeline on the device over a world-1 RCCL group: async shard
