@@ -75,14 +75,33 @@ def host_info():
                 model = line.split(":", 1)[1].strip()
     except Exception:
         pass
-    return model, os.cpu_count()
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except Exception:
+        allowed = os.cpu_count()
+    return {"lscpu_model": model, "nproc": os.cpu_count(), "sched_getaffinity": allowed,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_threads():
+    """CPUs this process may use: its affinity mask, capped by an explicit OMP_NUM_THREADS (the
+    GPU box grants each job a 16-CPU share and exports OMP_NUM_THREADS=16 for it)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except Exception:
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 def cpu_baseline(curve, Cm, z, y, P, n_full, seed, target_s):
-    """Time the C oracle (OpenMP, all threads it is given) on a bounded prefix sample."""
+    """Time the C oracle (OpenMP, on every CPU this process may use) on a bounded prefix sample."""
     from oracle import oracle as O  # cpu_baseline leg only
     g1b = 2 * kzgmi.FP_BYTES[curve]
     g2, tg2 = kzgmi.G2_GENERATOR[curve], None
+    O.set_threads(cpu_threads())
     threads = O.threads()
 
     def run(m):
@@ -116,8 +135,10 @@ def cpu_baseline(curve, Cm, z, y, P, n_full, seed, target_s):
         "unit": "batch-verifies/s (extrapolated linearly from the sample to n=%d tuples)" % n_full,
         "cores": threads,
         "kind": "port",
-        "sample": "oracle/c batch_verify on the first %d of the %d tuples, %.2f s on %d OpenMP threads "
-                  "(self-authored CPU verifier; the reference has none)" % (m, n_full, dt, threads),
+        "sample": "oracle/c batch_verify on the first %d of the %d tuples, %.2f s on %d OpenMP threads = every CPU "
+                  "this process may use; an unoptimised correctness oracle (unsigned-window Jacobian Pippenger, "
+                  "affine Miller loop, plain-pow final exponentiation), self-authored -- the reference has no "
+                  "CPU verifier" % (m, n_full, dt, threads),
         "sample_tuples_per_s": m / dt,
         "single_core": {"value": (m1 / dt1) / n_full, "sample_tuples": m1, "seconds": dt1,
                         "tuples_per_s": m1 / dt1},
@@ -144,6 +165,9 @@ def main():
                     help="secondary: fixed-base prover commits of n coefficients (0 = skip)")
     ap.add_argument("--compressed-steps", type=int, default=36,
                     help="secondary: pipelined batches with compressed inputs + subgroup checks (0 = skip)")
+    ap.add_argument("--cfg4-msms", type=int, default=6,
+                    help="configs[3]: G1 MSMs of --cfg4-n points split over the ranks (strong scaling; 0 = skip)")
+    ap.add_argument("--cfg4-n", type=int, default=1 << 24)
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU pipeline (RCCL all-gather per batch) even at world size 1")
     args = ap.parse_args()
@@ -447,6 +471,65 @@ def main():
         ctx.set_trusted_g1(False)
         assert ref_u == ref_t, "GLV MSM differs from the plain MSM"
 
+    # ---- configs[3]: one G1 MSM of cfg4_n points (2^24) split by point range over the ranks
+    # (strong scaling: 2^21 per rank at 8 GPUs), partial sums all-gathered over RCCL; 2 MSMs in
+    # flight per rank (each slot's workspace holds ~8 GB at 2^24 points)
+    cfg4 = None
+    if args.cfg4_msms > 0 and curve == "bls12_381":
+        off4, m4 = (rank * args.cfg4_n // world, (rank + 1) * args.cfg4_n // world - rank * args.cfg4_n // world)
+        gen = torch.Generator(device="cuda").manual_seed(1000 + rank)
+        k4 = torch.randint(0, 256, (m4, 32), dtype=torch.uint8, device="cuda", generator=gen)
+        k4[:, 0] &= 0x3F                               # < 2^254 < r
+        s4 = torch.randint(0, 256, (m4, 32), dtype=torch.uint8, device="cuda", generator=gen)
+        s4[:, 0] &= 0x3F
+        p4 = torch.empty(m4 * 2 * kzgmi.FP_BYTES[curve], dtype=torch.uint8, device="cuda")
+        ctx.gen_g1(curve, k4.reshape(-1), m4, p4)
+        del k4
+        s4 = s4.reshape(-1)
+        res4 = []
+        if world > 1 or sharded:
+            mp4 = ShardedMsmPipeline(ctx, curve, slots=2, lanes=2)
+            sub4 = lambda: res4.extend(mp4.submit(p4, s4, m4))  # noqa: E731
+            drain4 = lambda: res4.extend(mp4.drain())  # noqa: E731
+        else:
+            q4 = [0]
+
+            def sub4():
+                sl = q4[0] % 2
+                if q4[0] >= 2:
+                    res4.append(ctx.msm_wait(sl))
+                ctx.msm_g1_async(curve, sl, p4, s4, m4)
+                q4[0] += 1
+
+            def drain4():
+                first = q4[0] % 2 if q4[0] >= 2 else 0
+                for i in range(min(q4[0], 2)):
+                    res4.append(ctx.msm_wait((first + i) % 2))
+                q4[0] = 0
+        sub4()
+        drain4()                                        # warm both workspaces' allocation
+        sub4()
+        drain4()
+        barrier()
+        a = time.perf_counter()
+        for _ in range(args.cfg4_msms):
+            sub4()
+        drain4()
+        barrier()
+        dt4 = time.perf_counter() - a
+        if world > 1:
+            t = torch.tensor([dt4], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt4 = float(t.item())
+        assert len(set(res4)) == 1, "configs[3] MSM results differ between runs"
+        cfg4 = {"pts_per_s": args.cfg4_n * args.cfg4_msms / dt4, "ms_per_msm": 1e3 * dt4 / args.cfg4_msms,
+                "n_total": args.cfg4_n, "n_per_rank": m4, "msms": args.cfg4_msms, "world": world,
+                "scaling": "strong", "scalars": "uniform < 2^254 (16 windows of 16 bits)",
+                "method": "point-range shards, kzgmi_msm_partial_device_async + RCCL all-gather of partial "
+                          "sums + kzgmi_msm_combine_device_async, 2 MSMs in flight per rank" if world > 1 or sharded
+                          else "one device, kzgmi_msm_g1_device_async, 2 MSMs in flight"}
+        del p4, s4
+
     if rank != 0:
         dist.barrier()
         dist.destroy_process_group()
@@ -523,8 +606,7 @@ def main():
     if not args.no_cpu and world == 1:
         try:
             cpu = cpu_baseline(curve, Cm, z, y, P, n, vseed, args.cpu_seconds)
-            model, ncpu = host_info()
-            cpu["host"] = {"lscpu_model": model, "nproc": ncpu}
+            cpu["host"] = host_info()
         except Exception as e:  # the baseline must not kill the GPU measurement
             cpu = {"error": repr(e)}
     out = {
@@ -566,7 +648,10 @@ def main():
             "compressed_subgroup": comp,
             "fiat_shamir": fsm,
             "prover_commit": commit,
+            "cfg4_msm_2e24": cfg4,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu and "value" in cpu else None,
+            "gpu_vs_cpu_note": "against the unoptimised oracle on %s CPUs (see cpu_baseline.sample), not a tuned "
+                               "CPU verifier" % ((cpu or {}).get("cores")),
         },
     }
     print(json.dumps(out), flush=True)

@@ -49,12 +49,12 @@ void Launch<Cv>::reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, con
   k_reduce_segments<Cv><<<grid_for(nseg, 256), 256, 0, st>>>(nseg, cnt, buckets, R, U);
   // scratch: nsets * RB_PARTS partial sums
   k_reduce_bits<Cv><<<nsets * RB_PARTS, 256, 0, st>>>(R, U, scratch);
-  k_reduce_bits_finish<Cv><<<grid_for(nsets, 64), 64, 0, st>>>(nsets, scratch, winsum);
+  k_reduce_bits_finish<Cv><<<nsets, 64, 0, st>>>(scratch, winsum);
 }
 
 template <class Cv>
 void Launch<Cv>::window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res) {
-  k_window_combine<Cv><<<1, 64, 0, st>>>(mw, winsum, res);
+  k_window_combine<Cv><<<mw.nmsm, 64, 0, st>>>(mw, winsum, res);
 }
 
 template void Launch<KZ_CURVE_T>::sort(hipStream_t, const TermList&, uint32_t, const uint8_t*, uint32_t*, uint32_t*,
