@@ -36,6 +36,11 @@ struct F29 {
   }
 };
 
+#ifdef KZ_MAD29_PLAIN
+// A/B variant: let hipcc emit the v_mad_u64_u32 (no inline-asm boundary s_nop padding)
+KZ_DEV void mad29(uint64_t& acc, uint32_t a, uint32_t b) { acc += (uint64_t)a * (uint64_t)b; }
+KZ_DEV void mad29s(uint64_t& acc, uint32_t a, uint32_t b_uniform) { acc += (uint64_t)a * (uint64_t)b_uniform; }
+#else
 KZ_DEV void mad29(uint64_t& acc, uint32_t a, uint32_t b) {
   uint64_t cc;  // carry-out unused: column sums stay below 2^64
   asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
@@ -44,6 +49,7 @@ KZ_DEV void mad29s(uint64_t& acc, uint32_t a, uint32_t b_uniform) {
   uint64_t cc;
   asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "s"(b_uniform));
 }
+#endif
 
 // (a b [+ c d] + m p) / R29 -- product scanning, one 64-bit accumulator per column
 template <class Q, bool TWO>

@@ -46,7 +46,7 @@ template <class Cv>
 void Launch<Cv>::reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const XY* buckets, XY* R, XY* U,
                         XY* scratch, XY* winsum) {
   const uint32_t nseg = nsets * (NBUCKETS / SEG);
-  k_reduce_segments<Cv><<<grid_for(nseg, 256), 256, 0, st>>>(nseg, cnt, buckets, R, U);
+  k_reduce_segments<Cv><<<grid_for(2 * (size_t)nseg, 256), 256, 0, st>>>(nseg, cnt, buckets, R, U);  // 2 threads per segment
   // scratch: nsets * RB_PARTS partial sums
   k_reduce_bits<Cv><<<nsets * RB_PARTS, 256, 0, st>>>(R, U, scratch);
   k_reduce_bits_finish<Cv><<<nsets, 64, 0, st>>>(scratch, winsum);

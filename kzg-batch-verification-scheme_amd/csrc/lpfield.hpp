@@ -40,6 +40,18 @@ KZ_DEV int32_t lp_bcast(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0x150 + 
 KZ_DEV int32_t lp_next(int32_t x) { return __builtin_amdgcn_update_dpp(0, x, 0x101, 0xF, 0xF, true); }  // row_shl:1: lane j <- j+1, lane 15 <- 0
 KZ_DEV int32_t lp_prev(int32_t x) { return __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true); }  // row_shr:1: lane j <- j-1, lane 0 <- 0
 
+// acc += a b, signed 32 x 32 -> 64 (one v_mad_i64_i32; hipcc lowers the C++ form to two
+// unsigned mads plus sign fix-ups).  One instruction per asm statement (see field.hpp).
+KZ_DEV void lp_mad_i64(int64_t& acc, int32_t a, int32_t b) {
+  uint64_t cc;
+  asm("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
+}
+// acc += a b for 0 <= a, b < 2^31 (two's complement acc: the unsigned sum wraps correctly)
+KZ_DEV void lp_mad_u64(int64_t& acc, int32_t a, int32_t b) {
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
+}
+
 // per-lane constants of a lane-parallel kernel (lane j = threadIdx.x % 16 of row threadIdx.x / 16 % 4)
 template <class Cv>
 struct LpCtx {
@@ -80,18 +92,6 @@ KZ_DEV int32_t lp_norm(const LpCtx<Cv>& c, int32_t v) {
   return (v & c.lomask) + lp_prev(carry);
 }
 
-// acc += a b, signed 32 x 32 -> 64 (one v_mad_i64_i32; hipcc lowers the C++ form to two
-// unsigned mads plus sign fix-ups).  One instruction per asm statement (see field.hpp).
-KZ_DEV void lp_mad_i64(int64_t& acc, int32_t a, int32_t b) {
-  uint64_t cc;
-  asm("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
-}
-// acc += a b for 0 <= a, b < 2^31 (two's complement acc: the unsigned sum wraps correctly)
-KZ_DEV void lp_mad_u64(int64_t& acc, int32_t a, int32_t b) {
-  uint64_t cc;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
-}
-
 template <class Cv, int I>
 KZ_DEV void lp_mul_iter(int64_t& acc, int32_t a, int32_t b, int32_t pj) {
   const int32_t ai = lp_bcast<I>(a);
@@ -113,6 +113,38 @@ KZ_DEV int32_t lp_mul_raw(int32_t a, int32_t b, int32_t pj, std::integer_sequenc
 template <class Cv>
 KZ_DEV int32_t lp_mul(const LpCtx<Cv>& c, int32_t a, int32_t b) {
   return lp_norm(c, lp_mul_raw<Cv>(a, b, c.pj, std::make_integer_sequence<int, LpQ<Cv>::N>{}));
+}
+
+// 64-bit per-lane accumulator (|acc| < 2^58; the top lane's own value must fit 32 bits, which the
+// value bound guarantees) -> normalised limbs
+template <class Cv>
+KZ_DEV int32_t lp_norm64(const LpCtx<Cv>& c, int64_t acc) {
+  const bool top = c.cmask == 0;  // lanes >= N - 1 keep their value and emit no carry
+  const int32_t keep = top ? (int32_t)acc : (int32_t)((uint32_t)acc & (uint32_t)LP_M29);
+  const int32_t carry = top ? 0 : (int32_t)(acc >> 29);
+  return lp_norm(c, keep + lp_prev(carry));
+}
+
+// v - q p with q = round(v / p) from the row's two top limbs: |result| < 0.51 p, congruent to v.
+// Row-local (each row its own value); ~15 instructions instead of a Montgomery product by 1.
+template <class Cv>
+KZ_DEV int32_t lp_reduce(const LpCtx<Cv>& c, int32_t v) {
+  using Q = LpQ<Cv>;
+  const double t = (double)lp_bcast<Q::N - 1>(v) * Q::RED_C1 + (double)lp_bcast<Q::N - 2>(v) * Q::RED_C2;
+  const int32_t q = (int32_t)__builtin_rint(t);
+  int64_t acc = (int64_t)v;
+  lp_mad_i64(acc, -q, c.pj);
+  return lp_norm64(c, acc);
+}
+
+// v == 0 (mod p), row-local: reduce below p, then resolve every carry (value 0 <=> all limbs 0)
+template <class Cv>
+KZ_DEV bool lp_row_is_zero(const LpCtx<Cv>& c, int32_t v) {
+  int32_t r = lp_reduce(c, v);
+#pragma unroll
+  for (int k = 0; k < LpQ<Cv>::N; ++k) r = lp_norm(c, r);
+  const uint64_t nz = __builtin_amdgcn_ballot_w64(r != 0);
+  return ((nz >> (16 * c.row)) & 0xFFFFull) == 0;
 }
 
 template <class Cv> KZ_DEV int32_t lp_add(const LpCtx<Cv>& c, int32_t a, int32_t b) { return lp_norm(c, a + b); }
