@@ -50,6 +50,7 @@ HBM_PEAK = 8.0e12          # B/s, MI355X spec (MI355X_MICROARCH.md)
 TAU = 0x2A1B3C4D5E6F708192A3B4C5D6E7F8091A2B3C4D5E6F7081
 BYTES_PER_TUPLE = {"bls12_381": 256, "bn254": 192}
 BYTES_PER_MSM_POINT = {"bls12_381": 128, "bn254": 96}
+PROFILE_ROUND = "r02"      # profiles/<round>/rocprof_single: the committed rocprofv3 summaries
 
 
 def log(*a):
@@ -553,22 +554,27 @@ def main():
     # PMC traffic of the same kernel and config from the committed profile (tools/profile.sh:
     # separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE x 2 as MI355X_MICROARCH.md prescribes)
     traffic, traffic_src, rocprof_ms, rocprof_src, gather_bytes = None, None, None, None, None
-    pmc_path = os.path.join(ROOT, "profiles", "r01", "rocprof_single", "pmc_accumulate_single.json")
-    single_path = os.path.join(ROOT, "profiles", "r01", "rocprof_single", "kernel_single.json")
+    prof_dir = os.path.join("profiles", PROFILE_ROUND, "rocprof_single")
+    pmc_path = os.path.join(ROOT, prof_dir, "pmc_accumulate_single.json")
+    single_path = os.path.join(ROOT, prof_dir, "kernel_single.json")
     if curve == "bls12_381" and n == 1 << 20 and os.path.exists(pmc_path):
         with open(pmc_path) as f:
             pmc = json.load(f)
-        # FETCH_SIZE as counted (x1): the kernel's loads are 16-B-per-lane gathers of scattered
-        # 128-B points, not the wide streaming reads the guide's x2 correction was calibrated on
-        # (x2 would exceed the two 128-B lines a point can touch)
-        traffic = (pmc["FETCH_SIZE_KiB_per_launch_raw"] + pmc["WRITE_SIZE_KiB_per_launch"]) * 1024
-        traffic_src = "profiles/r01/rocprof_single/pmc_accumulate_single.json (%s; FETCH_SIZE + WRITE_SIZE)" % pmc["command"]
+        # FETCH_SIZE x 2 + WRITE_SIZE (MI355X_MICROARCH.md HBM section; calibrated on k_pts_to29,
+        # profiles/r02/pmc_sq_accumulate.json)
+        traffic = (2 * pmc["FETCH_SIZE_KiB_per_launch_raw"] + pmc["WRITE_SIZE_KiB_per_launch"]) * 1024
+        traffic_src = "%s/pmc_accumulate_single.json (%s; 2 x FETCH_SIZE + WRITE_SIZE)" % (prof_dir, pmc["command"])
         gather_bytes = pmc.get("gather_model_bytes_per_launch")
     if curve == "bls12_381" and n == 1 << 20 and os.path.exists(single_path):
         with open(single_path) as f:
             ks = json.load(f)
         rocprof_ms = ks["accumulate_phase_avg_ms"]
-        rocprof_src = "profiles/r01/rocprof_single/kernel_single.json (%s)" % ks["command"]
+        rocprof_src = "%s/kernel_single.json (%s)" % (prof_dir, ks["command"])
+    # hardware-derived compute floor: the measured v_mad_u64_u32 issue rate (8 independent chains,
+    # 8 waves per SIMD: 0.4596 wave-instructions per SIMD per ns, profiles/r01/probes/mad_rate.txt)
+    # x SIMDs x 64 lanes / 392 mads per radix-2^29 product (14 x 14 for a b + 14 x 14 for m p)
+    n_simd = 4 * torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    mad_floor = 0.4596e9 * n_simd * 64 / 392 if curve == "bls12_381" else None
     roofline = {
         "bound": "hbm",
         "achieved": achieved / 1e9 if achieved else None,
@@ -597,6 +603,14 @@ def main():
             "achieved_fpmul_per_s": acc_fpmuls / (acc_ms * 1e-3) if acc_ms > 0 else None,
             "peak_fpmul_per_s": fpmul_peak,
             "frac": (acc_fpmuls / (acc_ms * 1e-3)) / fpmul_peak if acc_ms > 0 else None,
+            "peak_note": "peak_fpmul_per_s: kzgmi_probe_fpmul (32-bit-limb products, 8 chains per thread, whole "
+                         "chip) measured in this run; hw_floor: the hardware mad issue rate",
+            "hw_floor": {
+                "mad_issue_rate_per_simd_ns": 0.4596, "simds": n_simd, "mads_per_product": 392,
+                "source": "profiles/r01/probes/mad_rate.txt (tools/probes/mad_rate.hip, 8 waves/SIMD)",
+                "peak_fpmul_per_s": mad_floor,
+                "frac": (acc_fpmuls / (acc_ms * 1e-3)) / mad_floor if (mad_floor and acc_ms > 0) else None,
+            },
             # whole pipeline: accumulation products per second of wall time (batches/s x
             # products per batch) against the probe peak -- what the overlap actually sustains
             "pipeline_frac": acc_fpmuls * value / world / fpmul_peak,

@@ -66,11 +66,12 @@ if fetch and write:
         "launches_fetch": len(fetch), "launches_write": len(write),
         "FETCH_SIZE_KiB_per_launch_raw": fetch_kib,
         "WRITE_SIZE_KiB_per_launch": write_kib,
-        "traffic_bytes_per_launch": (fetch_kib + write_kib) * 1024,
-        "traffic_bytes_per_launch_if_x2": (2 * fetch_kib + write_kib) * 1024,
-        "correction": "FETCH_SIZE taken as counted: the guide's x2 (gfx950 tallies 128-B requests of wide "
-                      "streaming reads at 64 B) does not fit these 16-B-per-lane gathers -- x2 would exceed the "
-                      "two 128-B lines a gathered point can touch.  Infinity-Cache hits are counted, so this is "
+        "traffic_bytes_per_launch": (2 * fetch_kib + write_kib) * 1024,
+        "traffic_bytes_per_launch_raw": (fetch_kib + write_kib) * 1024,
+        "correction": "FETCH_SIZE x 2 + WRITE_SIZE, as MI355X_MICROARCH.md's HBM section prescribes (gfx950 "
+                      "tallies 128-B requests at 64 B); calibrated in our own 16-B-per-lane access pattern: "
+                      "k_pts_to29 reads 268.4 MB of 128-B point slots and FETCH_SIZE reports 142.5 MB (x1.88, "
+                      "profiles/r02/pmc_sq_accumulate.json).  Infinity-Cache hits are counted, so this is "
                       "L2-miss traffic, an upper bound on HBM bytes",
         "algorithmic_bytes_per_launch": 256 * n,
         "gather_model_bytes_per_launch": entries * (112 + 8),
