@@ -84,6 +84,40 @@ KZ_DEV F29<Q> mont29(const F29<Q>& a, const F29<Q>& b, const F29<Q>& c, const F2
 }
 template <class Q>
 KZ_DEV F29<Q> mul29(const F29<Q>& a, const F29<Q>& b) { return mont29<Q, false>(a, b, a, b); }
+// a^2 / R29: the off-diagonal limb products once, against a pre-doubled operand (2 a_i < 2^30),
+// plus the squares on the diagonal -- 91 + 14 + 196 (m p) = 301 mads instead of 392.  Column
+// bound: 7 x 2^59 + 2^58 + 14 x 2^58 + carry < 2^63 (limbs < 2^29, top limb < 2^16).
+template <class Q>
+KZ_DEV F29<Q> sqr29(const F29<Q>& a) {
+  constexpr int N = Q::N;
+  uint32_t a2[N];
+  _Pragma("unroll") for (int i = 0; i < N; ++i) a2[i] = a.v[i] + a.v[i];
+  uint32_t m[N];
+  F29<Q> t;
+  uint64_t acc = 0;
+  _Pragma("unroll") for (int k = 0; k < N; ++k) {
+    _Pragma("unroll") for (int i = 0; i < k; ++i) {
+      if (i < k - i) mad29(acc, a2[i], a.v[k - i]);
+      mad29s(acc, m[i], Q::MOD[k - i]);
+    }
+    if ((k & 1) == 0) mad29(acc, a.v[k / 2], a.v[k / 2]);
+    m[k] = ((uint32_t)acc * Q::INV) & M29;
+    mad29s(acc, m[k], Q::MOD[0]);
+    acc >>= 29;
+  }
+  _Pragma("unroll") for (int k = N; k < 2 * N - 1; ++k) {
+    _Pragma("unroll") for (int i = k - N + 1; i < N; ++i) {
+      if (i < k - i) mad29(acc, a2[i], a.v[k - i]);
+      mad29s(acc, m[i], Q::MOD[k - i]);
+    }
+    if ((k & 1) == 0) mad29(acc, a.v[k / 2], a.v[k / 2]);
+    t.v[k - N] = (uint32_t)acc & M29;
+    acc >>= 29;
+  }
+  t.v[N - 1] = (uint32_t)acc;
+  return t;
+}
+
 template <class Q>
 KZ_DEV F29<Q> mul2_29(const F29<Q>& a, const F29<Q>& b, const F29<Q>& c, const F29<Q>& d) {
   return mont29<Q, true>(a, b, c, d);

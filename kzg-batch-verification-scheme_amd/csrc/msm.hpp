@@ -540,12 +540,12 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t len, uint32_t chun
         inf = true;
         continue;
       }
-      const G PP = mul29(P, P);
+      const G PP = sqr29(P);
       const G PPP = mul29(P, PP);
       st(s_zz, mul29(ld(s_zz), PP));
       st(s_zzz, mul29(ld(s_zzz), PPP));
       const G Q2 = mul29(x, PP);
-      const G X3 = sub29(mul29(R, R), add3_29(PPP, Q2, Q2), Q::B8);  // < 10p
+      const G X3 = sub29(sqr29(R), add3_29(PPP, Q2, Q2), Q::B8);  // < 10p
       y = mul2_29(R, sub29(Q2, X3, Q::B16), y, sub29(G::zero(), PPP, Q::B8));  // R (Q - X3) - Y1 PPP
       x = X3;
     }
