@@ -135,8 +135,12 @@ KZ_DEV Fp<P> fp_mul_cios(const Fp<P>& a, const Fp<P>& b) {
 // Each multiply-add is its own asm statement, so hipcc pads every boundary with `s_nop 0`
 // (~1 nop per product).  Fusing 2-4 (a*b, m*p) pairs per statement removes them but measured
 // no gain (tools/probes/macfuse.hip: 63.2 vs 64.1 G 12x12 products/s -- other waves fill the
-// pad) and produced wrong products inside the library kernels (not in the isolated probe), so
-// the verified one-product-per-statement form stays.
+// pad) and produced wrong products inside the library kernels (not in the isolated probe).
+// Cause (tools/probes/asm_clobber.hip): the fused statements declared the accumulators "+v"
+// without early clobber, so hipcc could give an accumulator the register of an input that a
+// LATER instruction of the same statement still reads (register allocation decides, hence
+// library-only); every output written before a later read needs "&".  The one-product-per-
+// statement form below cannot alias and stays (the fusion gained nothing anyway).
 KZ_DEV void mac32(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b) {
   uint64_t cc;
   asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"
