@@ -18,9 +18,134 @@
 #pragma once
 #include <type_traits>
 
+#include "field29.hpp"
 #include "kernels.hpp"
 
 namespace kzgmi {
+
+// ---- BLS12-381 in radix 2^29 (field29.hpp): the square root's 375 squarings and the
+// membership test's 126 doublings are throughput-bound chains of products, and a radix-29
+// squaring is 301 mads instead of ~650 VALU instructions for a 32-bit-limb product (round 2:
+// the convert phase of a compressed 2^20 batch 59 -> ~40 ms).  Value bounds per step below.
+using Q29 = Bls12_381Fp29;
+using G29 = F29<Q29>;
+
+KZ_DEV G29 sel8_29(uint32_t k, const G29 (&t)[8]) {
+  G29 r = t[0];
+#pragma unroll
+  for (int j = 1; j < 8; ++j)
+    if (k == (uint32_t)j) r = t[j];
+  return r;
+}
+
+// (x^3 + b)^((p+1)/4) for BLS12-381 in radix 2^29: the generated width-4 window of fp_pow_sqrt
+template <class P>
+KZ_DEV Fp<P> fp_pow_sqrt29(const Fp<P>& a) {
+  const G29 x = fp_to29<Q29>(a);
+  const G29 x2 = sqr29(x);
+  G29 t[8];
+  t[0] = x;
+#pragma unroll
+  for (int j = 1; j < 8; ++j) t[j] = mul29(t[j - 1], x2);
+  G29 acc = sel8_29((uint32_t)P::SQRT_FIRST, t);
+  for (int s = 0; s < P::SQRT_STEPS; ++s) {
+    const int nsq = P::SQRT_SQR[s];
+    for (int q = 0; q < nsq; ++q) acc = sqr29(acc);
+    const uint32_t k = P::SQRT_IDX[s];
+    if (k != 255u) acc = mul29(acc, sel8_29(k, t));
+  }
+  return fp_from29<Q29, P>(acc);
+}
+
+KZ_DEV G29 dbl29(const G29& a) { return add3_29(a, a, G29::zero()); }
+
+// a = 0 Jacobian point in radix 2^29 with an explicit infinity flag (exact; no zero test of Z)
+struct Jac29 {
+  G29 x, y, z;
+  bool inf;
+};
+
+// dbl-2009-l.  Inputs X < 34p, Y < 18p, Z < 8p  ->  X3 < 34p, Y3 < 18p, Z3 < 4p
+KZ_DEV Jac29 jac29_dbl(const Jac29& p) {
+  const G29 A = sqr29(p.x), B = sqr29(p.y), C = sqr29(B);                        // < 2p
+  const G29 D0 = sqr29(add3_29(p.x, B, G29::zero()));                           // < 2p
+  const G29 D = dbl29(sub29(sub29(D0, A, Q29::B2), C, Q29::B2));                // < 12p
+  const G29 E = add3_29(A, A, A);                                              // < 6p
+  Jac29 r;
+  r.x = sub29(sqr29(E), dbl29(D), Q29::B32);                                    // < 34p
+  r.y = sub29(mul29(E, sub29(D, r.x, Q29::B64)), dbl29(dbl29(dbl29(C))), Q29::B16);  // < 18p
+  r.z = dbl29(mul29(p.y, p.z));                                                 // < 4p
+  r.inf = p.inf;
+  return r;
+}
+
+// v == 0 mod p for any v < 2^12 p (one product by the Montgomery one brings it below 2p)
+KZ_DEV bool zero29(const G29& v) { return is_zero29(mul29(v, G29::from_const(Q29::ONE))); }
+
+// p + q, q affine (< 2p; madd-2007-bl).  p: X < 34p, Y < 18p, Z < 8p -> X3, Y3, Z3 < 8p
+__device__ __noinline__ Jac29 jac29_add_affine(const Jac29& p, const G29& qx, const G29& qy) {
+  if (p.inf) return {qx, qy, G29::from_const(Q29::ONE), false};
+  const G29 Z1Z1 = sqr29(p.z);
+  const G29 U2 = mul29(qx, Z1Z1);
+  const G29 S2 = mul29(qy, mul29(p.z, Z1Z1));
+  const G29 H = sub29(U2, p.x, Q29::B64);                                       // < 66p
+  const G29 rr = dbl29(sub29(S2, p.y, Q29::B32));                               // < 68p
+  if (zero29(H)) {
+    if (zero29(rr)) return jac29_dbl({qx, qy, G29::from_const(Q29::ONE), false});
+    Jac29 o = p;
+    o.inf = true;
+    return o;
+  }
+  const G29 HH = sqr29(H);
+  const G29 I = dbl29(dbl29(HH));                                               // < 8p
+  const G29 J = mul29(H, I), V = mul29(p.x, I);
+  Jac29 r;
+  r.x = sub29(sub29(sqr29(rr), J, Q29::B2), dbl29(V), Q29::B4);                 // < 8p
+  r.y = sub29(mul29(rr, sub29(V, r.x, Q29::B8)), dbl29(mul29(p.y, J)), Q29::B4);  // < 6p
+  r.z = sub29(sub29(sqr29(add3_29(p.z, H, G29::zero())), Z1Z1, Q29::B2), HH, Q29::B2);  // < 6p
+  r.inf = false;
+  return r;
+}
+
+// p + q, both Jacobian (add-2007-bl); inputs as jac29_dbl's outputs -> X3 < 8p, Y3 < 6p, Z3 < 2p
+__device__ __noinline__ Jac29 jac29_add(const Jac29& p, const Jac29& q) {
+  if (p.inf) return q;
+  if (q.inf) return p;
+  const G29 Z1Z1 = sqr29(p.z), Z2Z2 = sqr29(q.z);
+  const G29 U1 = mul29(p.x, Z2Z2), U2 = mul29(q.x, Z1Z1);
+  const G29 S1 = mul29(p.y, mul29(q.z, Z2Z2)), S2 = mul29(q.y, mul29(p.z, Z1Z1));
+  const G29 H = sub29(U2, U1, Q29::B2);                                         // < 4p
+  const G29 rr = dbl29(sub29(S2, S1, Q29::B2));                                 // < 8p
+  if (is_zero29(H)) {
+    if (is_zero29(rr)) return jac29_dbl(p);
+    Jac29 o = p;
+    o.inf = true;
+    return o;
+  }
+  const G29 I = sqr29(dbl29(H));
+  const G29 J = mul29(H, I), V = mul29(U1, I);
+  Jac29 r;
+  r.x = sub29(sub29(sqr29(rr), J, Q29::B2), dbl29(V), Q29::B4);                 // < 8p
+  r.y = sub29(mul29(rr, sub29(V, r.x, Q29::B8)), dbl29(mul29(S1, J)), Q29::B4);   // < 6p
+  r.z = mul29(sub29(sub29(sqr29(add3_29(p.z, q.z, G29::zero())), Z1Z1, Q29::B2), Z2Z2, Q29::B2), H);  // < 2p
+  r.inf = false;
+  return r;
+}
+
+// [|x|] q (BLS parameter bit pattern), radix 2^29
+template <class Cv, bool AFFINE>
+KZ_DEV Jac29 mul_by_x_abs29(const Jac29& q, const G29& qx, const G29& qy) {
+  constexpr uint64_t X = Cv::K::X_ABS;
+  Jac29 acc = q;  // top bit
+  for (int b = 62; b >= 0; --b) {
+    acc = jac29_dbl(acc);
+    if ((X >> b) & 1) {
+      if constexpr (AFFINE) acc = jac29_add_affine(acc, qx, qy);
+      else acc = jac29_add(acc, q);
+    }
+  }
+  return acc;
+}
 
 // raw (standard-form) a > b
 template <class P>
@@ -71,7 +196,9 @@ __global__ void __launch_bounds__(256) k_decompress_points(const uint8_t* __rest
     } else {
       a.x = fp_to_mont(x);
       const F rhs = fp_add(fp_mul(fp_sqr(a.x), a.x), F::from_const(Cv::K::B_M));
-      F y = fp_pow_sqrt(rhs);
+      F y;
+      if constexpr (Cv::ID == 0) y = fp_pow_sqrt29(rhs);
+      else y = fp_pow_sqrt(rhs);
       if (!(fp_sqr(y) == rhs)) {
         raise_err(err, DERR_NOT_ON_CURVE);
         is_inf = true;
@@ -230,12 +357,15 @@ __global__ void __launch_bounds__(256) k_subgroup_check(const Affine<Cv>* __rest
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || inf[i]) return;
   const Affine<Cv> p = pts[i];
-  const Jac<Cv> q1 = mul_by_x_abs<Cv>(p, Jac<Cv>{p.x, p.y, F::one()});
-  const Jac<Cv> q2 = mul_by_x_abs<Cv>(q1, q1);  // [x^2] p
+  // [x^2] p in radix 2^29 (the 126 doublings), then back to the 32-bit form for the comparison
+  const G29 px = fp_to29<Q29>(p.x), py = fp_to29<Q29>(p.y);
+  const Jac29 q1 = mul_by_x_abs29<Cv, true>({px, py, G29::from_const(Q29::ONE), false}, px, py);
+  const Jac29 r2 = mul_by_x_abs29<Cv, false>(q1, px, py);
+  const Jac<Cv> q2{fp_from29<Q29, P>(r2.x), fp_from29<Q29, P>(r2.y), r2.inf ? F::zero() : fp_from29<Q29, P>(r2.z)};
   // p in G1 <=> q2 == -phi(p) = (beta x, -y): X2 == beta x Z2^2 and Y2 == -y Z2^3, q2 finite
   const F bx = fp_mul(F::from_const(Cv::K::BETA_M), p.x);
   const F z2 = fp_sqr(q2.z);
-  const bool ok = !q2.is_inf() && q2.x == fp_mul(bx, z2) && q2.y == fp_mul(fp_neg(p.y), fp_mul(z2, q2.z));
+  const bool ok = !r2.inf && !q2.is_inf() && q2.x == fp_mul(bx, z2) && q2.y == fp_mul(fp_neg(p.y), fp_mul(z2, q2.z));
   if (!ok) raise_err(err, DERR_NOT_IN_SUBGROUP);
 }
 
