@@ -126,7 +126,9 @@ struct kzgmi_srs {
   int curve = 0;
   kzgmi_ctx* ctx = nullptr;
   DevBuf lines, q, q_inf;
-  DevBuf g1;                        // the SRS's [1]_1: Montgomery affine point + its infinity byte after it
+  DevBuf g1;                        // the SRS's [1]_1: Montgomery affine point + its infinity byte after it,
+  size_t g1_29_off = 0;             // then (BLS12-381) the same point in the accumulation's radix-29 format
+  void* g1_29() const { return static_cast<uint8_t*>(g1.p) + g1_29_off; }
   std::vector<kzgmi_srs*> peers;    // multi-device context: the same SRS on each peer device
 };
 
@@ -191,10 +193,11 @@ int map_device_err(uint32_t e) {
 // ------------------------------------------------------------------------------ MSM core
 template <class Cv>
 int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, size_t emax, const MsmWindows& mw,
-                 const Affine<Cv>* pts = nullptr, const uint8_t* inf = nullptr) {
+                 const Affine<Cv>* pts = nullptr, const uint8_t* inf = nullptr, bool pts29 = false) {
   // pts == nullptr: the slot's freshly converted points, put into the accumulation's format
-  // here; explicit pts (commit-key rows) are stored in that format already (kzgmi_ck_load)
-  const bool own_pts = pts == nullptr;
+  // here unless convert_points stored them in it already (pts29); explicit pts (commit-key
+  // rows) are stored in that format already (kzgmi_ck_load)
+  const bool own_pts = pts == nullptr && !pts29;
   TermList tl = tl_in;  // + each class's offset in the digit array
   size_t ndig = 0;
   for (uint32_t k = 0; k < tl.nclass; ++k) {
@@ -330,16 +333,18 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   uint32_t* err = s.flags.template as<uint32_t>() + 1;
   Affine<Cv>* pts = s.pts.template as<Affine<Cv>>();
   uint8_t* inf = s.inf.template as<uint8_t>();
+  // points that only feed the radix-29 accumulation are converted straight into its format
+  const bool pts29 = kAcc29<Cv> && !glv && !(flags & (KZGMI_FLAG_COMPRESSED | KZGMI_FLAG_SUBGROUP_CHECK));
   if (flags & KZGMI_FLAG_COMPRESSED) {
     L::decompress_points(st, (const uint8_t*)dpi, (uint32_t)n, pts, inf, err);
     L::decompress_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err);
   } else {
-    L::convert_points(st, (const uint8_t*)dpi, (uint32_t)n, pts, inf, err);
-    L::convert_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err);
+    L::convert_points(st, (const uint8_t*)dpi, (uint32_t)n, pts, inf, err, pts29);
+    L::convert_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err, pts29);
   }
   if (flags & KZGMI_FLAG_SUBGROUP_CHECK) L::subgroup_check(st, pts, inf, (uint32_t)(2 * n), err);
   // the SRS's [1]_1 as the last term of MSM#1: -t [1]_1
-  HIPCHK(hipMemcpyAsync(pts + 2 * n, srs->g1.p, sizeof(Affine<Cv>), hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpyAsync(pts + 2 * n, pts29 ? srs->g1_29() : srs->g1.p, sizeof(Affine<Cv>), hipMemcpyDeviceToDevice, st));
   HIPCHK(hipMemcpyAsync(inf + 2 * n, srs->g1.template as<uint8_t>() + sizeof(Affine<Cv>), 1, hipMemcpyDeviceToDevice, st));
   if (glv) L::endo_points(st, pts, inf, (uint32_t)PH, pts + PH, inf + PH);
   mark(c, s, PH_CONVERT + 1);
@@ -408,7 +413,7 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
     tl.nclass = 4;
     tl.total = 3 * nn + 1;
     const MsmWindows mw = powers ? MsmWindows{2, {0, 16}, {16, 16}} : MsmWindows{2, {0, 8}, {8, 16}};
-    CHK(run_msm_core<Cv>(c, s, tl, powers ? 32 : 24, (size_t)(powers ? 48 : 32) * n + 16, mw));
+    CHK(run_msm_core<Cv>(c, s, tl, powers ? 32 : 24, (size_t)(powers ? 48 : 32) * n + 16, mw, nullptr, nullptr, pts29));
   }
   if (d_partial_out) {
     HIPCHK(hipMemcpyAsync(d_partial_out, s.res.p, 2 * sizeof(XY), hipMemcpyDeviceToDevice, st));
@@ -566,7 +571,7 @@ int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uin
     int r = 0;
     if ((r = s.stage.ensure(2 * gb + g1b)) || (r = s.flags.ensure(16)) || (r = srs->q.ensure(2 * sizeof(G2Aff<Cv>))) ||
         (r = srs->q_inf.ensure(16)) || (r = srs->lines.ensure(2 * Launch<Cv>::num_lines() * sizeof(Line<Cv>))) ||
-        (r = srs->g1.ensure(sizeof(Affine<Cv>) + 16))) {
+        (r = srs->g1.ensure(2 * sizeof(Affine<Cv>) + 16))) {
       delete srs;
       return r;
     }
@@ -592,7 +597,11 @@ int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uin
       } else {   // NULL: the standard generator
         Launch<Cv>::set_generator(st, g1p, g1inf);
       }
-      okk = hipGetLastError() == hipSuccess &&
+      srs->g1_29_off = sizeof(Affine<Cv>) + 16;
+      Affine<Cv>* g1p29 = static_cast<Affine<Cv>*>(srs->g1_29());
+      okk = hipMemcpyAsync(g1p29, g1p, sizeof(Affine<Cv>), hipMemcpyDeviceToDevice, st) == hipSuccess;
+      Launch<Cv>::pts_to29(st, g1p29, 1);
+      okk = okk && hipGetLastError() == hipSuccess &&
             hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
             hipMemcpyAsync(&g1inf_h, g1inf, 1, hipMemcpyDeviceToHost, st) == hipSuccess &&
             hipStreamSynchronize(st) == hipSuccess;
@@ -760,7 +769,8 @@ int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t
   uint32_t* err = s.flags.template as<uint32_t>() + 1;
   Affine<Cv>* pts = s.pts.template as<Affine<Cv>>();
   uint8_t* inf = s.inf.template as<uint8_t>();
-  Launch<Cv>::convert_points(st, (const uint8_t*)dpts, (uint32_t)n, pts, inf, err);
+  const bool pts29 = kAcc29<Cv> && !glv;
+  Launch<Cv>::convert_points(st, (const uint8_t*)dpts, (uint32_t)n, pts, inf, err, pts29);
   if (glv) Launch<Cv>::endo_points(st, pts, inf, (uint32_t)n, pts + n, inf + n);
   mark(c, s, PH_CONVERT + 1);
   uint32_t* sc = s.scal_s.template as<uint32_t>();
@@ -782,7 +792,7 @@ int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t
     tl.nclass = 1;
     tl.total = nn;
     const MsmWindows mw{1, {0, 0}, {16, 0}};
-    CHK(run_msm_core<Cv>(c, s, tl, 16, (size_t)16 * n + 16, mw));
+    CHK(run_msm_core<Cv>(c, s, tl, 16, (size_t)16 * n + 16, mw, nullptr, nullptr, pts29));
   }
   s.curve = Cv::ID;
   return 0;
@@ -829,7 +839,7 @@ int kzgmi_ck_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1_powers, siz
         L::shift_points(st, pts + (size_t)(w - 1) * n, inf + (size_t)(w - 1) * n, (uint32_t)n, pts + (size_t)w * n,
                         inf + (size_t)w * n);
       L::pts_to29(st, pts, (uint32_t)(CK_ROWS * n));  // resident in the accumulation's format
-      okk = hipGetLastError() == hipSuccess &&
+      okk = okk && hipGetLastError() == hipSuccess &&
             hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
             hipStreamSynchronize(st) == hipSuccess;
     }

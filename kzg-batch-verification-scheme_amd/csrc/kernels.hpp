@@ -46,7 +46,9 @@ KZ_DEV void fp_to_be_words(const Fp<P>& a, uint32_t (&w)[NW], int o) {
 }
 
 // G1 encoding -> affine Montgomery point + infinity flag (errors into *err)
-template <class Cv>
+// To29 (BLS12-381 only): the validated point is stored directly in the accumulation's radix-29
+// format (what k_pts_to29 would make of it), saving that kernel's pass over the points.
+template <class Cv, bool To29 = false>
 __global__ void __launch_bounds__(256) k_convert_points(const uint8_t* __restrict__ bytes, uint32_t n,
                                                         Affine<Cv>* __restrict__ pts, uint8_t* __restrict__ inf,
                                                         uint32_t* __restrict__ err) {
@@ -81,10 +83,21 @@ __global__ void __launch_bounds__(256) k_convert_points(const uint8_t* __restric
     a.y = fp_to_mont(y);
     if (!is_inf && !affine_on_curve(a)) { raise_err(err, DERR_NOT_ON_CURVE); is_inf = true; }
   }
-  uint32_t o[NW];
+  if constexpr (To29) {
+    using Q = Bls12_381Fp29;
+    const F29<Q> x = fp_to29<Q>(a.x), y = fp_to29<Q>(a.y);
+    uint32_t w29[2 * Q::N];
 #pragma unroll
-  for (int k = 0; k < P::N; ++k) { o[k] = a.x.v[k]; o[P::N + k] = a.y.v[k]; }
-  store_words(reinterpret_cast<uint8_t*>(pts + i), o);
+    for (int k = 0; k < Q::N; ++k) { w29[k] = x.v[k]; w29[Q::N + k] = y.v[k]; }
+    uint4* d = reinterpret_cast<uint4*>(pts + i);
+#pragma unroll
+    for (int k = 0; k < Q::N / 2; ++k) d[k] = make_uint4(w29[4 * k], w29[4 * k + 1], w29[4 * k + 2], w29[4 * k + 3]);
+  } else {
+    uint32_t o[NW];
+#pragma unroll
+    for (int k = 0; k < P::N; ++k) { o[k] = a.x.v[k]; o[P::N + k] = a.y.v[k]; }
+    store_words(reinterpret_cast<uint8_t*>(pts + i), o);
+  }
   inf[i] = is_inf ? 1 : 0;
 }
 

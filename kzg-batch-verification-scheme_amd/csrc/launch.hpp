@@ -26,7 +26,10 @@ struct Launch {
                      XY* scratch, XY* winsum);
   static void window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res);
   // ---- I/O and scalars (launch_io.hip)
-  static void convert_points(hipStream_t st, const uint8_t* bytes, uint32_t n, AF* pts, uint8_t* inf, uint32_t* err);
+  // to29: store in the accumulation's radix-29 format (BLS12-381; ignored for BN254), for
+  // points that go straight into run_msm_core(..., pts29 = true)
+  static void convert_points(hipStream_t st, const uint8_t* bytes, uint32_t n, AF* pts, uint8_t* inf, uint32_t* err,
+                             bool to29 = false);
   static void set_generator(hipStream_t st, AF* pt, uint8_t* inf);
   static void decompress_points(hipStream_t st, const uint8_t* bytes, uint32_t n, AF* pts, uint8_t* inf,
                                 uint32_t* err);
