@@ -72,27 +72,44 @@ __global__ void __launch_bounds__(256) k_convert_points(const uint8_t* __restric
   } else {
     is_inf = (any | w[0]) == 0;
   }
-  Affine<Cv> a;
-  if (is_inf) {
-    a.x = Fp<P>::zero();
-    a.y = Fp<P>::zero();
-  } else {
-    Fp<P> x = fp_from_be_words<P>(w, 0), y = fp_from_be_words<P>(w, P::N);
-    if (!fp_raw_lt_mod(x) || !fp_raw_lt_mod(y)) { raise_err(err, DERR_ENCODING); is_inf = true; }
-    a.x = fp_to_mont(x);
-    a.y = fp_to_mont(y);
-    if (!is_inf && !affine_on_curve(a)) { raise_err(err, DERR_NOT_ON_CURVE); is_inf = true; }
-  }
-  if constexpr (To29) {
+  if constexpr (To29) {  // x R29 = mont29(x, R29^2); on-curve test y^2 - x^3 - 4 == 0 in radix 29
     using Q = Bls12_381Fp29;
-    const F29<Q> x = fp_to29<Q>(a.x), y = fp_to29<Q>(a.y);
+    F29<Q> x29 = F29<Q>::zero(), y29 = F29<Q>::zero();
+    if (!is_inf) {
+      const Fp<P> x = fp_from_be_words<P>(w, 0), y = fp_from_be_words<P>(w, P::N);
+      if (!fp_raw_lt_mod(x) || !fp_raw_lt_mod(y)) {
+        raise_err(err, DERR_ENCODING);
+        is_inf = true;
+      } else {
+        const F29<Q> r2 = F29<Q>::from_const(Q::R2);
+        x29 = mul29(limbs29<Q>(x.v), r2);  // < p (1 + 2^-24): inputs < p
+        y29 = mul29(limbs29<Q>(y.v), r2);
+        const F29<Q> rhs = add3_29(mul29(sqr29(x29), x29), F29<Q>::from_const(Q::BCURVE), F29<Q>::zero());  // < 2.1 p
+        if (!is_zero29(sub29(sqr29(y29), rhs, Q::B4))) {  // < 5.1 p, within is_zero29's range
+          raise_err(err, DERR_NOT_ON_CURVE);
+          is_inf = true;
+        }
+      }
+      if (is_inf) x29 = y29 = F29<Q>::zero();
+    }
     uint32_t w29[2 * Q::N];
 #pragma unroll
-    for (int k = 0; k < Q::N; ++k) { w29[k] = x.v[k]; w29[Q::N + k] = y.v[k]; }
+    for (int k = 0; k < Q::N; ++k) { w29[k] = x29.v[k]; w29[Q::N + k] = y29.v[k]; }
     uint4* d = reinterpret_cast<uint4*>(pts + i);
 #pragma unroll
     for (int k = 0; k < Q::N / 2; ++k) d[k] = make_uint4(w29[4 * k], w29[4 * k + 1], w29[4 * k + 2], w29[4 * k + 3]);
   } else {
+    Affine<Cv> a;
+    if (is_inf) {
+      a.x = Fp<P>::zero();
+      a.y = Fp<P>::zero();
+    } else {
+      Fp<P> x = fp_from_be_words<P>(w, 0), y = fp_from_be_words<P>(w, P::N);
+      if (!fp_raw_lt_mod(x) || !fp_raw_lt_mod(y)) { raise_err(err, DERR_ENCODING); is_inf = true; }
+      a.x = fp_to_mont(x);
+      a.y = fp_to_mont(y);
+      if (!is_inf && !affine_on_curve(a)) { raise_err(err, DERR_NOT_ON_CURVE); is_inf = true; }
+    }
     uint32_t o[NW];
 #pragma unroll
     for (int k = 0; k < P::N; ++k) { o[k] = a.x.v[k]; o[P::N + k] = a.y.v[k]; }

@@ -97,3 +97,21 @@ def invalid_compressed(C, seed=3):
         cases.append((bytes(b), ERR_ENCODING))
         cases.append((bytes([0x40]) + bytes(n - 2) + b"\x01", ERR_ENCODING))  # infinity + junk
     return cases
+
+
+def invalid_uncompressed(C, rng):
+    """[(encoding, expected error or None = valid identity)] for curve C's uncompressed format
+    (rules of oracle/pyspec/kzg.py g1_from_bytes)."""
+    n = C.fp_bytes
+    P = pc.g1_mul(C.g1, rng.randrange(1, C.r), C)
+    cases = [(C.p.to_bytes(n, "big") + P[1].to_bytes(n, "big"), -2),            # x = p
+             (P[0].to_bytes(n, "big") + (C.p + 1).to_bytes(n, "big"), -2),      # y = p + 1
+             (P[0].to_bytes(n, "big") + ((P[1] + 1) % C.p).to_bytes(n, "big"), -3),
+             ((P[0] + 1).to_bytes(n, "big") + P[1].to_bytes(n, "big"), -3),
+             (bytes(2 * n), -3 if C.name == "bls12_381" else None),            # (0, 0)
+             (pk.g1_to_bytes(None, C), None)]
+    if C.name == "bls12_381":
+        cases += [(bytes([0x80]) + bytes(2 * n - 1), -2),                        # compression bit
+                  (bytes([0x40]) + bytes(2 * n - 2) + b"\x01", -2),              # infinity + junk
+                  (bytes([0x20 | P[0] >> (8 * n - 8)]) + P[0].to_bytes(n, "big")[1:] + P[1].to_bytes(n, "big"), -2)]
+    return cases

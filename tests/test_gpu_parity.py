@@ -104,6 +104,36 @@ def test_errors_and_empty(ctx, curve, golden):
 
 
 @pytest.mark.parametrize("curve", CURVES)
+def test_uncompressed_point_validation(ctx, curve, golden):
+    """Every uncompressed-point rule through the batch conversion (radix-29 store for
+    BLS12-381) and the MSM conversion, against the oracle's MSM on the valid cases."""
+    import kzgmi
+    C = pc.CURVES[curve]
+    g = golden("%s_batch_n4.json" % curve)
+    srs = ctx.load_srs(curve, h(g["g2"]), h(g["tau_g2"]))
+    g1b = 2 * C.fp_bytes
+    cm = h(g["commitments"])
+    rng = random.Random(41)
+    pts = b"".join(pk.g1_to_bytes(pc.g1_mul(C.g1, rng.randrange(1, C.r), C), C) for _ in range(5))
+    sc = b"".join(rng.randrange(C.r).to_bytes(32, "big") for _ in range(5))
+    from pointcases import invalid_uncompressed
+    for enc, err in invalid_uncompressed(C, rng):
+        bad = cm[:g1b] + enc + cm[2 * g1b:]
+        bad_pts = pts[:2 * g1b] + enc + pts[3 * g1b:]
+        if err is None:  # the identity: a valid input that breaks the batch equation
+            assert ctx.batch_verify(srs, bad, h(g["zs"]), h(g["ys"]), h(g["proofs"]), seed=h(g["seed"])) is False
+            assert ctx.msm_g1(curve, bad_pts, sc) == O.msm_g1(curve, bad_pts, sc, 5)
+            continue
+        with pytest.raises(kzgmi.KzgmiError) as e:
+            ctx.batch_verify(srs, bad, h(g["zs"]), h(g["ys"]), h(g["proofs"]), seed=h(g["seed"]))
+        assert e.value.code == err, enc.hex()
+        with pytest.raises(kzgmi.KzgmiError) as e:
+            ctx.msm_g1(curve, bad_pts, sc)
+        assert e.value.code == err, enc.hex()
+    assert ctx.msm_g1(curve, pts, sc) == O.msm_g1(curve, pts, sc, 5)
+
+
+@pytest.mark.parametrize("curve", CURVES)
 def test_msm_random_vs_oracle(ctx, curve):
     C = pc.CURVES[curve]
     rng = random.Random(17)

@@ -151,6 +151,21 @@ def test_invalid_compressed(curve):
             pk.g1_from_bytes_compressed(enc, C)
 
 
+@pytest.mark.parametrize("curve", ["bls12_381", "bn254"])
+def test_invalid_uncompressed_cases(curve):
+    """The uncompressed cases the GPU validation test expects errors for are the ones the
+    Python spec's decoder rejects, and the valid ones decode to the identity."""
+    import random
+    from pointcases import invalid_uncompressed
+    C = pc.CURVES[curve]
+    for enc, want in invalid_uncompressed(C, random.Random(41)):
+        if want is None:
+            assert pk.g1_from_bytes(enc, C) is None
+        else:
+            with pytest.raises(ValueError):
+                pk.g1_from_bytes(enc, C)
+
+
 def test_subgroup_definition():
     """Oracle subgroup check ([r]P == O) on members, random non-members and small-order points."""
     from pointcases import subgroup_cases
