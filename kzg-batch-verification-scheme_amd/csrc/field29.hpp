@@ -51,35 +51,132 @@ KZ_DEV void mad29s(uint64_t& acc, uint32_t a, uint32_t b_uniform) {
 }
 #endif
 
+// Column terms issued up to 4 per asm statement: hipcc pads every inline-asm statement that
+// writes a VGPR with an s_nop before the next VALU reads it (it cannot see that the statement
+// has no dst-sel forwarding hazard), so one mad per statement costs one s_nop per mad; the
+// hardware interlocks a plain dependent v_mad_u64_u32 chain by itself.  The carry-out SGPR is
+// early-clobber ("=&s": an "s" input read by a later instruction must not share it); the
+// accumulator is "+v" -- its register holds its own (64-bit, runtime) value on entry, so no
+// 32-bit input can share it (field.hpp mac32 note: the aliasing case is an accumulator whose
+// value equals an input).  KZ_MAD29_SINGLE: one mad per statement (A/B reference).
+template <int K, int I, int CNT, int NX, int NY>
+KZ_DEV void vv_run(uint64_t& acc, const uint32_t (&x)[NX], const uint32_t (&y)[NY]) {
+  uint64_t cc;
+#ifndef KZ_MAD29_SINGLE
+  if constexpr (CNT >= 4) {
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n\tv_mad_u64_u32 %0, %1, %4, %5, %0\n\t"
+        "v_mad_u64_u32 %0, %1, %6, %7, %0\n\tv_mad_u64_u32 %0, %1, %8, %9, %0"
+        : "+v"(acc), "=&s"(cc)
+        : "v"(x[I]), "v"(y[K - I]), "v"(x[I + 1]), "v"(y[K - I - 1]), "v"(x[I + 2]), "v"(y[K - I - 2]),
+          "v"(x[I + 3]), "v"(y[K - I - 3]));
+    vv_run<K, I + 4, CNT - 4>(acc, x, y);
+  } else if constexpr (CNT == 3) {
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n\tv_mad_u64_u32 %0, %1, %4, %5, %0\n\t"
+        "v_mad_u64_u32 %0, %1, %6, %7, %0"
+        : "+v"(acc), "=&s"(cc)
+        : "v"(x[I]), "v"(y[K - I]), "v"(x[I + 1]), "v"(y[K - I - 1]), "v"(x[I + 2]), "v"(y[K - I - 2]));
+  } else if constexpr (CNT == 2) {
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n\tv_mad_u64_u32 %0, %1, %4, %5, %0"
+        : "+v"(acc), "=&s"(cc)
+        : "v"(x[I]), "v"(y[K - I]), "v"(x[I + 1]), "v"(y[K - I - 1]));
+  } else if constexpr (CNT == 1) {
+    mad29(acc, x[I], y[K - I]);
+  }
+#else
+  if constexpr (CNT >= 1) {
+    mad29(acc, x[I], y[K - I]);
+    vv_run<K, I + 1, CNT - 1>(acc, x, y);
+  }
+#endif
+  (void)cc;
+}
+// m_i MOD_{K-i}, i = I .. I+CNT-1 (MOD limbs: uniform, in SGPRs)
+template <class Q, int K, int I, int CNT>
+KZ_DEV void vs_run(uint64_t& acc, const uint32_t (&m)[Q::N]) {
+  uint64_t cc;
+#ifndef KZ_MAD29_SINGLE
+  if constexpr (CNT >= 4) {
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n\tv_mad_u64_u32 %0, %1, %4, %5, %0\n\t"
+        "v_mad_u64_u32 %0, %1, %6, %7, %0\n\tv_mad_u64_u32 %0, %1, %8, %9, %0"
+        : "+v"(acc), "=&s"(cc)
+        : "v"(m[I]), "s"(Q::MOD[K - I]), "v"(m[I + 1]), "s"(Q::MOD[K - I - 1]), "v"(m[I + 2]),
+          "s"(Q::MOD[K - I - 2]), "v"(m[I + 3]), "s"(Q::MOD[K - I - 3]));
+    vs_run<Q, K, I + 4, CNT - 4>(acc, m);
+  } else if constexpr (CNT == 3) {
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n\tv_mad_u64_u32 %0, %1, %4, %5, %0\n\t"
+        "v_mad_u64_u32 %0, %1, %6, %7, %0"
+        : "+v"(acc), "=&s"(cc)
+        : "v"(m[I]), "s"(Q::MOD[K - I]), "v"(m[I + 1]), "s"(Q::MOD[K - I - 1]), "v"(m[I + 2]),
+          "s"(Q::MOD[K - I - 2]));
+  } else if constexpr (CNT == 2) {
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n\tv_mad_u64_u32 %0, %1, %4, %5, %0"
+        : "+v"(acc), "=&s"(cc)
+        : "v"(m[I]), "s"(Q::MOD[K - I]), "v"(m[I + 1]), "s"(Q::MOD[K - I - 1]));
+  } else if constexpr (CNT == 1) {
+    mad29s(acc, m[I], Q::MOD[K - I]);
+  }
+#else
+  if constexpr (CNT >= 1) {
+    mad29s(acc, m[I], Q::MOD[K - I]);
+    vs_run<Q, K, I + 1, CNT - 1>(acc, m);
+  }
+#endif
+  (void)cc;
+}
+
+// column K of (a b [+ c d] + m p): low columns produce m_K, high ones the result limbs
+template <class Q, bool TWO, int K>
+KZ_DEV void mont29_cols(uint64_t& acc, uint32_t (&m)[Q::N], F29<Q>& t, const F29<Q>& a, const F29<Q>& b,
+                        const F29<Q>& c, const F29<Q>& d) {
+  constexpr int N = Q::N;
+  if constexpr (K < N) {
+    vv_run<K, 0, K + 1>(acc, a.v, b.v);
+    if constexpr (TWO) vv_run<K, 0, K + 1>(acc, c.v, d.v);
+    vs_run<Q, K, 0, K>(acc, m);
+    m[K] = ((uint32_t)acc * Q::INV) & M29;
+    mad29s(acc, m[K], Q::MOD[0]);  // low 29 bits become 0
+    acc >>= 29;
+    mont29_cols<Q, TWO, K + 1>(acc, m, t, a, b, c, d);
+  } else if constexpr (K < 2 * N - 1) {
+    vv_run<K, K - N + 1, 2 * N - 1 - K>(acc, a.v, b.v);
+    if constexpr (TWO) vv_run<K, K - N + 1, 2 * N - 1 - K>(acc, c.v, d.v);
+    vs_run<Q, K, K - N + 1, 2 * N - 1 - K>(acc, m);
+    t.v[K - N] = (uint32_t)acc & M29;
+    acc >>= 29;
+    mont29_cols<Q, TWO, K + 1>(acc, m, t, a, b, c, d);
+  }
+}
+
+// column K of a^2 + m p: off-diagonal a2_i a_{K-i} (i < K - i), the diagonal, m p
+template <class Q, int K>
+KZ_DEV void sqr29_cols(uint64_t& acc, uint32_t (&m)[Q::N], F29<Q>& t, const uint32_t (&a2)[Q::N], const F29<Q>& a) {
+  constexpr int N = Q::N;
+  if constexpr (K < 2 * N - 1) {
+    constexpr int lo = K < N ? 0 : K - N + 1;
+    constexpr int hi = (K - 1) / 2;  // last i with i < K - i
+    if constexpr (K >= 1 && hi >= lo) vv_run<K, lo, hi - lo + 1>(acc, a2, a.v);
+    if constexpr ((K & 1) == 0) mad29(acc, a.v[K / 2], a.v[K / 2]);
+    if constexpr (K < N) {
+      vs_run<Q, K, 0, K>(acc, m);
+      m[K] = ((uint32_t)acc * Q::INV) & M29;
+      mad29s(acc, m[K], Q::MOD[0]);
+    } else {
+      vs_run<Q, K, K - N + 1, 2 * N - 1 - K>(acc, m);
+      t.v[K - N] = (uint32_t)acc & M29;
+    }
+    acc >>= 29;
+    sqr29_cols<Q, K + 1>(acc, m, t, a2, a);
+  }
+}
+
 // (a b [+ c d] + m p) / R29 -- product scanning, one 64-bit accumulator per column
 template <class Q, bool TWO>
 KZ_DEV F29<Q> mont29(const F29<Q>& a, const F29<Q>& b, const F29<Q>& c, const F29<Q>& d) {
-  constexpr int N = Q::N;
-  uint32_t m[N];
+  uint32_t m[Q::N];
   F29<Q> t;
   uint64_t acc = 0;
-  _Pragma("unroll") for (int k = 0; k < N; ++k) {
-    _Pragma("unroll") for (int i = 0; i < k; ++i) {
-      mad29(acc, a.v[i], b.v[k - i]);
-      if constexpr (TWO) mad29(acc, c.v[i], d.v[k - i]);
-      mad29s(acc, m[i], Q::MOD[k - i]);
-    }
-    mad29(acc, a.v[k], b.v[0]);
-    if constexpr (TWO) mad29(acc, c.v[k], d.v[0]);
-    m[k] = ((uint32_t)acc * Q::INV) & M29;
-    mad29s(acc, m[k], Q::MOD[0]);  // low 29 bits become 0
-    acc >>= 29;
-  }
-  _Pragma("unroll") for (int k = N; k < 2 * N - 1; ++k) {
-    _Pragma("unroll") for (int i = k - N + 1; i < N; ++i) {
-      mad29(acc, a.v[i], b.v[k - i]);
-      if constexpr (TWO) mad29(acc, c.v[i], d.v[k - i]);
-      mad29s(acc, m[i], Q::MOD[k - i]);
-    }
-    t.v[k - N] = (uint32_t)acc & M29;
-    acc >>= 29;
-  }
-  t.v[N - 1] = (uint32_t)acc;
+  mont29_cols<Q, TWO, 0>(acc, m, t, a, b, c, d);
+  t.v[Q::N - 1] = (uint32_t)acc;
   return t;
 }
 template <class Q>
@@ -95,25 +192,7 @@ KZ_DEV F29<Q> sqr29(const F29<Q>& a) {
   uint32_t m[N];
   F29<Q> t;
   uint64_t acc = 0;
-  _Pragma("unroll") for (int k = 0; k < N; ++k) {
-    _Pragma("unroll") for (int i = 0; i < k; ++i) {
-      if (i < k - i) mad29(acc, a2[i], a.v[k - i]);
-      mad29s(acc, m[i], Q::MOD[k - i]);
-    }
-    if ((k & 1) == 0) mad29(acc, a.v[k / 2], a.v[k / 2]);
-    m[k] = ((uint32_t)acc * Q::INV) & M29;
-    mad29s(acc, m[k], Q::MOD[0]);
-    acc >>= 29;
-  }
-  _Pragma("unroll") for (int k = N; k < 2 * N - 1; ++k) {
-    _Pragma("unroll") for (int i = k - N + 1; i < N; ++i) {
-      if (i < k - i) mad29(acc, a2[i], a.v[k - i]);
-      mad29s(acc, m[i], Q::MOD[k - i]);
-    }
-    if ((k & 1) == 0) mad29(acc, a.v[k / 2], a.v[k / 2]);
-    t.v[k - N] = (uint32_t)acc & M29;
-    acc >>= 29;
-  }
+  sqr29_cols<Q, 0>(acc, m, t, a2, a);
   t.v[N - 1] = (uint32_t)acc;
   return t;
 }
