@@ -303,7 +303,7 @@ def main():
             ctx.batch_verify_async(srs, s, cc, z, y, pp, n, seed=vseed, compressed=True, subgroup_check=True)
             pending[s] = True
 
-        for k in range(min(4, args.compressed_steps)):
+        for k in range(min(slots, args.compressed_steps)):  # warm every slot's workspace (GLV sizes)
             cstep(k)
         drain()
         barrier()
@@ -363,7 +363,7 @@ def main():
             ctx.batch_verify_async(srs, s, Cm, z, y, P, n, fiat_shamir=True)
             pending[s] = True
 
-        for k in range(min(4, args.fs_steps)):
+        for k in range(min(slots, args.fs_steps)):  # warm every slot's workspace
             fstep(k)
         drain()
         barrier()
