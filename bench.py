@@ -589,10 +589,10 @@ def main():
                        "unique input is inherent to the bucket method, not a re-read to fix",
         "rocprof_kernel_avg_ms": rocprof_ms,
         "rocprof_source": rocprof_src,
-        "timing_note": "kernel_ms = HIP events around k_accumulate + k_from29 + k_fixup of a non-pipelined "
+        "timing_note": "kernel_ms = HIP events around k_accumulate + k_fixup of a non-pipelined "
                        "batch in this run (rocprof_kernel_avg_ms: the same kernels, rocprofv3 kernel trace of "
                        "single batches); kernel_ms_in_pipelined_region includes queueing behind other slots",
-        "kernel": "k_accumulate+k_from29+k_fixup (bucket accumulation, radix 2^29 on BLS12-381)",
+        "kernel": "k_accumulate+k_fixup (bucket accumulation, radix 2^29 on BLS12-381)",
         "kernel_ms": acc_ms,
         "kernel_ms_in_pipelined_region": acc_ms_pipe,
         "algorithmic_bytes": alg_bytes,

@@ -222,9 +222,11 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   CHK(s.total.ensure(16));
   CHK(s.sval.ensure(emax * 4));
   CHK(s.skey.ensure(emax * 4));
-  CHK(s.buckets.ensure((size_t)NB * sizeof(XY)));
-  CHK(s.pfirst.ensure(nchunks * sizeof(XY)));
-  CHK(s.plast.ensure(nchunks * sizeof(XY)));
+  if (!kAcc29<Cv>) {  // BLS12-381 keeps buckets and pieces as radix-29 records in acc29
+    CHK(s.buckets.ensure((size_t)NB * sizeof(XY)));
+    CHK(s.pfirst.ensure(nchunks * sizeof(XY)));
+    CHK(s.plast.ensure(nchunks * sizeof(XY)));
+  }
   if constexpr (kAcc29<Cv>) CHK(s.acc29.ensure(((size_t)NB + 2 * nchunks) * W29 * 4));
   CHK(s.R.ensure((size_t)NB / SEG * sizeof(XY)));
   CHK(s.U.ensure((size_t)NB / SEG * sizeof(XY)));
@@ -248,7 +250,8 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
                 s.buckets.template as<XY>(), s.pfirst.template as<XY>(), s.plast.template as<XY>(),
                 s.acc29.template as<uint32_t>(), NB);
   mark(c, s, PH_ACCUM + 1);
-  L::reduce(st, nsets, s.cnt.template as<uint32_t>(), s.buckets.template as<XY>(), s.R.template as<XY>(),
+  L::reduce(st, nsets, s.cnt.template as<uint32_t>(), s.buckets.template as<XY>(), s.acc29.template as<uint32_t>(),
+            s.R.template as<XY>(),
             s.U.template as<XY>(), s.scratch.template as<XY>(), s.winsum.template as<XY>());
   mark(c, s, PH_REDUCE + 1);
   L::window_combine(st, mw, s.winsum.template as<XY>(), s.res.template as<XY>());

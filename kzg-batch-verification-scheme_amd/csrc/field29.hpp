@@ -130,7 +130,8 @@ KZ_DEV void mont29_cols(uint64_t& acc, uint32_t (&m)[Q::N], F29<Q>& t, const F29
                         const F29<Q>& c, const F29<Q>& d) {
   constexpr int N = Q::N;
   if constexpr (K < N) {
-    vv_run<K, 0, K + 1>(acc, a.v, b.v);
+    if constexpr (K == 0) acc = (uint64_t)a.v[0] * b.v[0];  // compiler's mad with a 0 addend: no zeroed pair
+    else vv_run<K, 0, K + 1>(acc, a.v, b.v);
     if constexpr (TWO) vv_run<K, 0, K + 1>(acc, c.v, d.v);
     vs_run<Q, K, 0, K>(acc, m);
     m[K] = ((uint32_t)acc * Q::INV) & M29;
@@ -155,7 +156,8 @@ KZ_DEV void sqr29_cols(uint64_t& acc, uint32_t (&m)[Q::N], F29<Q>& t, const uint
     constexpr int lo = K < N ? 0 : K - N + 1;
     constexpr int hi = (K - 1) / 2;  // last i with i < K - i
     if constexpr (K >= 1 && hi >= lo) vv_run<K, lo, hi - lo + 1>(acc, a2, a.v);
-    if constexpr ((K & 1) == 0) mad29(acc, a.v[K / 2], a.v[K / 2]);
+    if constexpr (K == 0) acc = (uint64_t)a.v[0] * a.v[0];
+    else if constexpr ((K & 1) == 0) mad29(acc, a.v[K / 2], a.v[K / 2]);
     if constexpr (K < N) {
       vs_run<Q, K, 0, K>(acc, m);
       m[K] = ((uint32_t)acc * Q::INV) & M29;

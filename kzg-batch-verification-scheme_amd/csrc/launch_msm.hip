@@ -28,11 +28,7 @@ void Launch<Cv>::accumulate(hipStream_t st, size_t nchunks, const uint32_t* tota
   // length from the same grid
   const unsigned blocks = grid_for(nchunks, 256);
   k_accumulate<Cv><<<blocks, 256, 0, st>>>(total, sval, skey, off, cnt, pts, buckets, pfirst, plast, acc29, nb);
-  if constexpr (kAcc29<Cv>) {  // radix-29 records -> 32-bit XYZZ buckets and pieces
-    const uint32_t nthreads = blocks * 256u;
-    k_from29<Cv><<<grid_for(nb + 2 * nthreads, 256), 256, 0, st>>>(acc29, nb, nthreads, cnt, buckets, pfirst, plast);
-  }
-  k_fixup<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, pfirst, plast, buckets);
+  k_fixup<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, pfirst, plast, buckets, acc29, nb);
 }
 
 template <class Cv>
@@ -43,10 +39,10 @@ void Launch<Cv>::pts_to29(hipStream_t st, AF* pts, uint32_t n) {
 }
 
 template <class Cv>
-void Launch<Cv>::reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const XY* buckets, XY* R, XY* U,
-                        XY* scratch, XY* winsum) {
+void Launch<Cv>::reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const XY* buckets,
+                        const uint32_t* acc29, XY* R, XY* U, XY* scratch, XY* winsum) {
   const uint32_t nseg = nsets * (NBUCKETS / SEG);
-  k_reduce_segments<Cv><<<grid_for(2 * (size_t)nseg, 256), 256, 0, st>>>(nseg, cnt, buckets, R, U);  // 2 threads per segment
+  k_reduce_segments<Cv><<<grid_for(2 * (size_t)nseg, 256), 256, 0, st>>>(nseg, cnt, buckets, acc29, R, U);  // 2 threads per segment
   // scratch: nsets * RB_PARTS partial sums
   k_reduce_bits<Cv><<<nsets * RB_PARTS, 256, 0, st>>>(R, U, scratch);
   k_reduce_bits_finish<Cv><<<nsets, 64, 0, st>>>(scratch, winsum);
@@ -65,7 +61,7 @@ template void Launch<KZ_CURVE_T>::accumulate(hipStream_t, size_t, const uint32_t
                                              uint32_t);
 template void Launch<KZ_CURVE_T>::pts_to29(hipStream_t, Affine<KZ_CURVE_T>*, uint32_t);
 template void Launch<KZ_CURVE_T>::reduce(hipStream_t, uint32_t, const uint32_t*, const Xyzz<KZ_CURVE_T>*,
-                                         Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*);
+                                         const uint32_t*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*);
 template void Launch<KZ_CURVE_T>::window_combine(hipStream_t, const MsmWindows&, const Xyzz<KZ_CURVE_T>*,
                                                  Xyzz<KZ_CURVE_T>*);
 

@@ -371,8 +371,8 @@ KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_
 // Points arrive converted in place by k_pts_to29 (x in words 0..13, y in 14..27 of each 128-B
 // slot).  Finished bucket pieces are written as radix-29 records of W29 words (x, y, zz, zzz;
 // zz = 0 marks infinity) to `acc29` = [nb bucket records | nthreads first pieces | nthreads
-// last pieces]; k_from29 converts them to the 32-bit XYZZ arrays that k_fixup and the
-// reduction read.  Converting at each flush instead (4 products) would run on most
+// last pieces]; k_fixup joins pieces into records (via the 32-bit form) and k_reduce_segments
+// converts each record as it reads it.  Converting at each flush instead (4 products) would run on most
 // iterations of a wavefront, since some lane changes bucket in almost every step.
 #ifndef KZ_NO_ACC29
 template <class Cv>
@@ -398,16 +398,12 @@ __global__ void __launch_bounds__(256) k_pts_to29(Affine<Cv>* __restrict__ pts, 
   for (int k = 0; k < Q::N / 2; ++k) d[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
 }
 
+// radix-29 record r (x, y, zz, zzz; zz = 0: infinity) <-> 32-bit XYZZ, canonical coordinates
 template <class Cv>
-__global__ void __launch_bounds__(256) k_from29(const uint32_t* __restrict__ acc29, uint32_t nb, uint32_t nthreads,
-                                                const uint32_t* __restrict__ cnt, Xyzz<Cv>* __restrict__ buckets,
-                                                Xyzz<Cv>* __restrict__ part_first, Xyzz<Cv>* __restrict__ part_last) {
+KZ_DEV Xyzz<Cv> load_rec29(const uint32_t* __restrict__ acc29, size_t r) {
   using Q = Bls12_381Fp29;
   using P = typename Cv::FpP;
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nb + 2 * nthreads) return;
-  if (r < nb && cnt[r] == 0) return;  // never written, never read
-  const uint4* s4 = reinterpret_cast<const uint4*>(acc29 + (size_t)r * W29);
+  const uint4* s4 = reinterpret_cast<const uint4*>(acc29 + r * W29);
   uint32_t w[W29];
 #pragma unroll
   for (int k = 0; k < W29 / 4; ++k) {
@@ -422,10 +418,26 @@ __global__ void __launch_bounds__(256) k_from29(const uint32_t* __restrict__ acc
     for (int k = 0; k < Q::N; ++k) c[j].v[k] = w[j * Q::N + k];
 #pragma unroll
   for (int k = 0; k < Q::N; ++k) zz_or |= c[2].v[k];
-  Xyzz<Cv> o = Xyzz<Cv>::inf();
-  if (zz_or) o = {fp_from29<Q, P>(c[0]), fp_from29<Q, P>(c[1]), fp_from29<Q, P>(c[2]), fp_from29<Q, P>(c[3])};
-  Xyzz<Cv>* dst = r < nb ? &buckets[r] : r < nb + nthreads ? &part_first[r - nb] : &part_last[r - nb - nthreads];
-  store_xyzz(dst, o);
+  if (!zz_or) return Xyzz<Cv>::inf();
+  return {fp_from29<Q, P>(c[0]), fp_from29<Q, P>(c[1]), fp_from29<Q, P>(c[2]), fp_from29<Q, P>(c[3])};
+}
+template <class Cv>
+KZ_DEV void store_rec29(uint32_t* __restrict__ acc29, size_t r, const Xyzz<Cv>& v) {
+  using Q = Bls12_381Fp29;
+  uint32_t w[W29];
+  if (v.is_inf()) {
+#pragma unroll
+    for (int k = 0; k < W29; ++k) w[k] = 0;
+  } else {
+    const F29<Q> c[4] = {fp_to29<Q>(v.x), fp_to29<Q>(v.y), fp_to29<Q>(v.zz), fp_to29<Q>(v.zzz)};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < Q::N; ++k) w[j * Q::N + k] = c[j].v[k];
+  }
+  uint4* d4 = reinterpret_cast<uint4*>(acc29 + r * W29);
+#pragma unroll
+  for (int k = 0; k < W29 / 4; ++k) d4[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
 }
 
 // 2Q for an affine Q (rare path: the running sum equals the incoming point), bounds: qx < p,
@@ -672,6 +684,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
 
 // joins the pieces of buckets that cross chunk boundaries (launched with the same grid as
 // k_accumulate, so acc_chunk_len agrees)
+// BLS12-381 (kAcc29): the pieces and the bucket are radix-29 records of acc29 = [nb buckets |
+// nthreads first pieces | nthreads last pieces], joined in the 32-bit form (few buckets cross a
+// chunk boundary) and written back as a record that k_reduce_segments reads.
 template <class Cv>
 __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ total_p,
                                                const uint32_t* __restrict__ sorted_key,
@@ -679,7 +694,8 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
                                                const uint32_t* __restrict__ cnt,
                                                const Xyzz<Cv>* __restrict__ part_first,
                                                const Xyzz<Cv>* __restrict__ part_last,
-                                               Xyzz<Cv>* __restrict__ buckets) {
+                                               Xyzz<Cv>* __restrict__ buckets, uint32_t* __restrict__ acc29,
+                                               uint32_t nb) {
   KZ_TAIL_PRIO();
   const uint32_t total = *total_p;
   const uint32_t len = acc_chunk_len(total, gridDim.x * blockDim.x);
@@ -692,9 +708,16 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
   uint32_t c0 = o / len;
   if (c0 != c - 1) return;                // a later continuation chunk: handled by c0+1
   uint32_t c1 = (o + cnt[key] - 1) / len;
-  Xyzz<Cv> acc = load_xyzz(&part_last[c0]);
-  for (uint32_t cc = c; cc <= c1; ++cc) acc = xyzz_add(acc, load_xyzz(&part_first[cc]));
-  store_xyzz(&buckets[key], acc);
+  if constexpr (kAcc29<Cv>) {
+    const size_t nthreads = (size_t)gridDim.x * blockDim.x;
+    Xyzz<Cv> acc = load_rec29<Cv>(acc29, nb + nthreads + c0);
+    for (uint32_t cc = c; cc <= c1; ++cc) acc = xyzz_add(acc, load_rec29<Cv>(acc29, nb + cc));
+    store_rec29<Cv>(acc29, key, acc);
+  } else {
+    Xyzz<Cv> acc = load_xyzz(&part_last[c0]);
+    for (uint32_t cc = c; cc <= c1; ++cc) acc = xyzz_add(acc, load_xyzz(&part_first[cc]));
+    store_xyzz(&buckets[key], acc);
+  }
 }
 
 // ------------------------------------------------------------------------------ reduction
@@ -707,20 +730,26 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
 template <class Cv>
 __global__ void __launch_bounds__(256) k_reduce_segments(uint32_t nseg, const uint32_t* __restrict__ cnt,
                                                          const Xyzz<Cv>* __restrict__ buckets,
+                                                         const uint32_t* __restrict__ acc29,
                                                          Xyzz<Cv>* __restrict__ R, Xyzz<Cv>* __restrict__ U) {
   static_assert(SEG == 16, "two 8-bucket halves per segment");
   KZ_TAIL_PRIO();
   __shared__ __attribute__((aligned(16))) Xyzz<Cv> xch[256];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t g = t >> 1, h = t & 1;
+  // bucket b: the accumulation's radix-29 record (BLS12-381, converted here) or 32-bit XYZZ
+  auto bucket = [&](uint32_t b) {
+    if constexpr (kAcc29<Cv>) return load_rec29<Cv>(acc29, b);
+    else return load_xyzz(&buckets[b]);
+  };
   Xyzz<Cv> run = Xyzz<Cv>::inf(), acc = Xyzz<Cv>::inf();
   if (g < nseg) {
     const uint32_t base = g * SEG + 8 * h;
     for (int i = 7; i >= 1; --i) {
-      if (cnt[base + i]) run = xyzz_add_c(run, load_xyzz(&buckets[base + i]));
+      if (cnt[base + i]) run = xyzz_add_c(run, bucket(base + i));
       acc = xyzz_add_c(acc, run);
     }
-    if (cnt[base]) run = xyzz_add_c(run, load_xyzz(&buckets[base]));
+    if (cnt[base]) run = xyzz_add_c(run, bucket(base));
     if (h == 1) acc = xyzz_add_c(acc, xyzz_dbl_c(xyzz_dbl_c(xyzz_dbl_c(run))));  // R_1 + 8 U_1
   }
   // h = 0 needs the partner's R_1 + 8 U_1, h = 1 the partner's U_0
