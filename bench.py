@@ -50,6 +50,7 @@ HBM_PEAK = 8.0e12          # B/s, MI355X spec (MI355X_MICROARCH.md)
 TAU = 0x2A1B3C4D5E6F708192A3B4C5D6E7F8091A2B3C4D5E6F7081
 BYTES_PER_TUPLE = {"bls12_381": 256, "bn254": 192}
 BYTES_PER_MSM_POINT = {"bls12_381": 128, "bn254": 96}
+VALU_PER_ADD = 4602  # BLS12-381 k_accumulate, SQ_INSTS_VALU x 64 / 32n (profiles/r02/pmc_sq_accumulate.json)
 PROFILE_ROUND = "r02"      # profiles/<round>/rocprof_single: the committed rocprofv3 summaries
 
 
@@ -575,6 +576,7 @@ def main():
     # x SIMDs x 64 lanes / 392 mads per radix-2^29 product (14 x 14 for a b + 14 x 14 for m p)
     n_simd = 4 * torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
     mad_floor = 0.4596e9 * n_simd * 64 / 392 if curve == "bls12_381" else None
+    valu_floor_ms = (32 * n * VALU_PER_ADD / 64) / (0.4474e6 * n_simd) if curve == "bls12_381" else None
     roofline = {
         "bound": "hbm",
         "achieved": achieved / 1e9 if achieved else None,
@@ -611,6 +613,17 @@ def main():
                 "peak_fpmul_per_s": mad_floor,
                 "frac": (acc_fpmuls / (acc_ms * 1e-3)) / mad_floor if (mad_floor and acc_ms > 0) else None,
             },
+            # every VALU instruction of the loop (SQ_INSTS_VALU per addition, profiles/r02/
+            # pmc_sq_accumulate.json) at the issue rate a dependent mad chain reaches with the
+            # kernel's 4 waves per SIMD (profiles/r02/probes/mad_rate_blocks.txt): the time the
+            # kernel's instruction stream needs at that rate, over the measured accumulation phase
+            "valu_issue_floor": {
+                "valu_instr_per_addition": VALU_PER_ADD, "issue_rate_per_simd_ns": 0.4474, "simds": n_simd,
+                "source": "profiles/r02/pmc_sq_accumulate.json + profiles/r02/probes/mad_rate_blocks.txt "
+                          "('mad chain x8, 4/statement', 4 waves/SIMD)",
+                "floor_ms": valu_floor_ms,
+                "frac": valu_floor_ms / acc_ms if (valu_floor_ms and acc_ms > 0) else None,
+            } if valu_floor_ms else None,
             # whole pipeline: accumulation products per second of wall time (batches/s x
             # products per batch) against the probe peak -- what the overlap actually sustains
             "pipeline_frac": acc_fpmuls * value / world / fpmul_peak,

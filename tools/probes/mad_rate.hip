@@ -14,6 +14,11 @@
 #define MOV(x, y) asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(y))
 #define MULLO(x, y) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x) : "v"(y))
 #define U24(x, y) asm volatile("v_mad_u32_u24 %0, %0, %1, %0" : "+v"(x) : "v"(y))
+// 4 mads per statement: independent accumulators (MAD4I) or one dependent chain (MAD4D)
+#define MAD4I(c0, c1, c2, c3, a, b) asm volatile("v_mad_u64_u32 %0, %4, %5, %6, %0\n\tv_mad_u64_u32 %1, %4, %5, %6, %1\n\t" \
+    "v_mad_u64_u32 %2, %4, %5, %6, %2\n\tv_mad_u64_u32 %3, %4, %5, %6, %3" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "=&s"(cc) : "v"(a), "v"(b))
+#define MAD4D(c0, a, b) asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0\n\tv_mad_u64_u32 %0, %1, %3, %2, %0\n\t" \
+    "v_mad_u64_u32 %0, %1, %2, %3, %0\n\tv_mad_u64_u32 %0, %1, %3, %2, %0" : "+v"(c0), "=&s"(cc) : "v"(a), "v"(b))
 #define FMA64(x, y) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(x) : "v"(y))
 
 template <int MODE>
@@ -43,6 +48,15 @@ __global__ void __launch_bounds__(256) k_probe(uint32_t* out, int iters, uint32_
       U24(t0, a); U24(t1, a); U24(t2, a); U24(t3, a); U24(t4, a); U24(t5, a); U24(t6, a); U24(t7, a);
     } else if constexpr (MODE == 6) {  // 8 v_fma_f64
       FMA64(d0, dy); FMA64(d1, dy); FMA64(d2, dy); FMA64(d3, dy); FMA64(d4, dy); FMA64(d5, dy); FMA64(d6, dy); FMA64(d7, dy);
+    } else if constexpr (MODE == 8) {  // 8 independent mads, 4 per statement
+      MAD4I(acc0, acc1, acc2, acc3, a, b); MAD4I(acc4, acc5, acc6, acc7, a, b);
+    } else if constexpr (MODE == 9) {  // one dependent chain of 8 mads, 4 per statement
+      MAD4D(acc0, a, b); MAD4D(acc0, a, b);
+    } else if constexpr (MODE == 10) {  // one dependent chain of 8 mads, 1 per statement
+      MAD(acc0, a, b); MAD(acc0, a, b); MAD(acc0, a, b); MAD(acc0, a, b);
+      MAD(acc0, a, b); MAD(acc0, a, b); MAD(acc0, a, b); MAD(acc0, a, b);
+    } else if constexpr (MODE == 11) {  // two dependent chains, 4 per statement, alternating
+      MAD4D(acc0, a, b); MAD4D(acc1, a, b);
     } else if constexpr (MODE == 7) {  // 8 mad + 8 add_co
       MAD(acc0, a, b); ADDC(t0, a); MAD(acc1, a, b); ADDC(t1, a); MAD(acc2, a, b); ADDC(t2, a); MAD(acc3, a, b); ADDC(t3, a);
       MAD(acc4, a, b); ADDC(t4, a); MAD(acc5, a, b); ADDC(t5, a); MAD(acc6, a, b); ADDC(t6, a); MAD(acc7, a, b); ADDC(t7, a);
@@ -79,7 +93,7 @@ static void run(const char* name, int instr_per_iter, int waves_per_simd) {
 }
 
 int main() {
-  for (int w : {2, 4, 8}) {
+  for (int w : {1, 2, 3, 4, 8}) {
     run<0>("mad_u64_u32 x8", 8, w);
     run<1>("mad+addc (mac32) x8", 16, w);
     run<2>("add_co_u32 x8", 8, w);
@@ -88,6 +102,10 @@ int main() {
     run<4>("mul_lo_u32 x8", 8, w);
     run<5>("mad_u32_u24 x8", 8, w);
     run<6>("fma_f64 x8", 8, w);
+    run<8>("mad x8 indep, 4/statement", 8, w);
+    run<9>("mad chain x8, 4/statement", 8, w);
+    run<10>("mad chain x8, 1/statement", 8, w);
+    run<11>("2 mad chains, 4/statement", 8, w);
   }
   return 0;
 }
