@@ -176,22 +176,30 @@ static __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __rest
   if (threadIdx.x == 1023) *total = s[1023];
 }
 
+// Entries are ranked per coarse bin in LDS, staged in bin order, and written out so that
+// consecutive threads store consecutive addresses of a bin's run (the tile's run in each bin
+// is contiguous in `tmp`); writing each entry from the thread that ranked it scattered every
+// wavefront store over ~64 bins.
 static __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t* __restrict__ digits,
                                                      uint32_t* __restrict__ coarse_cursor,
                                                      uint64_t* __restrict__ tmp) {
   __shared__ uint32_t hist[BINS_PER_SET];
-  __shared__ uint32_t base[BINS_PER_SET];
+  __shared__ uint32_t base[BINS_PER_SET];   // global start of this tile's run in bin b
+  __shared__ uint32_t lstart[BINS_PER_SET]; // local (staged) start of bin b
+  __shared__ uint64_t stage[TILE_TERMS];
+  __shared__ uint8_t stage_bin[TILE_TERMS];
   const TileRef T = tile_decode(tl, blockIdx.x);
   const TermClass& C = tl.c[T.k];
   const uint32_t set = C.set_base + T.w;
   const uint32_t* dg = digits + C.dig_base + (size_t)T.w * C.count;
-  hist[threadIdx.x] = 0;
+  const uint32_t t = threadIdx.x;
+  hist[t] = 0;
   __syncthreads();
   uint32_t rank[TILE_TERMS / 256], key[TILE_TERMS / 256], ent[TILE_TERMS / 256];
 #pragma unroll
   for (int j = 0; j < TILE_TERMS / 256; ++j) {
     key[j] = 0xffffffffu;
-    const uint32_t local = T.c * TILE_TERMS + j * 256 + threadIdx.x;
+    const uint32_t local = T.c * TILE_TERMS + j * 256 + t;
     const uint32_t code = local < C.count ? dg[local] : 0u;
     if (!code) continue;
     const uint32_t mag = code & 0x7fffffffu;
@@ -200,13 +208,32 @@ static __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const u
     rank[j] = atomicAdd(&hist[(mag - 1) >> COARSE_SHIFT], 1u);
   }
   __syncthreads();
-  uint32_t h = hist[threadIdx.x];
-  base[threadIdx.x] = h ? atomicAdd(&coarse_cursor[set * BINS_PER_SET + threadIdx.x], h) : 0u;
+  const uint32_t h = hist[t];
+  base[t] = h ? atomicAdd(&coarse_cursor[set * BINS_PER_SET + t], h) : 0u;
+  lstart[t] = h;
+  __syncthreads();
+  for (int d = 1; d < BINS_PER_SET; d <<= 1) {  // inclusive scan of the tile's bin counts
+    const uint32_t x = t >= (uint32_t)d ? lstart[t - d] : 0u;
+    __syncthreads();
+    lstart[t] += x;
+    __syncthreads();
+  }
+  const uint32_t ntile = lstart[BINS_PER_SET - 1];
+  __syncthreads();
+  lstart[t] -= h;  // exclusive
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < TILE_TERMS / 256; ++j) {
     if (key[j] == 0xffffffffu) continue;
-    tmp[base[(key[j] >> COARSE_SHIFT) & (BINS_PER_SET - 1)] + rank[j]] = ((uint64_t)key[j] << 32) | ent[j];
+    const uint32_t bin = (key[j] >> COARSE_SHIFT) & (BINS_PER_SET - 1);
+    const uint32_t q = lstart[bin] + rank[j];
+    stage[q] = ((uint64_t)key[j] << 32) | ent[j];
+    stage_bin[q] = (uint8_t)bin;
+  }
+  __syncthreads();
+  for (uint32_t q = t; q < ntile; q += 256) {
+    const uint32_t bin = stage_bin[q];
+    tmp[base[bin] + (q - lstart[bin])] = stage[q];
   }
 }
 
