@@ -398,8 +398,8 @@ KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_
 // Points arrive converted in place by k_pts_to29 (x in words 0..13, y in 14..27 of each 128-B
 // slot).  Finished bucket pieces are written as radix-29 records of W29 words (x, y, zz, zzz;
 // zz = 0 marks infinity) to `acc29` = [nb bucket records | nthreads first pieces | nthreads
-// last pieces]; k_fixup joins pieces into records (via the 32-bit form) and k_reduce_segments
-// converts each record as it reads it.  Converting at each flush instead (4 products) would run on most
+// last pieces]; k_fixup joins pieces into records and k_reduce_segments runs its running sums on
+// the records, both with the radix-29 XYZZ addition (x29_add below).  Converting at each flush instead (4 products) would run on most
 // iterations of a wavefront, since some lane changes bucket in almost every step.
 #ifndef KZ_NO_ACC29
 template <class Cv>
@@ -425,11 +425,17 @@ __global__ void __launch_bounds__(256) k_pts_to29(Affine<Cv>* __restrict__ pts, 
   for (int k = 0; k < Q::N / 2; ++k) d[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
 }
 
-// radix-29 record r (x, y, zz, zzz; zz = 0: infinity) <-> 32-bit XYZZ, canonical coordinates
-template <class Cv>
-KZ_DEV Xyzz<Cv> load_rec29(const uint32_t* __restrict__ acc29, size_t r) {
-  using Q = Bls12_381Fp29;
-  using P = typename Cv::FpP;
+// ------------------------------------------------------------------------------ radix-29 XYZZ
+// A bucket record as loaded for the reduction: coordinates in radix 2^29 (record bounds:
+// x < 10p, y < 16p, zz, zzz < 2p) and an explicit infinity flag.
+template <class Q>
+struct X29 {
+  F29<Q> x, y, zz, zzz;
+  bool inf;
+};
+template <class Q>
+KZ_DEV X29<Q> load_x29(const uint32_t* __restrict__ acc29, size_t r) {
+  constexpr int N = Q::N;
   const uint4* s4 = reinterpret_cast<const uint4*>(acc29 + r * W29);
   uint32_t w[W29];
 #pragma unroll
@@ -437,35 +443,77 @@ KZ_DEV Xyzz<Cv> load_rec29(const uint32_t* __restrict__ acc29, size_t r) {
     const uint4 q = s4[k];
     w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w;
   }
-  F29<Q> c[4];
+  X29<Q> o;
   uint32_t zz_or = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int k = 0; k < Q::N; ++k) c[j].v[k] = w[j * Q::N + k];
-#pragma unroll
-  for (int k = 0; k < Q::N; ++k) zz_or |= c[2].v[k];
-  if (!zz_or) return Xyzz<Cv>::inf();
-  return {fp_from29<Q, P>(c[0]), fp_from29<Q, P>(c[1]), fp_from29<Q, P>(c[2]), fp_from29<Q, P>(c[3])};
+  for (int k = 0; k < N; ++k) {
+    o.x.v[k] = w[k];
+    o.y.v[k] = w[N + k];
+    o.zz.v[k] = w[2 * N + k];
+    o.zzz.v[k] = w[3 * N + k];
+    zz_or |= w[2 * N + k];
+  }
+  o.inf = zz_or == 0;
+  return o;
 }
-template <class Cv>
-KZ_DEV void store_rec29(uint32_t* __restrict__ acc29, size_t r, const Xyzz<Cv>& v) {
-  using Q = Bls12_381Fp29;
+template <class Q>
+KZ_DEV void store_x29(uint32_t* __restrict__ acc29, size_t r, const X29<Q>& a) {
+  constexpr int N = Q::N;
   uint32_t w[W29];
-  if (v.is_inf()) {
 #pragma unroll
-    for (int k = 0; k < W29; ++k) w[k] = 0;
-  } else {
-    const F29<Q> c[4] = {fp_to29<Q>(v.x), fp_to29<Q>(v.y), fp_to29<Q>(v.zz), fp_to29<Q>(v.zzz)};
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int k = 0; k < Q::N; ++k) w[j * Q::N + k] = c[j].v[k];
+  for (int k = 0; k < N; ++k) {
+    w[k] = a.x.v[k];
+    w[N + k] = a.y.v[k];
+    w[2 * N + k] = a.inf ? 0u : a.zz.v[k];  // zz = 0 marks infinity
+    w[3 * N + k] = a.zzz.v[k];
   }
   uint4* d4 = reinterpret_cast<uint4*>(acc29 + r * W29);
 #pragma unroll
   for (int k = 0; k < W29 / 4; ++k) d4[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
 }
+template <class Cv, class Q>
+KZ_DEV Xyzz<Cv> x29_to32(const X29<Q>& a) {
+  using P = typename Cv::FpP;
+  if (a.inf) return Xyzz<Cv>::inf();
+  return {fp_from29<Q, P>(a.x), fp_from29<Q, P>(a.y), fp_from29<Q, P>(a.zz), fp_from29<Q, P>(a.zzz)};
+}
+// a + a through the 32-bit doubling (P == 0 and R == 0 in x29_add: equal points, rare)
+template <class Cv, class Q>
+__device__ __noinline__ X29<Q> x29_dbl_via32(const X29<Q> a) {
+  const Xyzz<Cv> d = xyzz_dbl(x29_to32<Cv, Q>(a));
+  if (d.is_inf()) return {F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), true};
+  return {fp_to29<Q>(d.x), fp_to29<Q>(d.y), fp_to29<Q>(d.zz), fp_to29<Q>(d.zzz), false};
+}
+// a + b (add-2008-s, 12M + 2S with the Y3 pair sharing one reduction).  Inputs within the record
+// bounds (x < 10p, y < 16p, zz, zzz < 2p); outputs x < 9.1p, y, zz, zzz < 1.01p -- inside them.
+template <class Cv, class Q>
+KZ_DEV X29<Q> x29_add(const X29<Q>& a, const X29<Q>& b) {
+  using G = F29<Q>;
+  if (a.inf) return b;
+  if (b.inf) return a;
+  const G U1 = mul29(a.x, b.zz), U2 = mul29(b.x, a.zz);    // < 1.01p
+  const G S1 = mul29(a.y, b.zzz), S2 = mul29(b.y, a.zzz);
+  const G P = sub29(U2, U1, Q::B2);                         // < 3.02p
+  const G R = sub29(S2, S1, Q::B2);
+  if (is_zero29(P)) {
+    if (is_zero29(R)) return x29_dbl_via32<Cv, Q>(a);
+    return {G::zero(), G::zero(), G::zero(), G::zero(), true};
+  }
+  const G PP = sqr29(P);
+  const G PPP = mul29(P, PP);
+  const G Q2 = mul29(U1, PP);
+  X29<Q> o;
+  o.x = sub29(sqr29(R), add3_29(PPP, Q2, Q2), Q::B8);                           // < 9.1p
+  o.y = mul2_29(R, sub29(Q2, o.x, Q::B16), S1, sub29(G::zero(), PPP, Q::B8));  // R (Q - X3) - S1 PPP
+  o.zz = mul29(mul29(a.zz, b.zz), PP);
+  o.zzz = mul29(mul29(a.zzz, b.zzz), PPP);
+  o.inf = false;
+  return o;
+}
+
+// out of line for the latency-bound reduction (keeps its register peak at 2 waves per SIMD)
+template <class Cv, class Q>
+__device__ __noinline__ X29<Q> x29_add_c(const X29<Q> a, const X29<Q> b) { return x29_add<Cv, Q>(a, b); }
 
 // 2Q for an affine Q (rare path: the running sum equals the incoming point), bounds: qx < p,
 // qy < 8p in; x < 10p, y < 10p, zz, zzz < 2p out
@@ -712,8 +760,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
 // joins the pieces of buckets that cross chunk boundaries (launched with the same grid as
 // k_accumulate, so acc_chunk_len agrees)
 // BLS12-381 (kAcc29): the pieces and the bucket are radix-29 records of acc29 = [nb buckets |
-// nthreads first pieces | nthreads last pieces], joined in the 32-bit form (few buckets cross a
-// chunk boundary) and written back as a record that k_reduce_segments reads.
+// nthreads first pieces | nthreads last pieces], joined with the radix-29 XYZZ addition and
+// written back as the record k_reduce_segments reads.
 template <class Cv>
 __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ total_p,
                                                const uint32_t* __restrict__ sorted_key,
@@ -737,9 +785,10 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
   uint32_t c1 = (o + cnt[key] - 1) / len;
   if constexpr (kAcc29<Cv>) {
     const size_t nthreads = (size_t)gridDim.x * blockDim.x;
-    Xyzz<Cv> acc = load_rec29<Cv>(acc29, nb + nthreads + c0);
-    for (uint32_t cc = c; cc <= c1; ++cc) acc = xyzz_add(acc, load_rec29<Cv>(acc29, nb + cc));
-    store_rec29<Cv>(acc29, key, acc);
+    using Q = Bls12_381Fp29;
+    X29<Q> acc = load_x29<Q>(acc29, nb + nthreads + c0);
+    for (uint32_t cc = c; cc <= c1; ++cc) acc = x29_add<Cv, Q>(acc, load_x29<Q>(acc29, nb + cc));
+    store_x29<Q>(acc29, key, acc);
   } else {
     Xyzz<Cv> acc = load_xyzz(&part_last[c0]);
     for (uint32_t cc = c; cc <= c1; ++cc) acc = xyzz_add(acc, load_xyzz(&part_first[cc]));
@@ -755,7 +804,7 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
 // R_g = R_0 + (R_1 + 8 U_1), U_g = U_0 + U_1 after one LDS exchange: a chain of ~20 point
 // operations instead of 31 (the kernel is latency-bound at < 1 wave per SIMD; 1.14 ms before).
 template <class Cv>
-__global__ void __launch_bounds__(256) k_reduce_segments(uint32_t nseg, const uint32_t* __restrict__ cnt,
+__global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const uint32_t* __restrict__ cnt,
                                                          const Xyzz<Cv>* __restrict__ buckets,
                                                          const uint32_t* __restrict__ acc29,
                                                          Xyzz<Cv>* __restrict__ R, Xyzz<Cv>* __restrict__ U) {
@@ -764,19 +813,27 @@ __global__ void __launch_bounds__(256) k_reduce_segments(uint32_t nseg, const ui
   __shared__ __attribute__((aligned(16))) Xyzz<Cv> xch[256];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t g = t >> 1, h = t & 1;
-  // bucket b: the accumulation's radix-29 record (BLS12-381, converted here) or 32-bit XYZZ
-  auto bucket = [&](uint32_t b) {
-    if constexpr (kAcc29<Cv>) return load_rec29<Cv>(acc29, b);
-    else return load_xyzz(&buckets[b]);
-  };
   Xyzz<Cv> run = Xyzz<Cv>::inf(), acc = Xyzz<Cv>::inf();
   if (g < nseg) {
     const uint32_t base = g * SEG + 8 * h;
-    for (int i = 7; i >= 1; --i) {
-      if (cnt[base + i]) run = xyzz_add_c(run, bucket(base + i));
-      acc = xyzz_add_c(acc, run);
+    if constexpr (kAcc29<Cv>) {  // BLS12-381: the running sums in radix 2^29 on the records
+      using Q = Bls12_381Fp29;
+      const X29<Q> O{F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), true};
+      X29<Q> run29 = O, acc29v = O;
+      for (int i = 7; i >= 1; --i) {
+        if (cnt[base + i]) run29 = x29_add_c<Cv, Q>(run29, load_x29<Q>(acc29, base + i));
+        acc29v = x29_add_c<Cv, Q>(acc29v, run29);
+      }
+      if (cnt[base]) run29 = x29_add_c<Cv, Q>(run29, load_x29<Q>(acc29, base));
+      run = x29_to32<Cv, Q>(run29);
+      acc = x29_to32<Cv, Q>(acc29v);
+    } else {
+      for (int i = 7; i >= 1; --i) {
+        if (cnt[base + i]) run = xyzz_add_c(run, load_xyzz(&buckets[base + i]));
+        acc = xyzz_add_c(acc, run);
+      }
+      if (cnt[base]) run = xyzz_add_c(run, load_xyzz(&buckets[base]));
     }
-    if (cnt[base]) run = xyzz_add_c(run, bucket(base));
     if (h == 1) acc = xyzz_add_c(acc, xyzz_dbl_c(xyzz_dbl_c(xyzz_dbl_c(run))));  // R_1 + 8 U_1
   }
   // h = 0 needs the partner's R_1 + 8 U_1, h = 1 the partner's U_0
