@@ -619,8 +619,8 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t len, uint32_t chun
       const G S2 = mul29(qy, ld(s_zzz));
       const G P = sub29(U2, x, Q::B16);  // < 18p
       const G R = sub29(S2, y, Q::B16);  // < 18p
-      if (is_zero29(P)) {
-        if (is_zero29(R)) {
+      if (is_zero29_mf(P)) {
+        if (is_zero29_mf(R)) {
           dbl = true;
           break;
         }
