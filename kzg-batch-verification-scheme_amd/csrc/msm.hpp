@@ -821,10 +821,10 @@ __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const
       const X29<Q> O{F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), true};
       X29<Q> run29 = O, acc29v = O;
       for (int i = 7; i >= 1; --i) {
-        if (cnt[base + i]) run29 = x29_add_c<Cv, Q>(run29, load_x29<Q>(acc29, base + i));
-        acc29v = x29_add_c<Cv, Q>(acc29v, run29);
+        if (cnt[base + i]) run29 = x29_add<Cv, Q>(run29, load_x29<Q>(acc29, base + i));
+        acc29v = x29_add<Cv, Q>(acc29v, run29);
       }
-      if (cnt[base]) run29 = x29_add_c<Cv, Q>(run29, load_x29<Q>(acc29, base));
+      if (cnt[base]) run29 = x29_add<Cv, Q>(run29, load_x29<Q>(acc29, base));
       run = x29_to32<Cv, Q>(run29);
       acc = x29_to32<Cv, Q>(acc29v);
     } else {
