@@ -511,6 +511,27 @@ KZ_DEV X29<Q> x29_add(const X29<Q>& a, const X29<Q>& b) {
   return o;
 }
 
+// 2a (dbl-2008-s-1, a = 0).  Inputs within the record bounds; outputs x < 5.1p, y, zz, zzz <
+// 1.01p.  BLS12-381 G1 has no 2-torsion (#E(Fp) is odd), so only O doubles to O.
+template <class Q>
+KZ_DEV X29<Q> x29_dbl(const X29<Q>& a) {
+  using G = F29<Q>;
+  if (a.inf) return a;
+  const G U = add3_29(a.y, a.y, G::zero());  // < 32p
+  const G V = sqr29(U);
+  const G W = mul29(U, V);
+  const G S = mul29(a.x, V);
+  const G X2 = sqr29(a.x);
+  const G M = add3_29(X2, X2, X2);           // < 3.03p
+  X29<Q> o;
+  o.x = sub29(sqr29(M), add3_29(S, S, G::zero()), Q::B4);                    // < 5.1p
+  o.y = mul2_29(M, sub29(S, o.x, Q::B8), W, sub29(G::zero(), a.y, Q::B16));  // M (S - X3) - W Y
+  o.zz = mul29(V, a.zz);
+  o.zzz = mul29(W, a.zzz);
+  o.inf = false;
+  return o;
+}
+
 // out of line for the latency-bound reduction (keeps its register peak at 2 waves per SIMD)
 template <class Cv, class Q>
 __device__ __noinline__ X29<Q> x29_add_c(const X29<Q> a, const X29<Q> b) { return x29_add<Cv, Q>(a, b); }
@@ -825,6 +846,7 @@ __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const
         acc29v = x29_add<Cv, Q>(acc29v, run29);
       }
       if (cnt[base]) run29 = x29_add<Cv, Q>(run29, load_x29<Q>(acc29, base));
+      if (h == 1) acc29v = x29_add<Cv, Q>(acc29v, x29_dbl<Q>(x29_dbl<Q>(x29_dbl<Q>(run29))));  // R_1 + 8 U_1
       run = x29_to32<Cv, Q>(run29);
       acc = x29_to32<Cv, Q>(acc29v);
     } else {
@@ -834,7 +856,8 @@ __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const
       }
       if (cnt[base]) run = xyzz_add_c(run, load_xyzz(&buckets[base]));
     }
-    if (h == 1) acc = xyzz_add_c(acc, xyzz_dbl_c(xyzz_dbl_c(xyzz_dbl_c(run))));  // R_1 + 8 U_1
+    if constexpr (!kAcc29<Cv>)
+      if (h == 1) acc = xyzz_add_c(acc, xyzz_dbl_c(xyzz_dbl_c(xyzz_dbl_c(run))));  // R_1 + 8 U_1
   }
   // h = 0 needs the partner's R_1 + 8 U_1, h = 1 the partner's U_0
   store_xyzz(&xch[threadIdx.x], h ? acc : run);
