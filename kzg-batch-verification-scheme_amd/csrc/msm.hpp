@@ -875,7 +875,7 @@ KZ_DEV Xyzz<Cv> block_sum256(Xyzz<Cv> v, Xyzz<Cv>* lds) {
   for (int s = 128; s >= 1; s >>= 1) {
     if (t >= s && t < 2 * s) store_xyzz(&lds[t - s], v);
     __syncthreads();
-    if (t < s) v = xyzz_add_c(v, load_xyzz(&lds[t]));
+    if (t < s) v = xyzz_add(v, load_xyzz(&lds[t]));
     __syncthreads();
   }
   return v;  // valid in thread 0
@@ -907,15 +907,15 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
     for (uint32_t i = 0; i < 4; ++i) {  // q: 10-bit rank among the g with bit j set
       const uint32_t q = t + 256 * i;
       const uint32_t g = ((q >> j) << (j + 1)) | (1u << j) | (q & ((1u << j) - 1));
-      s = xyzz_add_c(s, load_xyzz(&Us[g]));
+      s = xyzz_add(s, load_xyzz(&Us[g]));
     }
   } else {
     const uint32_t base = (j - 11) * (NSEG / 4);
 #pragma unroll 1
     for (uint32_t i = 0; i < 2; ++i) {
       const uint32_t g = base + t + 256 * i;
-      s = xyzz_add_c(s, load_xyzz(&Rs[g]));
-      s = xyzz_add_c(s, load_xyzz(&Us[g]));
+      s = xyzz_add(s, load_xyzz(&Rs[g]));
+      s = xyzz_add(s, load_xyzz(&Us[g]));
     }
   }
   const Xyzz<Cv> v = block_sum256(s, lds);
