@@ -538,26 +538,32 @@ __device__ __noinline__ X29<Q> x29_add_c(const X29<Q> a, const X29<Q> b) { retur
 
 // 2Q for an affine Q (rare path: the running sum equals the incoming point), bounds: qx < p,
 // qy < 8p in; x < 10p, y < 10p, zz, zzz < 2p out
+// out of line: its temporaries would otherwise raise the loop's register peak.  ZZ, ZZZ go
+// straight to the caller's LDS columns (stride 256 words) so that arguments and result fit the
+// 32 argument/return VGPRs of a call -- a 56-word return travelled through scratch (304 B of
+// private segment per lane for the whole accumulation grid).
 template <class Q>
-struct Xyzz29 {
-  F29<Q> x, y, zz, zzz;
+struct Xy29 {
+  F29<Q> x, y;
 };
-// out of line: its temporaries would otherwise raise the loop's register peak
 template <class Q>
-__device__ __noinline__ Xyzz29<Q> dbl_affine29(const F29<Q> qx, const F29<Q> qy) {
+__device__ __noinline__ Xy29<Q> dbl_affine29(const F29<Q> qx, const F29<Q> qy, uint32_t* zz, uint32_t* zzz) {
   using G = F29<Q>;
-  G x, y, zz, zzz;
   const G U = add3_29(qy, qy, G::zero());                             // < 16p
   const G V = mul29(U, U);
   const G W = mul29(U, V);
   const G S = mul29(qx, V);
   const G X2 = mul29(qx, qx);
   const G M = add3_29(X2, X2, X2);                                    // < 6p
-  x = sub29(mul29(M, M), add3_29(S, S, G::zero()), Q::B8);           // < 10p
-  y = sub29(mul29(M, sub29(S, x, Q::B16)), mul29(W, qy), Q::B8);      // < 10p
-  zz = V;
-  zzz = W;
-  return {x, y, zz, zzz};
+  Xy29<Q> o;
+  o.x = sub29(mul29(M, M), add3_29(S, S, G::zero()), Q::B8);         // < 10p
+  o.y = sub29(mul29(M, sub29(S, o.x, Q::B16)), mul29(W, qy), Q::B8);  // < 10p
+#pragma unroll
+  for (int k = 0; k < Q::N; ++k) {
+    zz[k * 256] = V.v[k];
+    zzz[k * 256] = W.v[k];
+  }
+  return o;
 }
 
 // The mixed-addition loop.  Bounds (values, all normalised): q.x < p, q.y < 8p; x < 10p;
@@ -660,11 +666,11 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t len, uint32_t chun
     if (!dbl) break;
     G qx, qy;  // entry e: running sum := 2 q
     load_q(e, qx, qy);
-    const Xyzz29<Q> d = dbl_affine29<Q>(qx, qy);
+    asm volatile("" ::: "memory");
+    const Xy29<Q> d = dbl_affine29<Q>(qx, qy, &s_zz[0][tx], &s_zzz[0][tx]);
+    asm volatile("" ::: "memory");
     x = d.x;
     y = d.y;
-    st(s_zz, d.zz);
-    st(s_zzz, d.zzz);
     ++e;
   }
   flush(x, y, cur, inf);
