@@ -471,46 +471,26 @@ KZ_DEV void store_x29(uint32_t* __restrict__ acc29, size_t r, const X29<Q>& a) {
 #pragma unroll
   for (int k = 0; k < W29 / 4; ++k) d4[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
 }
+// value of lane (this lane ^ 1), every lane of the wave taking part
+template <class Q>
+KZ_DEV X29<Q> x29_swap_pair(const X29<Q>& a) {
+  X29<Q> o;
+#pragma unroll
+  for (int k = 0; k < Q::N; ++k) {
+    o.x.v[k] = (uint32_t)__shfl_xor((int)a.x.v[k], 1);
+    o.y.v[k] = (uint32_t)__shfl_xor((int)a.y.v[k], 1);
+    o.zz.v[k] = (uint32_t)__shfl_xor((int)a.zz.v[k], 1);
+    o.zzz.v[k] = (uint32_t)__shfl_xor((int)a.zzz.v[k], 1);
+  }
+  o.inf = __shfl_xor((int)a.inf, 1) != 0;
+  return o;
+}
 template <class Cv, class Q>
 KZ_DEV Xyzz<Cv> x29_to32(const X29<Q>& a) {
   using P = typename Cv::FpP;
   if (a.inf) return Xyzz<Cv>::inf();
   return {fp_from29<Q, P>(a.x), fp_from29<Q, P>(a.y), fp_from29<Q, P>(a.zz), fp_from29<Q, P>(a.zzz)};
 }
-// a + a through the 32-bit doubling (P == 0 and R == 0 in x29_add: equal points, rare)
-template <class Cv, class Q>
-__device__ __noinline__ X29<Q> x29_dbl_via32(const X29<Q> a) {
-  const Xyzz<Cv> d = xyzz_dbl(x29_to32<Cv, Q>(a));
-  if (d.is_inf()) return {F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), true};
-  return {fp_to29<Q>(d.x), fp_to29<Q>(d.y), fp_to29<Q>(d.zz), fp_to29<Q>(d.zzz), false};
-}
-// a + b (add-2008-s, 12M + 2S with the Y3 pair sharing one reduction).  Inputs within the record
-// bounds (x < 10p, y < 16p, zz, zzz < 2p); outputs x < 9.1p, y, zz, zzz < 1.01p -- inside them.
-template <class Cv, class Q>
-KZ_DEV X29<Q> x29_add(const X29<Q>& a, const X29<Q>& b) {
-  using G = F29<Q>;
-  if (a.inf) return b;
-  if (b.inf) return a;
-  const G U1 = mul29(a.x, b.zz), U2 = mul29(b.x, a.zz);    // < 1.01p
-  const G S1 = mul29(a.y, b.zzz), S2 = mul29(b.y, a.zzz);
-  const G P = sub29(U2, U1, Q::B2);                         // < 3.02p
-  const G R = sub29(S2, S1, Q::B2);
-  if (is_zero29(P)) {
-    if (is_zero29(R)) return x29_dbl_via32<Cv, Q>(a);
-    return {G::zero(), G::zero(), G::zero(), G::zero(), true};
-  }
-  const G PP = sqr29(P);
-  const G PPP = mul29(P, PP);
-  const G Q2 = mul29(U1, PP);
-  X29<Q> o;
-  o.x = sub29(sqr29(R), add3_29(PPP, Q2, Q2), Q::B8);                           // < 9.1p
-  o.y = mul2_29(R, sub29(Q2, o.x, Q::B16), S1, sub29(G::zero(), PPP, Q::B8));  // R (Q - X3) - S1 PPP
-  o.zz = mul29(mul29(a.zz, b.zz), PP);
-  o.zzz = mul29(mul29(a.zzz, b.zzz), PPP);
-  o.inf = false;
-  return o;
-}
-
 // 2a (dbl-2008-s-1, a = 0).  Inputs within the record bounds; outputs x < 5.1p, y, zz, zzz <
 // 1.01p.  BLS12-381 G1 has no 2-torsion (#E(Fp) is odd), so only O doubles to O.
 template <class Q>
@@ -532,9 +512,34 @@ KZ_DEV X29<Q> x29_dbl(const X29<Q>& a) {
   return o;
 }
 
-// out of line for the latency-bound reduction (keeps its register peak at 2 waves per SIMD)
+// a + b (add-2008-s, 12M + 2S with the Y3 pair sharing one reduction).  Inputs within the record
+// bounds (x < 10p, y < 16p, zz, zzz < 2p); outputs x < 9.1p, y, zz, zzz < 1.01p -- inside them.
 template <class Cv, class Q>
-__device__ __noinline__ X29<Q> x29_add_c(const X29<Q> a, const X29<Q> b) { return x29_add<Cv, Q>(a, b); }
+KZ_DEV X29<Q> x29_add(const X29<Q>& a, const X29<Q>& b) {
+  using G = F29<Q>;
+  if (a.inf) return b;
+  if (b.inf) return a;
+  const G U1 = mul29(a.x, b.zz), U2 = mul29(b.x, a.zz);    // < 1.01p
+  const G S1 = mul29(a.y, b.zzz), S2 = mul29(b.y, a.zzz);
+  const G P = sub29(U2, U1, Q::B2);                         // < 3.02p
+  const G R = sub29(S2, S1, Q::B2);
+  if (is_zero29(P)) {
+    if (is_zero29(R)) return x29_dbl<Q>(a);  // equal points (rare)
+    return {G::zero(), G::zero(), G::zero(), G::zero(), true};
+  }
+  const G PP = sqr29(P);
+  const G PPP = mul29(P, PP);
+  const G Q2 = mul29(U1, PP);
+  X29<Q> o;
+  o.x = sub29(sqr29(R), add3_29(PPP, Q2, Q2), Q::B8);                           // < 9.1p
+  o.y = mul2_29(R, sub29(Q2, o.x, Q::B16), S1, sub29(G::zero(), PPP, Q::B8));  // R (Q - X3) - S1 PPP
+  o.zz = mul29(mul29(a.zz, b.zz), PP);
+  o.zzz = mul29(mul29(a.zzz, b.zzz), PPP);
+  o.inf = false;
+  return o;
+}
+
+
 
 // 2Q for an affine Q (rare path: the running sum equals the incoming point), bounds: qx < p,
 // qy < 8p in; x < 10p, y < 10p, zz, zzz < 2p out
@@ -837,41 +842,46 @@ __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const
                                                          Xyzz<Cv>* __restrict__ R, Xyzz<Cv>* __restrict__ U) {
   static_assert(SEG == 16, "two 8-bucket halves per segment");
   KZ_TAIL_PRIO();
-  __shared__ __attribute__((aligned(16))) Xyzz<Cv> xch[256];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t g = t >> 1, h = t & 1;
-  Xyzz<Cv> run = Xyzz<Cv>::inf(), acc = Xyzz<Cv>::inf();
-  if (g < nseg) {
-    const uint32_t base = g * SEG + 8 * h;
-    if constexpr (kAcc29<Cv>) {  // BLS12-381: the running sums in radix 2^29 on the records
-      using Q = Bls12_381Fp29;
-      const X29<Q> O{F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), true};
-      X29<Q> run29 = O, acc29v = O;
+  if constexpr (kAcc29<Cv>) {  // BLS12-381: radix 2^29 on the records; R, U written as records
+    using Q = Bls12_381Fp29;
+    const X29<Q> O{F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), true};
+    X29<Q> run = O, acc = O;
+    if (g < nseg) {
+      const uint32_t base = g * SEG + 8 * h;
       for (int i = 7; i >= 1; --i) {
-        if (cnt[base + i]) run29 = x29_add<Cv, Q>(run29, load_x29<Q>(acc29, base + i));
-        acc29v = x29_add<Cv, Q>(acc29v, run29);
+        if (cnt[base + i]) run = x29_add<Cv, Q>(run, load_x29<Q>(acc29, base + i));
+        acc = x29_add<Cv, Q>(acc, run);
       }
-      if (cnt[base]) run29 = x29_add<Cv, Q>(run29, load_x29<Q>(acc29, base));
-      if (h == 1) acc29v = x29_add<Cv, Q>(acc29v, x29_dbl<Q>(x29_dbl<Q>(x29_dbl<Q>(run29))));  // R_1 + 8 U_1
-      run = x29_to32<Cv, Q>(run29);
-      acc = x29_to32<Cv, Q>(acc29v);
-    } else {
+      if (cnt[base]) run = x29_add<Cv, Q>(run, load_x29<Q>(acc29, base));
+      if (h == 1) acc = x29_add<Cv, Q>(acc, x29_dbl<Q>(x29_dbl<Q>(x29_dbl<Q>(run))));  // R_1 + 8 U_1
+    }
+    // h = 0 needs the partner's R_1 + 8 U_1, h = 1 the partner's U_0 (adjacent lanes, whole wave)
+    const X29<Q> other = x29_swap_pair<Q>(h ? acc : run);
+    if (g >= nseg) return;
+    if (h == 0) store_x29<Q>(reinterpret_cast<uint32_t*>(R), g, x29_add<Cv, Q>(acc, other));
+    else store_x29<Q>(reinterpret_cast<uint32_t*>(U), g, x29_add<Cv, Q>(run, other));
+  } else {
+    __shared__ __attribute__((aligned(16))) Xyzz<Cv> xch[256];
+    Xyzz<Cv> run = Xyzz<Cv>::inf(), acc = Xyzz<Cv>::inf();
+    if (g < nseg) {
+      const uint32_t base = g * SEG + 8 * h;
       for (int i = 7; i >= 1; --i) {
         if (cnt[base + i]) run = xyzz_add_c(run, load_xyzz(&buckets[base + i]));
         acc = xyzz_add_c(acc, run);
       }
       if (cnt[base]) run = xyzz_add_c(run, load_xyzz(&buckets[base]));
-    }
-    if constexpr (!kAcc29<Cv>)
       if (h == 1) acc = xyzz_add_c(acc, xyzz_dbl_c(xyzz_dbl_c(xyzz_dbl_c(run))));  // R_1 + 8 U_1
+    }
+    // h = 0 needs the partner's R_1 + 8 U_1, h = 1 the partner's U_0
+    store_xyzz(&xch[threadIdx.x], h ? acc : run);
+    __syncthreads();
+    if (g >= nseg) return;
+    const Xyzz<Cv> other = load_xyzz(&xch[threadIdx.x ^ 1]);
+    if (h == 0) store_xyzz(&R[g], xyzz_add_c(acc, other));
+    else store_xyzz(&U[g], xyzz_add_c(run, other));
   }
-  // h = 0 needs the partner's R_1 + 8 U_1, h = 1 the partner's U_0
-  store_xyzz(&xch[threadIdx.x], h ? acc : run);
-  __syncthreads();
-  if (g >= nseg) return;
-  const Xyzz<Cv> other = load_xyzz(&xch[threadIdx.x ^ 1]);
-  if (h == 0) store_xyzz(&R[g], xyzz_add_c(acc, other));
-  else store_xyzz(&U[g], xyzz_add_c(run, other));
 }
 
 // LDS tree sum over a 256-thread block (all threads must call).
@@ -907,21 +917,30 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
   const Xyzz<Cv>* Rs = R + (size_t)set * NSEG;
   const Xyzz<Cv>* Us = U + (size_t)set * NSEG;
   const uint32_t t = threadIdx.x;
+  // segment sum g: 32-bit XYZZ, or (BLS12-381) a radix-29 record converted as it is read
+  auto seg = [&](bool r, uint32_t g) {
+    if constexpr (kAcc29<Cv>) {
+      using Q = Bls12_381Fp29;
+      return x29_to32<Cv, Q>(load_x29<Q>(reinterpret_cast<const uint32_t*>(r ? R : U) + (size_t)set * NSEG * W29, g));
+    } else {
+      return load_xyzz(&(r ? Rs : Us)[g]);
+    }
+  };
   Xyzz<Cv> s = Xyzz<Cv>::inf();
   if (j < 11) {
 #pragma unroll 1
     for (uint32_t i = 0; i < 4; ++i) {  // q: 10-bit rank among the g with bit j set
       const uint32_t q = t + 256 * i;
       const uint32_t g = ((q >> j) << (j + 1)) | (1u << j) | (q & ((1u << j) - 1));
-      s = xyzz_add(s, load_xyzz(&Us[g]));
+      s = xyzz_add(s, seg(false, g));
     }
   } else {
     const uint32_t base = (j - 11) * (NSEG / 4);
 #pragma unroll 1
     for (uint32_t i = 0; i < 2; ++i) {
       const uint32_t g = base + t + 256 * i;
-      s = xyzz_add(s, load_xyzz(&Rs[g]));
-      s = xyzz_add(s, load_xyzz(&Us[g]));
+      s = xyzz_add(s, seg(true, g));
+      s = xyzz_add(s, seg(false, g));
     }
   }
   const Xyzz<Cv> v = block_sum256(s, lds);
