@@ -867,20 +867,20 @@ __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const
     Xyzz<Cv> run = Xyzz<Cv>::inf(), acc = Xyzz<Cv>::inf();
     if (g < nseg) {
       const uint32_t base = g * SEG + 8 * h;
-      for (int i = 7; i >= 1; --i) {
-        if (cnt[base + i]) run = xyzz_add_c(run, load_xyzz(&buckets[base + i]));
-        acc = xyzz_add_c(acc, run);
+      for (int i = 7; i >= 1; --i) {  // inline additions: no call frames in scratch
+        if (cnt[base + i]) run = xyzz_add(run, load_xyzz(&buckets[base + i]));
+        acc = xyzz_add(acc, run);
       }
-      if (cnt[base]) run = xyzz_add_c(run, load_xyzz(&buckets[base]));
-      if (h == 1) acc = xyzz_add_c(acc, xyzz_dbl_c(xyzz_dbl_c(xyzz_dbl_c(run))));  // R_1 + 8 U_1
+      if (cnt[base]) run = xyzz_add(run, load_xyzz(&buckets[base]));
+      if (h == 1) acc = xyzz_add(acc, xyzz_dbl(xyzz_dbl(xyzz_dbl(run))));  // R_1 + 8 U_1
     }
     // h = 0 needs the partner's R_1 + 8 U_1, h = 1 the partner's U_0
     store_xyzz(&xch[threadIdx.x], h ? acc : run);
     __syncthreads();
     if (g >= nseg) return;
     const Xyzz<Cv> other = load_xyzz(&xch[threadIdx.x ^ 1]);
-    if (h == 0) store_xyzz(&R[g], xyzz_add_c(acc, other));
-    else store_xyzz(&U[g], xyzz_add_c(run, other));
+    if (h == 0) store_xyzz(&R[g], xyzz_add(acc, other));
+    else store_xyzz(&U[g], xyzz_add(run, other));
   }
 }
 
