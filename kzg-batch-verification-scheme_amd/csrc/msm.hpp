@@ -575,7 +575,7 @@ __device__ __noinline__ Xy29<Q> dbl_affine29(const F29<Q> qx, const F29<Q> qy, u
 // y < 16p; zz, zzz < 2p; products < 2p.  Only two biased multiples of p (8p, 16p) are used, so
 // few constants stay live across the loop.  ZZ/ZZZ in LDS as in the 32-bit loop below.
 template <class Cv>
-KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t len, uint32_t chunk, uint32_t cur,
+KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t chunk, uint32_t cur,
                        const uint32_t* __restrict__ sorted_val, const uint32_t* __restrict__ sorted_key,
                        const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
                        const uint32_t* __restrict__ pts29, uint32_t* __restrict__ acc29, uint32_t nb) {
@@ -599,11 +599,15 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t len, uint32_t chun
   auto put = [](uint32_t* d, const G& a) {
     _Pragma("unroll") for (int k = 0; k < N / 2; ++k) reinterpret_cast<uint2*>(d)[k] = make_uint2(a.v[2 * k], a.v[2 * k + 1]);
   };
-  auto flush = [&](const G& x, const G& y, uint32_t key, bool inf) {
-    const uint32_t o = off[key];
-    const bool started_before = o < start;
-    const bool ends_after = o + cnt[key] > start + len;
-    const size_t rec = started_before ? (size_t)nb + chunk : ends_after ? (size_t)nb + nthreads + chunk : key;
+  // Where a finished bucket goes: only the chunk's first bucket can have started in an earlier
+  // chunk (first piece) and only its last can continue into a later one (last piece), so both
+  // are decided from the neighbouring sorted keys at the chunk's ends -- no off/cnt loads in the
+  // loop (a flush runs in most iterations of a wavefront: some lane changes bucket).
+  const bool started_before = start > 0 && sorted_key[start - 1] == cur;
+  bool first = true;
+  auto flush = [&](const G& x, const G& y, uint32_t key, bool inf, bool ends_after) {
+    const size_t rec = (first && started_before) ? (size_t)nb + chunk : ends_after ? (size_t)nb + nthreads + chunk : key;
+    first = false;
     uint32_t* d = acc29 + rec * W29;
     put(d, x);
     put(d + N, y);
@@ -633,7 +637,7 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t len, uint32_t chun
     for (; e < end; ++e) {
       const uint32_t key = sorted_key[e];
       if (key != cur) {
-        flush(x, y, cur, inf);
+        flush(x, y, cur, inf, false);
         inf = true;
         cur = key;
       }
@@ -678,7 +682,7 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t len, uint32_t chun
     y = d.y;
     ++e;
   }
-  flush(x, y, cur, inf);
+  flush(x, y, cur, inf, end < total && sorted_key[end] == cur);
 }
 
 // Waves per SIMD the accumulation is compiled for (VGPR budget 512 / waves per lane); the host
@@ -712,7 +716,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
   const uint32_t end = min(start + len, total);
   uint32_t cur = sorted_key[start];
   if constexpr (kAcc29<Cv>) {
-    acc_loop29<Cv>(start, end, len, chunk, cur, sorted_val, sorted_key, off, cnt,
+    acc_loop29<Cv>(start, end, total, chunk, cur, sorted_val, sorted_key, off, cnt,
                    reinterpret_cast<const uint32_t*>(pts), acc29, nb);
   } else {  // BN254: 32-bit limbs (8 x 32 bits; radix 2^29 would need 9 limbs)
   // ZZ and ZZZ of the running bucket sum live in LDS (word-major per thread: conflict-free
