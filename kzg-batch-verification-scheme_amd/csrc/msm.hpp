@@ -617,8 +617,7 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
   G x = G::zero(), y = G::zero();
   bool inf = true;  // running sum = O: at every bucket start, and after P + (-P)
   // loads entry e's point (sign applied: -y as 8p - y)
-  auto load_q = [&](uint32_t e, G& qx, G& qy) {
-    const uint32_t v = sorted_val[e];
+  auto load_q = [&](uint32_t v, G& qx, G& qy) {
     const uint4* s4 = reinterpret_cast<const uint4*>(pts29 + (size_t)(v >> 1) * (sizeof(Affine<Cv>) / 4));
     uint32_t w[2 * N];
     _Pragma("unroll") for (int k = 0; k < N / 2; ++k) {
@@ -634,15 +633,22 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
   uint32_t e = start;
   for (;;) {
     bool dbl = false;
+    // entry e + 1's key and value are loaded one iteration ahead: the loop's memory chain is
+    // then the point gather alone instead of key -> value -> point
+    uint32_t key_n = e < end ? sorted_key[e] : 0u, val_n = e < end ? sorted_val[e] : 0u;
     for (; e < end; ++e) {
-      const uint32_t key = sorted_key[e];
+      const uint32_t key = key_n, v = val_n;
+      if (e + 1 < end) {
+        key_n = sorted_key[e + 1];
+        val_n = sorted_val[e + 1];
+      }
       if (key != cur) {
         flush(x, y, cur, inf, false);
         inf = true;
         cur = key;
       }
       G qx, qy;
-      load_q(e, qx, qy);
+      load_q(v, qx, qy);
       if (inf) {
         x = qx;
         y = qy;
@@ -674,7 +680,7 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
     }
     if (!dbl) break;
     G qx, qy;  // entry e: running sum := 2 q
-    load_q(e, qx, qy);
+    load_q(sorted_val[e], qx, qy);
     asm volatile("" ::: "memory");
     const Xy29<Q> d = dbl_affine29<Q>(qx, qy, &s_zz[0][tx], &s_zzz[0][tx]);
     asm volatile("" ::: "memory");
