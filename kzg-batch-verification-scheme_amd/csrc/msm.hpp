@@ -7,6 +7,7 @@
 //                     ACC_CHUNK consecutive sorted entries (not a bucket), so Poisson bucket
 //                     sizes do not diverge a wavefront; bucket pieces cut by a chunk
 //                     boundary go to partial slots and are joined by k_fixup.
+//   k_fixup           joins the pieces of buckets cut by chunk boundaries
 //   k_reduce_segments sum_b b*S_b per window: 16-bucket segments (running sums) ...
 //   k_reduce_bits     ... combined per window by bit decomposition of the segment index
 //   k_window_combine  Horner over the 16-bit windows (2^16 * acc + W_w)
@@ -395,12 +396,14 @@ KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_
 }
 
 // ---- radix-2^29 accumulation (BLS12-381; field29.hpp) ------------------------------------
-// Points arrive converted in place by k_pts_to29 (x in words 0..13, y in 14..27 of each 128-B
-// slot).  Finished bucket pieces are written as radix-29 records of W29 words (x, y, zz, zzz;
-// zz = 0 marks infinity) to `acc29` = [nb bucket records | nthreads first pieces | nthreads
-// last pieces]; k_fixup joins pieces into records and k_reduce_segments runs its running sums on
-// the records, both with the radix-29 XYZZ addition (x29_add below).  Converting at each flush instead (4 products) would run on most
-// iterations of a wavefront, since some lane changes bucket in almost every step.
+// Points arrive in radix-29 form (x in words 0..13, y in 14..27 of each 128-B slot), written so
+// by k_convert_points<To29> or converted in place by k_pts_to29.  Finished buckets and bucket
+// pieces are radix-29 records of W29 words (x, y, zz, zzz; zz = 0 marks infinity) in `acc29` =
+// [nb bucket records | nthreads first pieces | nthreads last pieces]; k_fixup joins pieces into
+// the records and k_reduce_segments runs its running sums on them, both with the radix-29 XYZZ
+// addition (x29_add below), writing R/U as records too; k_reduce_bits converts to 32-bit limbs
+// as it reads them.  No conversion at the flushes: some lane of a wavefront changes bucket in
+// almost every step, so per-flush work runs on most iterations.
 #ifndef KZ_NO_ACC29
 template <class Cv>
 constexpr bool kAcc29 = Cv::FpP::N == 12;
@@ -577,7 +580,6 @@ __device__ __noinline__ Xy29<Q> dbl_affine29(const F29<Q> qx, const F29<Q> qy, u
 template <class Cv>
 KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t chunk, uint32_t cur,
                        const uint32_t* __restrict__ sorted_val, const uint32_t* __restrict__ sorted_key,
-                       const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
                        const uint32_t* __restrict__ pts29, uint32_t* __restrict__ acc29, uint32_t nb) {
   using Q = Bls12_381Fp29;
   using G = F29<Q>;
@@ -722,7 +724,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
   const uint32_t end = min(start + len, total);
   uint32_t cur = sorted_key[start];
   if constexpr (kAcc29<Cv>) {
-    acc_loop29<Cv>(start, end, total, chunk, cur, sorted_val, sorted_key, off, cnt,
+    acc_loop29<Cv>(start, end, total, chunk, cur, sorted_val, sorted_key,
                    reinterpret_cast<const uint32_t*>(pts), acc29, nb);
   } else {  // BN254: 32-bit limbs (8 x 32 bits; radix 2^29 would need 9 limbs)
   // ZZ and ZZZ of the running bucket sum live in LDS (word-major per thread: conflict-free
