@@ -924,8 +924,61 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
   KZ_TAIL_PRIO();
   constexpr uint32_t NSEG = NBUCKETS / SEG;  // 2048 = 2^11
   static_assert(NSEG == 2048 && RB_PARTS == 15, "bit decomposition assumes 2^11 segments per set");
-  __shared__ __attribute__((aligned(16))) Xyzz<Cv> lds[128];
   const uint32_t set = blockIdx.x / RB_PARTS, j = blockIdx.x % RB_PARTS;
+  if constexpr (kAcc29<Cv>) {  // BLS12-381: radix 2^29 on the R/U records, inline additions
+    using Q = Bls12_381Fp29;
+    constexpr int N = Q::N;
+    __shared__ uint32_t lds29[W29 + 1][128];
+    const uint32_t t = threadIdx.x;
+    const uint32_t* R29 = reinterpret_cast<const uint32_t*>(R) + (size_t)set * NSEG * W29;
+    const uint32_t* U29 = reinterpret_cast<const uint32_t*>(U) + (size_t)set * NSEG * W29;
+    X29<Q> v{F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), true};
+    if (j < 11) {
+#pragma unroll 1
+      for (uint32_t i = 0; i < 4; ++i) {  // q: 10-bit rank among the g with bit j set
+        const uint32_t q = t + 256 * i;
+        const uint32_t g = ((q >> j) << (j + 1)) | (1u << j) | (q & ((1u << j) - 1));
+        v = x29_add<Cv, Q>(v, load_x29<Q>(U29, g));
+      }
+    } else {
+      const uint32_t base = (j - 11) * (NSEG / 4);
+#pragma unroll 1
+      for (uint32_t i = 0; i < 2; ++i) {
+        const uint32_t g = base + t + 256 * i;
+        v = x29_add<Cv, Q>(v, load_x29<Q>(R29, g));
+        v = x29_add<Cv, Q>(v, load_x29<Q>(U29, g));
+      }
+    }
+    for (int st = 128; st >= 1; st >>= 1) {  // LDS tree, one coordinate word per row
+      if (t >= (uint32_t)st && t < 2u * st) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+          lds29[k][t - st] = v.x.v[k];
+          lds29[N + k][t - st] = v.y.v[k];
+          lds29[2 * N + k][t - st] = v.zz.v[k];
+          lds29[3 * N + k][t - st] = v.zzz.v[k];
+        }
+        lds29[W29][t - st] = v.inf ? 1u : 0u;
+      }
+      __syncthreads();
+      if (t < (uint32_t)st) {
+        X29<Q> o;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+          o.x.v[k] = lds29[k][t];
+          o.y.v[k] = lds29[N + k][t];
+          o.zz.v[k] = lds29[2 * N + k][t];
+          o.zzz.v[k] = lds29[3 * N + k][t];
+        }
+        o.inf = lds29[W29][t] != 0;
+        v = x29_add<Cv, Q>(v, o);
+      }
+      __syncthreads();
+    }
+    if (t == 0) store_xyzz(&parts[(size_t)set * RB_PARTS + j], x29_to32<Cv, Q>(v));
+    return;
+  }
+  __shared__ __attribute__((aligned(16))) Xyzz<Cv> lds[128];
   const Xyzz<Cv>* Rs = R + (size_t)set * NSEG;
   const Xyzz<Cv>* Us = U + (size_t)set * NSEG;
   const uint32_t t = threadIdx.x;
