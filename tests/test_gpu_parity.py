@@ -145,6 +145,31 @@ def test_msm_random_vs_oracle(ctx, curve):
 
 
 @pytest.mark.parametrize("curve", CURVES)
+def test_msm_reduction_special_cases(ctx, curve):
+    """Adjacent buckets whose sums cancel or coincide, so that the bucket-sum reduction's running
+    sums hit P + (-P) = O and P + P (the doubling branch of its general addition):
+    digits 8, 7, 6, 5 on P, -P, P, P (buckets 7..4 of the first segment half) = 12 P, plus the
+    same pattern repeated in a high window and a lone top-bucket digit (acc + run = 2 run)."""
+    C = pc.CURVES[curve]
+    rng = random.Random(83)
+    k = rng.randrange(1, C.r)
+    base = O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(x) for x in [k, C.r - k]), 2)
+    g1b = 2 * C.fp_bytes
+    P, nP = base[:g1b], base[g1b:]
+    cases = [
+        ([P, nP, P, P], [8, 7, 6, 5]),
+        ([P, nP, P, P], [8 << 48, 7 << 48, 6 << 48, 5 << 48]),
+        ([P], [8]),
+        ([P, P], [8, 7]),
+        ([P, nP], [16, 15]),
+    ]
+    for pts, sc in cases:
+        pb = b"".join(pts)
+        sb = b"".join(pk.fr_to_bytes(x) for x in sc)
+        assert ctx.msm_g1(curve, pb, sb) == O.msm_g1(curve, pb, sb, len(pts)), sc
+
+
+@pytest.mark.parametrize("curve", CURVES)
 def test_msm_skewed_buckets(ctx, curve):
     """Adversarial digit distribution: one huge bucket (all scalars equal) + duplicates."""
     C = pc.CURVES[curve]

@@ -19,6 +19,9 @@
     "v_mad_u64_u32 %2, %4, %5, %6, %2\n\tv_mad_u64_u32 %3, %4, %5, %6, %3" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "=&s"(cc) : "v"(a), "v"(b))
 #define MAD4D(c0, a, b) asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0\n\tv_mad_u64_u32 %0, %1, %3, %2, %0\n\t" \
     "v_mad_u64_u32 %0, %1, %2, %3, %0\n\tv_mad_u64_u32 %0, %1, %3, %2, %0" : "+v"(c0), "=&s"(cc) : "v"(a), "v"(b))
+#define SHR64(x) asm volatile("v_lshrrev_b64 %0, 29, %0" : "+v"(x))
+#define ALIGN(lo, hi) asm volatile("v_alignbit_b32 %0, %1, %0, 29" : "+v"(lo) : "v"(hi))
+#define MULLO_AND(m, x, y) asm volatile("v_mul_lo_u32 %0, %1, %2\n\tv_and_b32 %0, 0x1fffffff, %0" : "=&v"(m) : "v"(x), "v"(y))
 #define FMA64(x, y) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(x) : "v"(y))
 
 template <int MODE>
@@ -57,6 +60,10 @@ __global__ void __launch_bounds__(256) k_probe(uint32_t* out, int iters, uint32_
       MAD(acc0, a, b); MAD(acc0, a, b); MAD(acc0, a, b); MAD(acc0, a, b);
     } else if constexpr (MODE == 11) {  // two dependent chains, 4 per statement, alternating
       MAD4D(acc0, a, b); MAD4D(acc1, a, b);
+    } else if constexpr (MODE == 12) {  // 8 v_lshrrev_b64 (the column shift of the radix-29 products)
+      SHR64(acc0); SHR64(acc1); SHR64(acc2); SHR64(acc3); SHR64(acc4); SHR64(acc5); SHR64(acc6); SHR64(acc7);
+    } else if constexpr (MODE == 13) {  // 8 v_alignbit_b32
+      ALIGN(t0, t1); ALIGN(t1, t2); ALIGN(t2, t3); ALIGN(t3, t4); ALIGN(t4, t5); ALIGN(t5, t6); ALIGN(t6, t7); ALIGN(t7, t0);
     } else if constexpr (MODE == 7) {  // 8 mad + 8 add_co
       MAD(acc0, a, b); ADDC(t0, a); MAD(acc1, a, b); ADDC(t1, a); MAD(acc2, a, b); ADDC(t2, a); MAD(acc3, a, b); ADDC(t3, a);
       MAD(acc4, a, b); ADDC(t4, a); MAD(acc5, a, b); ADDC(t5, a); MAD(acc6, a, b); ADDC(t6, a); MAD(acc7, a, b); ADDC(t7, a);
@@ -93,7 +100,7 @@ static void run(const char* name, int instr_per_iter, int waves_per_simd) {
 }
 
 int main() {
-  for (int w : {1, 2, 3, 4, 8}) {
+  for (int w : {4, 8}) {
     run<0>("mad_u64_u32 x8", 8, w);
     run<1>("mad+addc (mac32) x8", 16, w);
     run<2>("add_co_u32 x8", 8, w);
@@ -106,6 +113,8 @@ int main() {
     run<9>("mad chain x8, 4/statement", 8, w);
     run<10>("mad chain x8, 1/statement", 8, w);
     run<11>("2 mad chains, 4/statement", 8, w);
+    run<12>("lshrrev_b64 x8", 8, w);
+    run<13>("alignbit_b32 x8", 8, w);
   }
   return 0;
 }
