@@ -1,5 +1,8 @@
-// Radix-2^29 Montgomery arithmetic for the BLS12-381 bucket accumulation (msm.hpp
-// k_accumulate).  14 limbs of 29 bits in 32-bit VGPRs, R29 = 2^406.
+// Radix-2^29 Montgomery arithmetic for BLS12-381: the bucket accumulation (msm.hpp
+// k_accumulate) and everything around it that is full-chip or on the pipeline's critical path
+// -- the point conversion and on-curve test (kernels.hpp), the piece join and both bucket-sum
+// reductions (msm.hpp x29_add), square roots and the subgroup check (points.hpp).  14 limbs
+// of 29 bits in 32-bit VGPRs, R29 = 2^406.
 //
 // Why: the accumulation is VALU-issue bound, and in the 32-bit-limb product (field.hpp) every
 // limb product costs TWO issue slots, the v_mad_u64_u32 and the v_addc_co_u32 folding its
