@@ -31,6 +31,22 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "kzg-batch-verification-scheme_amd"))
 
+
+def _launch_ranks():
+    """`--gpus N` (N > 1) started directly, not by torchrun: run N rank processes of this script
+    (kzgmi/launch.py) and exit with the job's status -- before anything here touches the GPU."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    a, _ = pre.parse_known_args()
+    from kzgmi.launch import maybe_launch
+    return maybe_launch([os.path.abspath(__file__)] + sys.argv[1:], a.gpus)
+
+
+if __name__ == "__main__":
+    _rc = _launch_ranks()
+    if _rc is not None:
+        sys.exit(_rc)
+
 # HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default).  The slot
 # pipeline needs about one queue per batch in flight -- batches whose streams share a queue
 # serialise (measured: 12 slots on 4 queues 77/s, on 12-16 queues 106/s; after the latency-tail
@@ -68,6 +84,57 @@ def gen_inputs(ctx, curve, n, seed):
     return C, z, y, P
 
 
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _cpuset_count(spec):
+    """Number of CPUs in a cpuset list such as '0-15,32-47'."""
+    n = 0
+    for part in (spec or "").split(","):
+        part = part.strip()
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        n += (int(b) - int(a) + 1) if b else 1
+    return n
+
+
+def cpu_grant():
+    """CPUs this process may really use, and what limits it: the affinity mask, the cgroup v2
+    CPU quota (/sys/fs/cgroup/cpu.max = "quota period" or "max period"), the cgroup cpuset, and an
+    explicit OMP_NUM_THREADS (the GPU box exports 16 = its per-GPU CPU share)."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except Exception:
+        affinity = os.cpu_count() or 1
+    limits = {"sched_getaffinity": affinity}
+    cpu_max = _read("/sys/fs/cgroup/cpu.max")
+    quota = None
+    if cpu_max:
+        q, _, per = cpu_max.partition(" ")
+        if q != "max" and per:
+            quota = -(-int(q) // int(per))  # ceil: CPUs' worth of time per period
+            limits["cgroup_cpu_max"] = quota
+    cpuset = _read("/sys/fs/cgroup/cpuset.cpus.effective")
+    if cpuset:
+        limits["cgroup_cpuset"] = _cpuset_count(cpuset)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        limits["OMP_NUM_THREADS"] = int(omp)
+    n = min(limits.values())
+    binding = [k for k, v in limits.items() if v == n]
+    info = {"nproc": os.cpu_count(), "sched_getaffinity": affinity, "cgroup_cpu_max_raw": cpu_max,
+            "cgroup_quota_cpus": quota, "cgroup_cpuset_effective": cpuset, "OMP_NUM_THREADS": omp,
+            "threads_used": max(1, n), "limited_by": binding,
+            "grant": "%d of %d host CPUs (%s)" % (max(1, n), os.cpu_count() or 0, ", ".join(binding))}
+    return max(1, n), info
+
+
 def host_info():
     model = ""
     try:
@@ -77,73 +144,72 @@ def host_info():
                 model = line.split(":", 1)[1].strip()
     except Exception:
         pass
-    try:
-        allowed = len(os.sched_getaffinity(0))
-    except Exception:
-        allowed = os.cpu_count()
-    return {"lscpu_model": model, "nproc": os.cpu_count(), "sched_getaffinity": allowed,
-            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
-
-
-def cpu_threads():
-    """CPUs this process may use: its affinity mask, capped by an explicit OMP_NUM_THREADS (the
-    GPU box grants each job a 16-CPU share and exports OMP_NUM_THREADS=16 for it)."""
-    try:
-        n = len(os.sched_getaffinity(0))
-    except Exception:
-        n = os.cpu_count() or 1
-    omp = os.environ.get("OMP_NUM_THREADS")
-    if omp and omp.isdigit() and int(omp) > 0:
-        n = min(n, int(omp))
-    return max(1, n)
+    _, grant = cpu_grant()
+    return dict(grant, lscpu_model=model)
 
 
 def cpu_baseline(curve, Cm, z, y, P, n_full, seed, target_s):
-    """Time the C oracle (OpenMP, on every CPU this process may use) on a bounded prefix sample."""
+    """Time the C oracle (OpenMP over this process's CPU grant) on the same tuples: the whole
+    batch when it fits the time budget (no extrapolation), else the largest power-of-two prefix
+    that does; plus a single-core sample and configs[0] (n = 256)."""
     from oracle import oracle as O  # cpu_baseline leg only
     g1b = 2 * kzgmi.FP_BYTES[curve]
-    g2, tg2 = kzgmi.G2_GENERATOR[curve], None
-    O.set_threads(cpu_threads())
+    threads, grant = cpu_grant()
+    O.set_threads(threads)
     threads = O.threads()
+    tg2_bytes = cpu_baseline.tg2
+    g2 = kzgmi.G2_GENERATOR[curve]
+    host = {}
+
+    def host_bytes(m):
+        if m not in host:
+            host.clear()
+            host[m] = [t[: m * w].cpu().numpy().tobytes() for t, w in ((Cm, g1b), (z, 32), (y, 32), (P, g1b))]
+        return host[m]
 
     def run(m):
-        hb = [t[: m * w].cpu().numpy().tobytes() for t, w in ((Cm, g1b), (z, 32), (y, 32), (P, g1b))]
+        hb = host_bytes(m)
         t0 = time.perf_counter()
         ok = O.batch_verify(curve, hb[0], hb[1], hb[2], hb[3], m, g2, tg2_bytes, seed)
-        return time.perf_counter() - t0, ok
-
-    tg2_bytes = cpu_baseline.tg2
-
-    def sized_run(budget_s):
-        m = 1 << 10
-        dt, ok = run(m)
-        # MSM cost ~ linear in m: pick the largest power of two expected to take <= budget_s
-        while m * 2 <= n_full and dt * 2 * (1.15) <= budget_s:
-            m *= 2
-            dt *= 2
-        dt, ok = run(m)
+        dt = time.perf_counter() - t0
         assert ok, "oracle rejected a valid batch"
-        return m, dt
+        return dt
+
+    def sized_run(budget_s, m0=4096):
+        # time = constant (pairing) + slope x m: two sample sizes give both
+        dt0, dt1 = run(m0), run(4 * m0)
+        slope = max(dt1 - dt0, 1e-9) / (3 * m0)
+        m = 4 * m0
+        while m * 2 <= n_full and dt1 + slope * (2 * m - 4 * m0) <= budget_s:
+            m *= 2
+        return m, (run(m) if m != 4 * m0 else dt1)
 
     m, dt = sized_run(target_s)
+    # configs[0] (BASELINE.json:7): a 256-tuple batch on the CPU verifier, median of 5
+    cfg0 = sorted(run(256) for _ in range(5))
     # single-core figure (SURVEY.md 8d "also record the single-core time")
     O.set_threads(1)
     try:
-        m1, dt1 = sized_run(min(target_s, 4.0))
+        m1, dt1 = sized_run(min(target_s, 6.0))
     finally:
         O.set_threads(threads)
+    whole = m == n_full
     return {
-        "value": (m / dt) / n_full,
-        "unit": "batch-verifies/s (extrapolated linearly from the sample to n=%d tuples)" % n_full,
+        "value": 1.0 / dt if whole else (m / dt) / n_full,
+        "unit": "batch-verifies/s of n=%d tuples%s" % (n_full, "" if whole else " (linear extrapolation from the sample)"),
         "cores": threads,
         "kind": "port",
-        "sample": "oracle/c batch_verify on the first %d of the %d tuples, %.2f s on %d OpenMP threads = every CPU "
-                  "this process may use; an unoptimised correctness oracle (unsigned-window Jacobian Pippenger, "
-                  "affine Miller loop, plain-pow final exponentiation), self-authored -- the reference has no "
-                  "CPU verifier" % (m, n_full, dt, threads),
+        "sample": "oracle/c batch_verify on %s of the %d tuples, %.2f s on %d OpenMP threads = %s; an "
+                  "unoptimised correctness oracle (unsigned-window Jacobian Pippenger, affine Miller loop, "
+                  "plain-pow final exponentiation), self-authored -- the reference has no CPU verifier"
+                  % ("all" if whole else "the first %d" % m, n_full, dt, threads, grant["grant"]),
+        "sample_tuples": m,
+        "sample_seconds": dt,
         "sample_tuples_per_s": m / dt,
         "single_core": {"value": (m1 / dt1) / n_full, "sample_tuples": m1, "seconds": dt1,
                         "tuples_per_s": m1 / dt1},
+        "cfg0_cpu_n256_ms": 1e3 * cfg0[len(cfg0) // 2],
+        "cfg0_cpu_n256_runs_ms": [1e3 * t for t in cfg0],
     }
 
 
@@ -159,7 +225,8 @@ def main():
     ap.add_argument("--msm-steps", type=int, default=24)
     ap.add_argument("--trusted-steps", type=int, default=96,
                     help="secondary: pipelined batches with KZGMI_FLAG_TRUSTED_G1 (GLV on BLS12-381; 0 = skip)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="time budget of the multi-threaded CPU-baseline sample (whole batch if it fits)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fs-steps", type=int, default=96,
                     help="secondary: pipelined batches in Fiat-Shamir mode (r_i = r^i, 0 = skip)")
@@ -172,6 +239,9 @@ def main():
     ap.add_argument("--cfg4-n", type=int, default=1 << 24)
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU pipeline (RCCL all-gather per batch) even at world size 1")
+    ap.add_argument("--strong-steps", type=int, default=0,
+                    help="sharded runs: batches of the strong-scaled leg (one --n batch split over the ranks; "
+                         "default = --steps)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -206,6 +276,9 @@ def main():
     tg2 = ctx.g2_mul(curve, g2, TAU)
     cpu_baseline.tg2 = tg2
     srs = ctx.load_srs(curve, g2, tg2)
+    # every slot's workspace sized up front (kzgmi_ctx_reserve): the timed region allocates
+    # nothing however few warm-up steps run (checked below with kzgmi_alloc_count)
+    ctx.reserve(curve, n)
     gseed = hashlib.sha256(b"kzgmi-bench-%d" % rank).digest()
     vseed = hashlib.sha256(b"kzgmi-bench-verify").digest()
     t0 = time.perf_counter()
@@ -254,6 +327,7 @@ def main():
     barrier()
     # ---- timed region (phase events on the kernels' own streams)
     ctx.set_profiling(True)
+    allocs0 = kzgmi.alloc_count()
     t0 = time.perf_counter()
     for k in range(args.steps):
         if sharded:
@@ -263,6 +337,7 @@ def main():
     drain()
     barrier()
     elapsed = time.perf_counter() - t0
+    allocs_timed = kzgmi.alloc_count() - allocs0
     phases = ctx.phase_ms()
     ctx.set_profiling(False)
     if world > 1:
@@ -274,19 +349,77 @@ def main():
     # ---- single-batch latency (not pipelined), rank 0 view
     lat = None
     phases_single = None
+    lat_runs = None
     if world == 1:
         ts = []
-        for _ in range(3):
+        for _ in range(10):  # median of >= 10 runs
             torch.cuda.synchronize()
             a = time.perf_counter()
             assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n)
             ts.append(time.perf_counter() - a)
-        lat = 1e3 * min(ts)
+        ts.sort()
+        lat = 1e3 * ts[len(ts) // 2]
+        lat_runs = [1e3 * t for t in ts]
         ctx.set_profiling(True)
         for _ in range(2):
             assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n)
         phases_single = ctx.phase_ms()
         ctx.set_profiling(False)
+
+    # ---- configs[0] (BASELINE.json:7): a 256-tuple batch (the CPU verifier's time is added by
+    # cpu_baseline below); GPU latency of the same batch, median of 10 synchronous calls
+    cfg0 = None
+    if world == 1 and not sharded and n >= 256:
+        ts = []
+        for _ in range(10):
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=256)
+            ts.append(time.perf_counter() - a)
+        ts.sort()
+        cfg0 = {"n": 256, "curve": curve, "gpu_latency_ms": 1e3 * ts[len(ts) // 2],
+                "gpu_latency_runs_ms": [1e3 * t for t in ts],
+                "note": "first 256 of the generated tuples; GPU: one synchronous kzgmi_batch_verify_device "
+                        "(latency-bound: pairing + per-batch fixed costs); CPU: oracle/c batch_verify"}
+
+    # ---- strong scaling (configs[2] as one batch over all ranks): ONE global batch of n tuples
+    # split n/world per rank (shard_range), `slots` global batches in flight -- the per-rank
+    # fixed costs (bucket reduction, window combination, pairing) do not shrink with the shard
+    strong = None
+    if sharded:
+        from kzgmi.distributed import shard_range
+        off_s, n_s = shard_range(n, world, rank)
+        g1b = 2 * kzgmi.FP_BYTES[curve]
+        views = (Cm[: n_s * g1b], z[: n_s * 32], y[: n_s * 32], P[: n_s * g1b])
+        ssteps = args.strong_steps or args.steps
+
+        def step_strong():
+            for ok in pipe.submit(*views, n_s, off_s, vseed):
+                assert ok, "batch rejected"
+
+        for _ in range(min(slots, ssteps)):
+            step_strong()
+        drain()
+        barrier()
+        ctx.set_profiling(True)
+        a = time.perf_counter()
+        for _ in range(ssteps):
+            step_strong()
+        drain()
+        barrier()
+        dts = time.perf_counter() - a
+        sph = ctx.phase_ms()
+        ctx.set_profiling(False)
+        if world > 1:
+            t = torch.tensor([dts], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dts = float(t.item())
+        strong = {"batch_verifies_per_s": ssteps / dts, "ms_per_batch": 1e3 * dts / ssteps, "steps": ssteps,
+                  "n_total": n, "n_per_rank": n_s, "world": world, "scaling": "strong",
+                  "phase_ms_avg_in_timed_region": sph,
+                  "method": "one n-tuple batch split by point range (kzgmi.distributed.shard_range), partial "
+                            "(A_k, B_k) per rank, RCCL all-gather, combine + pairing on every rank; %d batches "
+                            "in flight" % slots}
 
     # ---- secondary: compressed inputs + subgroup checks, single GPU
     comp = None
@@ -304,6 +437,7 @@ def main():
             ctx.batch_verify_async(srs, s, cc, z, y, pp, n, seed=vseed, compressed=True, subgroup_check=True)
             pending[s] = True
 
+        ctx.reserve(curve, n, compressed=True, subgroup_check=True)
         for k in range(min(slots, args.compressed_steps)):  # warm every slot's workspace (GLV sizes)
             cstep(k)
         drain()
@@ -337,6 +471,7 @@ def main():
             ctx.batch_verify_async(srs, s, Cm, z, y, P, n, seed=vseed, trusted_g1=True)
             pending[s] = True
 
+        ctx.reserve(curve, n, trusted_g1=True)
         for k in range(min(slots, args.trusted_steps)):
             tstep(k)
         drain()
@@ -364,6 +499,7 @@ def main():
             ctx.batch_verify_async(srs, s, Cm, z, y, P, n, fiat_shamir=True)
             pending[s] = True
 
+        ctx.reserve(curve, n, fiat_shamir=True)
         for k in range(min(slots, args.fs_steps)):  # warm every slot's workspace
             fstep(k)
         drain()
@@ -377,7 +513,8 @@ def main():
         ctx.set_profiling(True)
         assert ctx.batch_verify(srs, Cm, z, y, P, n=n, fiat_shamir=True)
         fsm = {"batch_verifies_per_s": args.fs_steps / dt, "steps": args.fs_steps,
-               "randomisers": "r_i = r^i, r from the GPU Merkle transcript of the batch (255-bit scalars)",
+               "randomisers": "counter-mode 127-bit r_i seeded with the Fiat-Shamir challenge r (GPU Merkle "
+                              "transcript of the batch, KZGMI_FLAG_FIAT_SHAMIR)",
                "phase_ms_single_batch": ctx.phase_ms()}
         ctx.set_profiling(False)
 
@@ -488,37 +625,57 @@ def main():
         ctx.gen_g1(curve, k4.reshape(-1), m4, p4)
         del k4
         s4 = s4.reshape(-1)
-        res4 = []
+        res4, t4 = [], []  # results and the host time each one arrived (outliers name their MSM)
+
+        def got4(rs):
+            res4.extend(rs)
+            t4.extend([time.perf_counter()] * len(rs))
         if world > 1 or sharded:
             mp4 = ShardedMsmPipeline(ctx, curve, slots=2, lanes=2)
-            sub4 = lambda: res4.extend(mp4.submit(p4, s4, m4))  # noqa: E731
-            drain4 = lambda: res4.extend(mp4.drain())  # noqa: E731
+            sub4 = lambda: got4(mp4.submit(p4, s4, m4))  # noqa: E731
+            drain4 = lambda: got4(mp4.drain())  # noqa: E731
         else:
             q4 = [0]
 
             def sub4():
                 sl = q4[0] % 2
                 if q4[0] >= 2:
-                    res4.append(ctx.msm_wait(sl))
+                    got4([ctx.msm_wait(sl)])
                 ctx.msm_g1_async(curve, sl, p4, s4, m4)
                 q4[0] += 1
 
             def drain4():
                 first = q4[0] % 2 if q4[0] >= 2 else 0
                 for i in range(min(q4[0], 2)):
-                    res4.append(ctx.msm_wait((first + i) % 2))
+                    got4([ctx.msm_wait((first + i) % 2)])
                 q4[0] = 0
         sub4()
         drain4()                                        # warm both workspaces' allocation
         sub4()
         drain4()
         barrier()
+        ctx.set_profiling(True)
+        n_warm4 = len(t4)
         a = time.perf_counter()
         for _ in range(args.cfg4_msms):
             sub4()
         drain4()
         barrier()
         dt4 = time.perf_counter() - a
+        ph4 = ctx.phase_ms()
+        ctx.set_profiling(False)
+        arrivals = [a] + t4[n_warm4:]
+        gaps4 = [1e3 * (arrivals[i + 1] - arrivals[i]) for i in range(len(arrivals) - 1)]
+        # one MSM alone, per phase (HIP events on its stream): the reference shape for the above
+        ctx.set_profiling(True)
+        if world > 1 or sharded:
+            got4(mp4.submit(p4, s4, m4))
+            got4(mp4.drain())
+        else:
+            ctx.msm_g1_async(curve, 0, p4, s4, m4)
+            got4([ctx.msm_wait(0)])
+        ph4_single = ctx.phase_ms()
+        ctx.set_profiling(False)
         if world > 1:
             t = torch.tensor([dt4], dtype=torch.float64, device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -526,6 +683,9 @@ def main():
         assert len(set(res4)) == 1, "configs[3] MSM results differ between runs"
         cfg4 = {"pts_per_s": args.cfg4_n * args.cfg4_msms / dt4, "ms_per_msm": 1e3 * dt4 / args.cfg4_msms,
                 "n_total": args.cfg4_n, "n_per_rank": m4, "msms": args.cfg4_msms, "world": world,
+                "result_gaps_ms": gaps4, "phase_ms_avg_in_timed_region": ph4, "phase_ms_single_msm": ph4_single,
+                "timing_note": "result_gaps_ms: host time between consecutive results (first from the start of "
+                               "the timed region; 2 MSMs in flight); phases: HIP events on the MSM's own stream",
                 "scaling": "strong", "scalars": "uniform < 2^254 (16 windows of 16 bits)",
                 "method": "point-range shards, kzgmi_msm_partial_device_async + RCCL all-gather of partial "
                           "sums + kzgmi_msm_combine_device_async, 2 MSMs in flight per rank" if world > 1 or sharded
@@ -636,6 +796,10 @@ def main():
             cpu["host"] = host_info()
         except Exception as e:  # the baseline must not kill the GPU measurement
             cpu = {"error": repr(e)}
+    cfg0_cpu_ms = (cpu or {}).get("cfg0_cpu_n256_ms")
+    if cfg0 is not None and cfg0_cpu_ms is not None:
+        cfg0["cpu_ms"] = cfg0_cpu_ms
+        cfg0["cpu_threads"] = cpu.get("cores")
     out = {
         "metric": METRIC,
         "value": value,
@@ -670,6 +834,12 @@ def main():
                                    "note": "points declared G1 members (kzgmi_set_trusted_g1): GLV split"},
             "trusted_g1": trusted,
             "single_batch_latency_ms": lat,
+            "single_batch_latency_note": "median of 10 synchronous batches (host clock, HBM-resident inputs)",
+            "single_batch_latency_runs_ms": lat_runs,
+            "strong_scaling_batch": strong,
+            "allocs_in_timed_region": allocs_timed,
+            "cfg0_n256": cfg0,
+            "cfg0_cpu_n256_ms": cfg0_cpu_ms,
             "phase_ms_avg_in_timed_region": phases,
             "phase_ms_single_batch": phases_single,
             "compressed_subgroup": comp,

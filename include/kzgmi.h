@@ -46,6 +46,11 @@ extern "C" {
 
 typedef enum { KZGMI_BLS12_381 = 0, KZGMI_BN254 = 1 } kzgmi_curve;
 
+/* ABI revision of this header.  2: kzgmi_srs_load gained the g1 argument (3rd position),
+ * kzgmi_ctx_reserve / kzgmi_alloc_count / kzgmi_abi_version were added.  A caller built
+ * against another revision must not bind the library: compare with kzgmi_abi_version(). */
+#define KZGMI_ABI_VERSION 2
+
 #define KZGMI_OK 0
 #define KZGMI_ERR_ARG (-1)
 #define KZGMI_ERR_ENCODING (-2)
@@ -79,6 +84,8 @@ typedef struct kzgmi_ck kzgmi_ck;   /* prover commit key: [tau^i]_1 + fixed-base
 
 /* Version string of the library build. */
 const char* kzgmi_version(void);
+/* KZGMI_ABI_VERSION the library was built with. */
+int kzgmi_abi_version(void);
 /* Thread-local description of the last error. */
 const char* kzgmi_last_error(void);
 
@@ -95,10 +102,22 @@ void kzgmi_ctx_destroy(kzgmi_ctx* ctx);
  * over all devices (balanced, in units of 4096), run the shards concurrently and combine the
  * partial sums on the primary; kzgmi_batch_verify_multi_device / kzgmi_msm_g1_multi_device take
  * shards already resident on each device.  The exchange is 2 (batch) or 1 (MSM) partial
- * records per device, copied to the primary with hipMemcpyPeer (xGMI); processes that own one
- * GPU each instead all-gather kzgmi_batch_partial_device records over RCCL. */
+ * records per device, copied to the primary with hipMemcpyPeerAsync (xGMI) on the primary's
+ * slot-0 stream after every shard completed; processes that own one GPU each instead
+ * all-gather kzgmi_batch_partial_device records over RCCL.  Peer devices get
+ * one workspace each (their shard); pipeline_slots applies to the primary. */
 int kzgmi_ctx_create_multi(kzgmi_ctx** out, const int* device_ids, int n_devices, int pipeline_slots);
 int kzgmi_ctx_num_devices(const kzgmi_ctx* ctx);
+
+/* Size every pipeline slot's device workspace (and, on a multi-device context, each device's
+ * shard workspace) for batches of up to n tuples of `curve` verified with `flags`
+ * (KZGMI_FLAG_*), and create the profiling events, so that later batch calls of at most that
+ * size and mode allocate nothing.  Workspaces otherwise grow on first use; a caller timing a
+ * steady state calls this first.  No job may be in flight. */
+int kzgmi_ctx_reserve(kzgmi_ctx* ctx, kzgmi_curve curve, size_t n, uint32_t flags);
+/* Process-wide number of device workspace allocations the library has made so far (a timed
+ * region that leaves it unchanged allocated nothing). */
+uint64_t kzgmi_alloc_count(void);
 
 /* Order slot `slot`'s stream after all work enqueued so far on `hip_stream` (a hipStream_t of
  * the ctx's primary device, passed as void*; NULL = the null stream), without a host sync. */
@@ -288,7 +307,8 @@ int kzgmi_set_trusted_g1(kzgmi_ctx* ctx, int on);
  * When enabled, every batch / MSM call records HIP events around each phase on the stream
  * its kernels run on; kzgmi_get_phase_ms() returns the per-phase device time (ms) averaged
  * over all calls completed since profiling was (re)enabled, in the order of
- * kzgmi_phase_names() (comma-separated).  Enabling resets the averages. */
+ * kzgmi_phase_names() (comma-separated).  Enabling resets the averages.  On a multi-device
+ * context the switch applies to every device and the times are the primary device's. */
 int kzgmi_set_profiling(kzgmi_ctx* ctx, int on);
 const char* kzgmi_phase_names(void);
 int kzgmi_get_phase_ms(kzgmi_ctx* ctx, double* out, int max_n);

@@ -8,12 +8,15 @@
 #include "launch.hpp"
 #include "kzgmi.h"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include <sys/random.h>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 using namespace kzgmi;
@@ -39,6 +42,10 @@ int fail(int code, const std::string& msg) {
     if (r_ != 0) return r_;     \
   } while (0)
 
+// process-wide count of workspace (re)allocations: kzgmi_alloc_count(), so a caller (bench.py,
+// tests) can check that kzgmi_ctx_reserve left nothing to allocate inside a timed region
+std::atomic<uint64_t> g_allocs{0};
+
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -50,6 +57,7 @@ struct DevBuf {
     cap = 0;
     if (hipMalloc(&p, bytes) != hipSuccess) return fail(KZGMI_ERR_OOM, "hipMalloc failed (" + std::to_string(bytes) + " bytes)");
     cap = bytes;
+    g_allocs.fetch_add(1, std::memory_order_relaxed);
     return 0;
   }
   void release() {
@@ -58,6 +66,15 @@ struct DevBuf {
     cap = 0;
   }
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// roctx range over a host-side scope (SURVEY.md 5 tracing): the enqueue of each batch phase and
+// every blocking wait, visible in `rocprofv3 --marker-trace` beside the kernels they issue
+struct Roctx {
+  explicit Roctx(const char* m) { roctxRangePushA(m); }
+  ~Roctx() { roctxRangePop(); }
+  Roctx(const Roctx&) = delete;
+  Roctx& operator=(const Roctx&) = delete;
 };
 
 const char* const kPhaseNames = "convert,scalars,sort,accumulate,reduce,combine,pairing";
@@ -193,7 +210,8 @@ int map_device_err(uint32_t e) {
 // ------------------------------------------------------------------------------ MSM core
 template <class Cv>
 int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, size_t emax, const MsmWindows& mw,
-                 const Affine<Cv>* pts = nullptr, const uint8_t* inf = nullptr, bool pts29 = false) {
+                 const Affine<Cv>* pts = nullptr, const uint8_t* inf = nullptr, bool pts29 = false,
+                 bool dry = false) {
   // pts == nullptr: the slot's freshly converted points, put into the accumulation's format
   // here unless convert_points stored them in it already (pts29); explicit pts (commit-key
   // rows) are stored in that format already (kzgmi_ck_load)
@@ -234,6 +252,8 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   CHK(s.scratch.ensure((size_t)nsets * RB_PARTS * sizeof(XY)));  // k_reduce_bits partial sums
   CHK(s.winsum.ensure((size_t)nsets * sizeof(XY)));
   CHK(s.res.ensure(2 * sizeof(XY)));
+  if (dry) return 0;  // kzgmi_ctx_reserve: workspace sized, nothing enqueued
+  Roctx rx("kzgmi.msm.sort+accumulate+reduce+combine");
   hipStream_t st = s.stream;
   using L = Launch<Cv>;
   if (own_pts) {
@@ -304,11 +324,24 @@ int enqueue_fs_challenge(Slot& s, const uint32_t* digests, uint32_t nch, uint64_
   return 0;
 }
 
+// the workspaces enqueue_fs_digests + enqueue_fs_challenge grow for a batch of n tuples
+template <class Cv>
+int reserve_fs(Slot& s, size_t n) {
+  const uint32_t nch = (uint32_t)((n + FS_CHUNK - 1) / FS_CHUNK);
+  const size_t slots = (size_t)nch * FS_CHUNK;
+  CHK(s.fs_leaves.ensure(slots * 32));
+  CHK(s.fs_tmp.ensure(slots * 24 + 64));
+  CHK(s.fs_top.ensure((size_t)next_pow2(nch) * 32 * 2 + 64));
+  CHK(s.pow.ensure(FS_POW_BITS * sizeof(Fp<typename Cv::FrP>)));
+  CHK(s.chal.ensure(32));
+  return 0;
+}
+
 // ------------------------------------------------------------------------------ batch
 template <class Cv>
 int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, const void* dz, const void* dy,
                   const void* dpi, size_t n, const Seed& seed, uint64_t offset, void* d_partial_out,
-                  uint32_t flags) {
+                  uint32_t flags, bool dry = false) {
   using XY = Xyzz<Cv>;
   using FrF = Fp<typename Cv::FrP>;
   const bool glv = c->glv_batch &&
@@ -331,53 +364,63 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   CHK(s.scal_t.ensure(32));
   CHK(s.tpart.ensure(L::tpart_bytes((uint32_t)n)));
   CHK(s.flags.ensure(16));
+  if (dry) {  // kzgmi_ctx_reserve: the randomiser workspaces of this mode, no launches
+    if (flags & KZGMI_FLAG_FIAT_SHAMIR) CHK(reserve_fs<Cv>(s, n));
+    else if (flags & KZGMI_FLAG_POWERS) CHK(s.pow.ensure(FS_POW_BITS * sizeof(FrF)));
+  }
   hipStream_t st = s.stream;
-  mark(c, s, 0);
-  HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
   uint32_t* err = s.flags.template as<uint32_t>() + 1;
   Affine<Cv>* pts = s.pts.template as<Affine<Cv>>();
   uint8_t* inf = s.inf.template as<uint8_t>();
   // points that only feed the radix-29 accumulation are converted straight into its format
   const bool pts29 = kAcc29<Cv> && !glv && !(flags & (KZGMI_FLAG_COMPRESSED | KZGMI_FLAG_SUBGROUP_CHECK));
-  if (flags & KZGMI_FLAG_COMPRESSED) {
-    L::decompress_points(st, (const uint8_t*)dpi, (uint32_t)n, pts, inf, err);
-    L::decompress_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err);
-  } else {
-    L::convert_points(st, (const uint8_t*)dpi, (uint32_t)n, pts, inf, err, pts29);
-    L::convert_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err, pts29);
-  }
-  if (flags & KZGMI_FLAG_SUBGROUP_CHECK) L::subgroup_check(st, pts, inf, (uint32_t)(2 * n), err);
-  // the SRS's [1]_1 as the last term of MSM#1: -t [1]_1
-  HIPCHK(hipMemcpyAsync(pts + 2 * n, pts29 ? srs->g1_29() : srs->g1.p, sizeof(Affine<Cv>), hipMemcpyDeviceToDevice, st));
-  HIPCHK(hipMemcpyAsync(inf + 2 * n, srs->g1.template as<uint8_t>() + sizeof(Affine<Cv>), 1, hipMemcpyDeviceToDevice, st));
-  if (glv) L::endo_points(st, pts, inf, (uint32_t)PH, pts + PH, inf + PH);
-  mark(c, s, PH_CONVERT + 1);
-  if (flags & KZGMI_FLAG_FIAT_SHAMIR) {  // r from the transcript of this (whole) batch
-    const uint32_t* digests = nullptr;
-    CHK(enqueue_fs_digests<Cv>(s, dC, dpi, dz, dy, n, 0, (flags & KZGMI_FLAG_COMPRESSED) != 0, &digests));
-    CHK(enqueue_fs_challenge<Cv>(s, digests, (uint32_t)((n + FS_CHUNK - 1) / FS_CHUNK), n));
-  } else if (flags & KZGMI_FLAG_POWERS) {  // r supplied by the caller in place of the seed
-    CHK(s.pow.ensure(FS_POW_BITS * sizeof(FrF)));
-    L::pow_table(st, seed, s.pow.p, err);
-  }
-  if (powers)
-    L::scalar_prep_pow(st, s.pow.p, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n,
-                       s.scal_r.template as<uint32_t>(), s.scal_s.template as<uint32_t>(), s.tpart.p,
-                       s.scal_t.template as<uint32_t>(), err);
-  else
-    L::scalar_prep(st, seed, (flags & KZGMI_FLAG_FIAT_SHAMIR) ? s.chal.template as<uint32_t>() : nullptr, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n,
-                   s.scal_r.template as<uint32_t>(), s.scal_s.template as<uint32_t>(), s.tpart.p,
-                   s.scal_t.template as<uint32_t>(), err);
   const uint32_t nn = (uint32_t)n;
   uint32_t* gs = s.glv_s.template as<uint32_t>();
   uint32_t* gt = s.glv_t.template as<uint32_t>();
   uint32_t* gr = s.glv_r.template as<uint32_t>();
-  if (glv) {
-    L::glv_split(st, s.scal_s.template as<uint32_t>(), 8, nn, gs, gs + 4 * (size_t)n);
-    L::glv_split(st, s.scal_t.template as<uint32_t>(), 8, 1, gt, gt + 4);
-    if (powers) L::glv_split(st, s.scal_r.template as<uint32_t>(), 8, nn, gr, gr + 4 * (size_t)n);
-  }
-  mark(c, s, PH_SCALARS + 1);
+  // decode + validate the points, derive the randomisers and the MSM scalars
+  auto front = [&]() -> int {
+    Roctx rx("kzgmi.batch.convert+scalars");
+    mark(c, s, 0);
+    HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
+    if (flags & KZGMI_FLAG_COMPRESSED) {
+      L::decompress_points(st, (const uint8_t*)dpi, (uint32_t)n, pts, inf, err);
+      L::decompress_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err);
+    } else {
+      L::convert_points(st, (const uint8_t*)dpi, (uint32_t)n, pts, inf, err, pts29);
+      L::convert_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err, pts29);
+    }
+    if (flags & KZGMI_FLAG_SUBGROUP_CHECK) L::subgroup_check(st, pts, inf, (uint32_t)(2 * n), err);
+    // the SRS's [1]_1 as the last term of MSM#1: -t [1]_1
+    HIPCHK(hipMemcpyAsync(pts + 2 * n, pts29 ? srs->g1_29() : srs->g1.p, sizeof(Affine<Cv>), hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(inf + 2 * n, srs->g1.template as<uint8_t>() + sizeof(Affine<Cv>), 1, hipMemcpyDeviceToDevice, st));
+    if (glv) L::endo_points(st, pts, inf, (uint32_t)PH, pts + PH, inf + PH);
+    mark(c, s, PH_CONVERT + 1);
+    if (flags & KZGMI_FLAG_FIAT_SHAMIR) {  // r from the transcript of this (whole) batch
+      const uint32_t* digests = nullptr;
+      CHK(enqueue_fs_digests<Cv>(s, dC, dpi, dz, dy, n, 0, (flags & KZGMI_FLAG_COMPRESSED) != 0, &digests));
+      CHK(enqueue_fs_challenge<Cv>(s, digests, (uint32_t)((n + FS_CHUNK - 1) / FS_CHUNK), n));
+    } else if (flags & KZGMI_FLAG_POWERS) {  // r supplied by the caller in place of the seed
+      CHK(s.pow.ensure(FS_POW_BITS * sizeof(FrF)));
+      L::pow_table(st, seed, s.pow.p, err);
+    }
+    if (powers)
+      L::scalar_prep_pow(st, s.pow.p, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n,
+                         s.scal_r.template as<uint32_t>(), s.scal_s.template as<uint32_t>(), s.tpart.p,
+                         s.scal_t.template as<uint32_t>(), err);
+    else
+      L::scalar_prep(st, seed, (flags & KZGMI_FLAG_FIAT_SHAMIR) ? s.chal.template as<uint32_t>() : nullptr, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n,
+                     s.scal_r.template as<uint32_t>(), s.scal_s.template as<uint32_t>(), s.tpart.p,
+                     s.scal_t.template as<uint32_t>(), err);
+    if (glv) {
+      L::glv_split(st, s.scal_s.template as<uint32_t>(), 8, nn, gs, gs + 4 * (size_t)n);
+      L::glv_split(st, s.scal_t.template as<uint32_t>(), 8, 1, gt, gt + 4);
+      if (powers) L::glv_split(st, s.scal_r.template as<uint32_t>(), 8, nn, gr, gr + 4 * (size_t)n);
+    }
+    mark(c, s, PH_SCALARS + 1);
+    return 0;
+  };
+  if (!dry) CHK(front());
   TermList tl{};
   const uint32_t ph = (uint32_t)PH;
   if (glv) {  // every MSM in 8 windows of half scalars: sets 0..7 (MSM#0), 8..15 (MSM#1)
@@ -400,7 +443,7 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
     tl.total = 0;
     for (uint32_t j = 0; j < k; ++j) tl.total += tl.c[j].count;
     const MsmWindows mw{2, {0, 8}, {8, 8}};
-    CHK(run_msm_core<Cv>(c, s, tl, 16, (size_t)(powers ? 48 : 32) * n + 16, mw));
+    CHK(run_msm_core<Cv>(c, s, tl, 16, (size_t)(powers ? 48 : 32) * n + 16, mw, nullptr, nullptr, false, dry));
   } else if (!powers) {  // 127-bit r_i: MSM#0 in 8 windows (sets 0..7), MSM#1 in 16 (sets 8..23)
     tl.c[0] = {nn, 0, 4, 8, 0, 4, s.scal_r.template as<uint32_t>()};          // MSM#0: r_i pi_i
     tl.c[1] = {nn, nn, 4, 8, 8, 4, s.scal_r.template as<uint32_t>()};         // MSM#1: r_i C_i
@@ -417,8 +460,11 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
     tl.nclass = 4;
     tl.total = 3 * nn + 1;
     const MsmWindows mw = powers ? MsmWindows{2, {0, 16}, {16, 16}} : MsmWindows{2, {0, 8}, {8, 16}};
-    CHK(run_msm_core<Cv>(c, s, tl, powers ? 32 : 24, (size_t)(powers ? 48 : 32) * n + 16, mw, nullptr, nullptr, pts29));
+    CHK(run_msm_core<Cv>(c, s, tl, powers ? 32 : 24, (size_t)(powers ? 48 : 32) * n + 16, mw, nullptr, nullptr, pts29,
+                         dry));
   }
+  if (dry) return 0;
+  Roctx rx("kzgmi.batch.pairing");
   if (d_partial_out) {
     HIPCHK(hipMemcpyAsync(d_partial_out, s.res.p, 2 * sizeof(XY), hipMemcpyDeviceToDevice, st));
   } else {
@@ -436,7 +482,10 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
 }
 
 int finish_slot(kzgmi_ctx* c, Slot& s, int* ok_out) {
-  HIPCHK(hipStreamSynchronize(s.stream));
+  {
+    Roctx rx("kzgmi.slot_wait");
+    HIPCHK(hipStreamSynchronize(s.stream));
+  }
   s.pending = false;
   collect_phases(c, s);
   int e = map_device_err((uint32_t)s.host_flags[1]);
@@ -490,7 +539,9 @@ int ensure_table(kzgmi_ctx* c, hipStream_t st) {
 // ================================================================================ C ABI
 extern "C" {
 
-const char* kzgmi_version(void) { return "kzgmi 0.1 (gfx950, HIP)"; }
+const char* kzgmi_version(void) { return "kzgmi 0.3 (abi 2, gfx950, HIP)"; }
+int kzgmi_abi_version(void) { return KZGMI_ABI_VERSION; }
+uint64_t kzgmi_alloc_count(void) { return g_allocs.load(std::memory_order_relaxed); }
 const char* kzgmi_last_error(void) { return g_err.c_str(); }
 const char* kzgmi_phase_names(void) { return kPhaseNames; }
 
@@ -557,6 +608,31 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
   peers.swap(c->peers);
   delete c;
   for (kzgmi_ctx* p : peers) kzgmi_ctx_destroy(p);
+}
+
+int kzgmi_ctx_reserve(kzgmi_ctx* c, kzgmi_curve curve, size_t n, uint32_t flags) {
+  CHK(check_ctx(c));
+  if (flags & ~kAllFlags) return fail(KZGMI_ERR_ARG, "unknown flags");
+  if ((flags & KZGMI_FLAG_POWERS) && (flags & KZGMI_FLAG_FIAT_SHAMIR))
+    return fail(KZGMI_ERR_ARG, "KZGMI_FLAG_POWERS and KZGMI_FLAG_FIAT_SHAMIR are exclusive");
+  if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "batch too large (max 2^26 tuples per call)");
+  for (auto& s : c->slots)
+    if (s.pending) return fail(KZGMI_ERR_ARG, "kzgmi_ctx_reserve with jobs in flight");
+  const Seed none{};
+  for (auto& s : c->slots) {
+    if (n)
+      CHK(dispatch(curve, [&](auto cv) -> int {
+        return enqueue_batch<decltype(cv)>(c, s, nullptr, nullptr, nullptr, nullptr, nullptr, n, none, 0, nullptr, flags,
+                                           /*dry=*/true);
+      }));
+    for (auto& e : s.ev)  // the phase events kzgmi_set_profiling records
+      if (!e) HIPCHK(hipEventCreate(&e));
+  }
+  // multi-device context: each peer runs one shard of at most ceil(n / devices) (4096-aligned)
+  const size_t D = 1 + c->peers.size();
+  const size_t per = ((n + D - 1) / D + FS_CHUNK - 1) / FS_CHUNK * FS_CHUNK;
+  for (kzgmi_ctx* p : c->peers) CHK(kzgmi_ctx_reserve(p, curve, std::min(n, per), flags));
+  return set_dev(c);
 }
 
 int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uint8_t* g2, const uint8_t* tau_g2,
@@ -683,6 +759,7 @@ int kzgmi_batch_verify_device_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int s
     s.msm_job = false;
     return 0;
   }
+  Roctx rx("kzgmi_batch_verify_device_ex_async");
   return dispatch(srs->curve, [&](auto cv) -> int {
     return enqueue_batch<decltype(cv)>(c, s, srs, dC, dz, dy, dpi, n, seed, 0, nullptr, flags);
   });
@@ -969,6 +1046,7 @@ int kzgmi_msm_g1_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, const v
   if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "MSM too large (max 2^26 points per call)");
   Slot& s = c->slots[slot];
   if (s.pending) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_msm_wait first");
+  Roctx rx("kzgmi_msm_g1_device_async");
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     const size_t gb = g1_bytes(Cv::ID);
@@ -1030,6 +1108,7 @@ size_t kzgmi_partial_bytes(kzgmi_curve curve) {
 int kzgmi_batch_partial_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const void* dC, const void* dz,
                                      const void* dy, const void* dpi, size_t n, uint64_t index_offset,
                                      const uint8_t* seed32, uint32_t flags, void* d_partial_out) {
+  Roctx rx("kzgmi_batch_partial_device_async");
   if (flags & ~kAllFlags) return fail(KZGMI_ERR_ARG, "unknown flags");
   if (flags & KZGMI_FLAG_FIAT_SHAMIR)
     return fail(KZGMI_ERR_ARG, "shards take the Fiat-Shamir r as seed32 (see kzgmi_fs_challenge_from_digests_device)");
@@ -1237,6 +1316,7 @@ int kzgmi_msm_partial_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dpts, 
 int kzgmi_msm_partial_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, const void* dpts, const void* dsc,
                                    size_t n, void* d_partial_out) {
   CHK(check_ctx(c, slot));
+  Roctx rx("kzgmi_msm_partial_device_async");
   if (!d_partial_out || (n && (!dpts || !dsc))) return fail(KZGMI_ERR_ARG, "bad argument");
   if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "MSM too large (max 2^26 points per call)");
   Slot& s = c->slots[slot];
@@ -1480,6 +1560,9 @@ int kzgmi_set_profiling(kzgmi_ctx* c, int on) {
   c->profiling = on != 0;
   for (int k = 0; k < kNumPhases; ++k) c->phase_ms[k] = 0;
   c->phase_calls = 0;
+  // multi-device context: every device records its phases; kzgmi_get_phase_ms reports the
+  // primary device's (the peers' shards run the same phases concurrently)
+  for (kzgmi_ctx* p : c->peers) CHK(kzgmi_set_profiling(p, on));
   return 0;
 }
 
@@ -1525,7 +1608,7 @@ int kzgmi_ctx_create_multi(kzgmi_ctx** out, const int* device_ids, int n_devices
   CHK(kzgmi_ctx_create(&c, device_ids[0], pipeline_slots));
   for (int k = 1; k < n_devices; ++k) {
     kzgmi_ctx* p = nullptr;
-    if (int r = kzgmi_ctx_create(&p, device_ids[k], pipeline_slots)) {
+    if (int r = kzgmi_ctx_create(&p, device_ids[k], 1)) {  // peers only ever run on their slot 0
       kzgmi_ctx_destroy(c);
       return r;
     }
@@ -1563,13 +1646,17 @@ int wait_all(kzgmi_ctx* c, int started) {
   return 0;
 }
 
-// children's records (in their `gath`) -> c->gath[d]
+// children's records (in their `gath`, complete: wait_all synchronised every peer's slot 0) ->
+// c->gath[d], copied on the primary's slot-0 stream, the stream kzgmi_batch_combine_device /
+// kzgmi_msm_combine_device then read them on -- so the order is explicit, not left to how the
+// runtime orders a null-stream peer copy against a non-blocking stream
 int gather_records(kzgmi_ctx* c, size_t rec) {
+  CHK(set_dev(c));
   for (size_t d = 1; d <= c->peers.size(); ++d) {
     kzgmi_ctx* p = c->peers[d - 1];
-    HIPCHK(hipMemcpyPeer((uint8_t*)c->gath.p + d * rec, c->device, p->gath.p, p->device, rec));
+    HIPCHK(hipMemcpyPeerAsync((uint8_t*)c->gath.p + d * rec, c->device, p->gath.p, p->device, rec, c->slots[0].stream));
   }
-  return set_dev(c);
+  return 0;
 }
 
 int batch_multi(kzgmi_ctx* c, const kzgmi_srs* srs, const void* const* dC, const void* const* dz,
@@ -1605,7 +1692,11 @@ int batch_multi(kzgmi_ctx* c, const kzgmi_srs* srs, const void* const* dC, const
       CHK(p->mdig.ensure(nch * 32));
       CHK(kzgmi_fs_chunk_digests_device(p, curve, dC[d], dz[d], dy[d], dpi[d], nd[d], off[d],
                                         flags & KZGMI_FLAG_COMPRESSED, p->mdig.p));
-      HIPCHK(hipMemcpyPeer((uint8_t*)c->mdig_all.p + at * 32, c->device, p->mdig.p, p->device, nch * 32));
+      // kzgmi_fs_chunk_digests_device returned with p's digests complete; the copy is ordered
+      // before the challenge derivation on the primary's slot-0 stream
+      CHK(set_dev(c));
+      HIPCHK(hipMemcpyPeerAsync((uint8_t*)c->mdig_all.p + at * 32, c->device, p->mdig.p, p->device, nch * 32,
+                                c->slots[0].stream));
       at += nch;
     }
     CHK(kzgmi_fs_challenge_from_digests_device(c, curve, c->mdig_all.p, nch_tot, ntot, sb));

@@ -22,6 +22,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # KZGMI_LIB selects an alternative build (timing experiments); default: the in-tree library
 LIB_PATH = os.environ.get("KZGMI_LIB") or os.path.join(_HERE, "libkzgmi.so")
 
+ABI_VERSION = 2  # include/kzgmi.h KZGMI_ABI_VERSION
 CURVES = {"bls12_381": 0, "bn254": 1}
 FP_BYTES = {"bls12_381": 48, "bn254": 32}
 PHASES = ["convert", "scalars", "sort", "accumulate", "reduce", "combine", "pairing"]
@@ -65,6 +66,9 @@ def lib():
         "kzgmi_srs_load": ([vp, c.c_int, u8p, u8p, u8p, c.POINTER(vp)], c.c_int),
         "kzgmi_ctx_create_multi": ([c.POINTER(vp), c.POINTER(c.c_int), c.c_int, c.c_int], c.c_int),
         "kzgmi_ctx_num_devices": ([vp], c.c_int),
+        "kzgmi_abi_version": ([], c.c_int),
+        "kzgmi_ctx_reserve": ([vp, c.c_int, sz, c.c_uint32], c.c_int),
+        "kzgmi_alloc_count": ([], c.c_uint64),
         "kzgmi_stream_wait": ([vp, c.c_int, vp], c.c_int),
         "kzgmi_partial_encode_device": ([vp, c.c_int, vp, sz, u8p], c.c_int),
         "kzgmi_batch_verify_multi_device": ([vp, vp, c.POINTER(vp), c.POINTER(vp), c.POINTER(vp), c.POINTER(vp),
@@ -116,6 +120,9 @@ def lib():
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
+    if L.kzgmi_abi_version() != ABI_VERSION:  # include/kzgmi.h KZGMI_ABI_VERSION
+        raise ImportError("libkzgmi.so ABI %d, this binding expects %d (rebuild: __graft_entry__.build())"
+                          % (L.kzgmi_abi_version(), ABI_VERSION))
     _lib = L
     return L
 
@@ -137,6 +144,7 @@ def exported_symbols():
         "kzgmi_g2_mul", "kzgmi_probe_fpmul", "kzgmi_set_profiling", "kzgmi_get_phase_ms",
         "kzgmi_ctx_create_multi", "kzgmi_ctx_num_devices", "kzgmi_stream_wait", "kzgmi_partial_encode_device",
         "kzgmi_batch_verify_multi_device", "kzgmi_msm_g1_multi_device",
+        "kzgmi_abi_version", "kzgmi_ctx_reserve", "kzgmi_alloc_count",
     ]
 
 
@@ -270,6 +278,13 @@ class Context:
 
     def num_devices(self) -> int:
         return int(lib().kzgmi_ctx_num_devices(self.handle))
+
+    def reserve(self, curve: str, n: int, compressed: bool = False, subgroup_check: bool = False,
+                fiat_shamir: bool = False, powers: bool = False, trusted_g1: bool = False):
+        """kzgmi_ctx_reserve: size every slot's workspace for batches of up to n tuples in this
+        mode (and create the profiling events) -- later calls of that size allocate nothing."""
+        fl = _flags(compressed, subgroup_check, fiat_shamir, 0 if powers else None, trusted_g1)
+        _check(lib().kzgmi_ctx_reserve(self.handle, CURVES[curve], int(n), fl))
 
     def _order(self, slot: int = 0):
         """Order `slot`'s stream after torch's current stream (device inputs written by torch)."""
@@ -651,6 +666,11 @@ G2_GENERATOR = {
 }
 
 _default_ctx: Optional[Context] = None
+
+
+def alloc_count() -> int:
+    """Process-wide number of device workspace allocations made by the library so far."""
+    return int(lib().kzgmi_alloc_count())
 
 
 def default_context() -> Context:

@@ -11,7 +11,8 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+# KZGO_LIB: an alternative build of the same source (the ASan/UBSan one, `make -C oracle sanitize`)
+LIB_PATH = os.environ.get("KZGO_LIB") or os.path.join(HERE, "build", "liboracle.so")
 CURVE_IDS = {"bls12_381": 0, "bn254": 1}
 FP_BYTES = {"bls12_381": 48, "bn254": 32}
 

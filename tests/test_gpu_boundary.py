@@ -306,3 +306,45 @@ def test_two_rank_gloo_pipeline_on_gpu():
     for p, out in zip(procs, outs):
         assert p.returncode == 0, out[-3000:]
         assert "RANK OK" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("curve,mode", [("bls12_381", {}), ("bls12_381", {"trusted_g1": True}),
+                                        ("bls12_381", {"fiat_shamir": True}), ("bn254", {})])
+def test_reserve_leaves_nothing_to_allocate(curve, mode):
+    """kzgmi_ctx_reserve sizes every slot for the mode: pipelined batches of at most that size then
+    make no workspace allocation (kzgmi_alloc_count unchanged), and verify as the oracle does."""
+    import kzgmi
+    n, slots = 5000, 3
+    c = kzgmi.Context(0, slots)
+    try:
+        tau = 0x1234567890ABCDEF
+        srs = c.load_srs(curve, kzgmi.G2_GENERATOR[curve], c.g2_mul(curve, kzgmi.G2_GENERATOR[curve], tau))
+        Cm, z, y, P = _gen_batch(c, curve, n, tau, hashlib.sha256(b"reserve").digest())
+        c.reserve(curve, n, **mode)
+        a0 = kzgmi.alloc_count()
+        seed = None if mode.get("fiat_shamir") else hashlib.sha256(b"r").digest()
+        for k in range(2 * slots):                      # every slot used twice, two sizes
+            s = k % slots
+            if k >= slots:
+                assert c.wait(s)
+            c.batch_verify_async(srs, s, Cm, z, y, P, n if k % 2 == 0 else n - 17, seed=seed, **mode)
+        for s in range(slots):
+            assert c.wait(s)
+        assert kzgmi.alloc_count() == a0, "a reserved context allocated inside the steady state"
+        c.batch_verify_async(srs, 0, Cm, z, y, P, n, seed=seed, **mode)  # still accepts after the reuse
+        assert c.wait(0)
+        # a larger batch than reserved still works (the workspace grows)
+        Cm2, z2, y2, P2 = _gen_batch(c, curve, 2 * n, tau, hashlib.sha256(b"reserve2").digest())
+        assert c.batch_verify(srs, Cm2, z2, y2, P2, seed=seed, n=2 * n, **mode)
+        assert kzgmi.alloc_count() > a0
+    finally:
+        c.close()
+
+
+def test_reserve_argument_checks(ctx):
+    import kzgmi
+    with pytest.raises(kzgmi.KzgmiError):
+        kzgmi.lib().kzgmi_ctx_reserve(ctx.handle, 0, 1 << 27, 0)   # above the 2^26 per-call limit
+    with pytest.raises(kzgmi.KzgmiError):
+        ctx.reserve("bls12_381", 16, fiat_shamir=True, powers=True)  # exclusive modes
+    assert kzgmi.lib().kzgmi_abi_version() == kzgmi.ABI_VERSION
