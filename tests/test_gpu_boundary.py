@@ -343,8 +343,8 @@ def test_reserve_leaves_nothing_to_allocate(curve, mode):
 
 def test_reserve_argument_checks(ctx):
     import kzgmi
-    with pytest.raises(kzgmi.KzgmiError):
-        kzgmi.lib().kzgmi_ctx_reserve(ctx.handle, 0, 1 << 27, 0)   # above the 2^26 per-call limit
+    assert kzgmi.lib().kzgmi_ctx_reserve(ctx.handle, 0, 1 << 27, 0) == -1   # above the 2^26 per-call limit
+    assert kzgmi.lib().kzgmi_ctx_reserve(ctx.handle, 0, 16, 1 << 10) == -1  # unknown flag
     with pytest.raises(kzgmi.KzgmiError):
         ctx.reserve("bls12_381", 16, fiat_shamir=True, powers=True)  # exclusive modes
     assert kzgmi.lib().kzgmi_abi_version() == kzgmi.ABI_VERSION
