@@ -85,7 +85,7 @@ struct Slot {
   hipStream_t stream = nullptr;
   DevBuf pts, inf, scal_r, scal_s, scal_t, tpart, cnt, off, coarse, ent, total, sval, skey;
   DevBuf buckets, pfirst, plast, R, U, scratch, winsum, res, flags, stage, outb;
-  DevBuf acc29;                                  // radix-29 bucket records (BLS12-381, msm.hpp)
+  DevBuf acc29;                                  // radix-29 bucket records (msm.hpp)
   DevBuf fs_leaves, fs_tmp, fs_top, pow, chal;  // Fiat-Shamir / powers-of-r randomisers
   DevBuf glv_r, glv_s, glv_t;                    // GLV half scalars (glv.hpp): [h0 x n | h1 x n]
   DevBuf digits;                                 // signed window digit codes of every term (msm.hpp)
@@ -144,7 +144,7 @@ struct kzgmi_srs {
   kzgmi_ctx* ctx = nullptr;
   DevBuf lines, q, q_inf;
   DevBuf g1;                        // the SRS's [1]_1: Montgomery affine point + its infinity byte after it,
-  size_t g1_29_off = 0;             // then (BLS12-381) the same point in the accumulation's radix-29 format
+  size_t g1_29_off = 0;             // then the same point in the accumulation's radix-29 format
   void* g1_29() const { return static_cast<uint8_t*>(g1.p) + g1_29_off; }
   std::vector<kzgmi_srs*> peers;    // multi-device context: the same SRS on each peer device
 };
@@ -238,9 +238,10 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   CHK(s.coarse.ensure((size_t)3 * nsets * BINS_PER_SET * 4));
   CHK(s.ent.ensure(emax * 8));
   CHK(s.total.ensure(16));
-  CHK(s.sval.ensure(emax * 4));
+  CHK(s.sval.ensure(emax * 4 + 16));  // + 16: k_accumulate reads values 4 at a time, up to 3 past the end
   CHK(s.skey.ensure(emax * 4));
-  if (!kAcc29<Cv>) {  // BLS12-381 keeps buckets and pieces as radix-29 records in acc29
+  constexpr int W29 = kW29<Fp29Of<Cv>>;
+  if (!kAcc29<Cv>) {  // the radix-29 accumulation keeps buckets and pieces as records in acc29
     CHK(s.buckets.ensure((size_t)NB * sizeof(XY)));
     CHK(s.pfirst.ensure(nchunks * sizeof(XY)));
     CHK(s.plast.ensure(nchunks * sizeof(XY)));

@@ -1,31 +1,39 @@
-// Radix-2^29 Montgomery arithmetic for BLS12-381: the bucket accumulation (msm.hpp
-// k_accumulate) and everything around it that is full-chip or on the pipeline's critical path
-// -- the point conversion and on-curve test (kernels.hpp), the piece join and both bucket-sum
-// reductions (msm.hpp x29_add), square roots and the subgroup check (points.hpp).  14 limbs
-// of 29 bits in 32-bit VGPRs, R29 = 2^406.
+// Radix-2^29 Montgomery arithmetic: the bucket accumulation (msm.hpp k_accumulate) and
+// everything around it that is full-chip or on the pipeline's critical path -- the point
+// conversion and on-curve test (kernels.hpp), the piece join and both bucket-sum reductions
+// (msm.hpp x29_add), and on BLS12-381 square roots and the subgroup check (points.hpp).
+// BLS12-381: 14 limbs of 29 bits in 32-bit VGPRs, R29 = 2^406; BN254: 9 limbs, R29 = 2^261.
 //
 // Why: the accumulation is VALU-issue bound, and in the 32-bit-limb product (field.hpp) every
 // limb product costs TWO issue slots, the v_mad_u64_u32 and the v_addc_co_u32 folding its
 // carry-out (tools/probes/mad_rate.hip: both full rate).  With 29-bit limbs every column of
-// the product -- at most 28 (a b) + 14 (m p) products < 2^58 plus the carry -- fits the 64-bit
-// accumulator, so a limb product is ONE v_mad_u64_u32: 392 mads + ~4 column ops x 27 instead
-// of 288 x 2 + column moves.  Additions and subtractions pay a carry pass instead (sub29:
-// a + B - b with B a multiple of p whose limbs are biased into [2^29, 2^30), so no limb goes
-// negative).  Measured in one harness (tools/probes/radix29/acc29.hip): the mixed addition
-// runs 1.17-1.22x faster than the 32-bit lazy form, and it fits 108 VGPRs without spills.
+// the product -- at most 2N (a b) + N (m p) products < 2^58 plus the carry -- fits the 64-bit
+// accumulator, so a limb product is ONE v_mad_u64_u32: 2N^2 mads + ~4 column ops x (2N - 1)
+// (BLS12-381 392 mads instead of 288 x 2 + column moves; BN254 162 instead of 128 x 2).
+// Additions and subtractions pay a carry pass instead (sub29: a + B - b with B a multiple of p
+// whose limbs are biased into [2^29, 2^30), so no limb goes negative).  Measured in one harness
+// (tools/probes/radix29/acc29.hip): the BLS12-381 mixed addition runs 1.17-1.22x faster than
+// the 32-bit lazy form, and it fits 108 VGPRs without spills.
 //
-// Value bounds (all values are normalised: limbs 0..12 < 2^29): a product of inputs below
-// 2^12 p returns < 2p (R29 > 2^24 p); callers track the bounds of sums and differences and
-// pick the bias B_k with k p >= the subtrahend's bound (msm.hpp documents them per step).
+// Value bounds (all values are normalised: limbs 0..N-2 < 2^29): a product of inputs below
+// a p and b p returns below (a b p / R29 + 1) p -- < 2p for a b < 2^24 on BLS12-381 but only
+// for a b < ~169 on BN254 -- so callers track the bounds of sums and differences and pick the
+// bias B_k with k p >= the subtrahend's bound.  The accumulation loop names its biases by role
+// (Q::ACC_*, Q::DBL_*), chosen per curve and checked step by step by tools/gen_params29.py.
 // Reference: none (LICENSE only); checked bit-exactly against the C oracle through the MSM and
-// batch parity tests, which all run through this path on BLS12-381.
+// batch parity tests, which all run through this path.
 #pragma once
 #include "field.hpp"
+#include <type_traits>
 #include "params29_gen.hpp"
 
 namespace kzgmi {
 
 constexpr uint32_t M29 = (1u << 29) - 1;
+
+// the radix-2^29 parameters of a curve's base field (Cv::ID 0: BLS12-381, 1: BN254)
+template <class Cv>
+using Fp29Of = std::conditional_t<Cv::ID == 0, Bls12_381Fp29, Bn254Fp29>;
 
 template <class Q>
 struct F29 {

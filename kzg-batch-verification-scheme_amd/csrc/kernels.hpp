@@ -46,7 +46,7 @@ KZ_DEV void fp_to_be_words(const Fp<P>& a, uint32_t (&w)[NW], int o) {
 }
 
 // G1 encoding -> affine Montgomery point + infinity flag (errors into *err)
-// To29 (BLS12-381 only): the validated point is stored directly in the accumulation's radix-29
+// To29: the validated point is stored directly in the accumulation's radix-29
 // format (what k_pts_to29 would make of it), saving that kernel's pass over the points.
 template <class Cv, bool To29 = false>
 __global__ void __launch_bounds__(256) k_convert_points(const uint8_t* __restrict__ bytes, uint32_t n,
@@ -72,8 +72,8 @@ __global__ void __launch_bounds__(256) k_convert_points(const uint8_t* __restric
   } else {
     is_inf = (any | w[0]) == 0;
   }
-  if constexpr (To29) {  // x R29 = mont29(x, R29^2); on-curve test y^2 - x^3 - 4 == 0 in radix 29
-    using Q = Bls12_381Fp29;
+  if constexpr (To29) {  // x R29 = mont29(x, R29^2); on-curve test y^2 - x^3 - b == 0 in radix 29
+    using Q = Fp29Of<Cv>;
     F29<Q> x29 = F29<Q>::zero(), y29 = F29<Q>::zero();
     if (!is_inf) {
       const Fp<P> x = fp_from_be_words<P>(w, 0), y = fp_from_be_words<P>(w, P::N);
@@ -92,12 +92,15 @@ __global__ void __launch_bounds__(256) k_convert_points(const uint8_t* __restric
       }
       if (is_inf) x29 = y29 = F29<Q>::zero();
     }
-    uint32_t w29[2 * Q::N];
+    constexpr int NQ = (2 * Q::N + 3) / 4;  // 16-B stores (BN254: 18 words, zero-padded to 20)
+    uint32_t w29[4 * NQ];
 #pragma unroll
     for (int k = 0; k < Q::N; ++k) { w29[k] = x29.v[k]; w29[Q::N + k] = y29.v[k]; }
+#pragma unroll
+    for (int k = 2 * Q::N; k < 4 * NQ; ++k) w29[k] = 0;
     uint4* d = reinterpret_cast<uint4*>(pts + i);
 #pragma unroll
-    for (int k = 0; k < Q::N / 2; ++k) d[k] = make_uint4(w29[4 * k], w29[4 * k + 1], w29[4 * k + 2], w29[4 * k + 3]);
+    for (int k = 0; k < NQ; ++k) d[k] = make_uint4(w29[4 * k], w29[4 * k + 1], w29[4 * k + 2], w29[4 * k + 3]);
   } else {
     Affine<Cv> a;
     if (is_inf) {

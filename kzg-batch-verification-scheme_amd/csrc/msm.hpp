@@ -57,13 +57,19 @@ struct TermList {
 //   k_bin_scatter same digits; LDS ranks, one global atomic per bin reserves the tile's run,
 //                 entries written as (key << 32 | value) into their coarse bin
 //   k_fine_sort   one workgroup per coarse bin (128 buckets): LDS counting sort, writes the
-//                 sorted (value, key) arrays and every bucket's offset/count
+//                 sorted (value, key) arrays and every bucket's offset/count; the value of
+//                 a bucket's first entry carries SV_FIRST (bit 31), so the accumulation
+//                 streams the values alone and reads a key only where a bucket starts
 // Sorting is unstable inside a bucket; bucket sums (and the final affine result) do not
 // depend on the order.
 constexpr int COARSE_SHIFT = 7;
 constexpr int FINE = 1 << COARSE_SHIFT;                 // buckets per coarse bin
 constexpr int BINS_PER_SET = NBUCKETS >> COARSE_SHIFT;  // 256
 constexpr int TILE_TERMS = 4096;                        // terms per tile (16 per thread)
+// sorted value = point index << 1 | sign, | SV_FIRST on the first entry of each bucket (point
+// indices stay below 2^30: at most 16 x 2^26 commit-key points)
+constexpr uint32_t SV_FIRST = 1u << 31;
+KZ_DEV uint32_t sv_point(uint32_t v) { return (v & ~SV_FIRST) >> 1; }
 
 struct TileRef {
   int k, w;
@@ -305,10 +311,11 @@ static __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __rest
       if (v[j] == ~0ull) continue;
       const uint32_t key = (uint32_t)(v[j] >> 32);
       const uint32_t p = atomicAdd(&cursor[key & (FINE - 1)], 1u);
+      const uint32_t first = p == scan[key & (FINE - 1)] - fine[key & (FINE - 1)] ? SV_FIRST : 0u;
       if (staged) {
-        stage[p] = (uint32_t)v[j];
+        stage[p] = (uint32_t)v[j] | first;
       } else {
-        sorted_val[start + p] = (uint32_t)v[j];
+        sorted_val[start + p] = (uint32_t)v[j] | first;
         sorted_key[start + p] = key;
       }
     }
@@ -374,11 +381,13 @@ KZ_DEV Xyzz<Cv> load_xyzz(const Xyzz<Cv>* src) {
 
 // ------------------------------------------------------------------------------ accumulation
 // Chunk length: every accumulation thread owns `len` consecutive sorted entries, len =
-// max(ACC_CHUNK, ceil(total / nthreads)) for the launched thread count nthreads (the same
-// value in k_accumulate and k_fixup).  nthreads >= total / ACC_CHUNK gives the fixed 64-entry
-// chunks; a smaller grid gives longer, equal chunks (fewer pieces, no partial last round).
+// max(ACC_CHUNK, ceil(total / nthreads)) rounded up to a multiple of 4 (chunks start on 16-B
+// boundaries: the radix-29 loop reads its values 4 at a time) for the launched thread count
+// nthreads (the same value in k_accumulate and k_fixup).  nthreads >= total / ACC_CHUNK gives
+// the fixed 64-entry chunks; a smaller grid gives longer, equal chunks (fewer pieces, no
+// partial last round).
 KZ_DEV uint32_t acc_chunk_len(uint32_t total, uint32_t nthreads) {
-  const uint32_t per = (total + nthreads - 1) / nthreads;
+  const uint32_t per = ((total + nthreads - 1) / nthreads + 3) & ~3u;
   return per > (uint32_t)ACC_CHUNK ? per : (uint32_t)ACC_CHUNK;
 }
 
@@ -404,28 +413,36 @@ KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_
 // addition (x29_add below), writing R/U as records too; k_reduce_bits converts to 32-bit limbs
 // as it reads them.  No conversion at the flushes: some lane of a wavefront changes bucket in
 // almost every step, so per-flush work runs on most iterations.
-#ifndef KZ_NO_ACC29
-template <class Cv>
-constexpr bool kAcc29 = Cv::FpP::N == 12;
-#else  // A/B reference: the 32-bit-limb loop for both curves
+#if defined(KZ_NO_ACC29)  // A/B reference: the 32-bit-limb loop for both curves
 template <class Cv>
 constexpr bool kAcc29 = false;
+#elif defined(KZ_NO_ACC29_BN254)  // A/B reference: BN254 on the 32-bit-limb loop
+template <class Cv>
+constexpr bool kAcc29 = Cv::ID == 0;
+#else
+template <class Cv>
+constexpr bool kAcc29 = true;
 #endif
-constexpr int W29 = 4 * Bls12_381Fp29::N;  // 56 words, 224 B
+// words of a radix-29 XYZZ record: BLS12-381 56 (224 B), BN254 36 (144 B)
+template <class Q>
+constexpr int kW29 = 4 * Q::N;
 
 template <class Cv>
 __global__ void __launch_bounds__(256) k_pts_to29(Affine<Cv>* __restrict__ pts, uint32_t n) {
-  using Q = Bls12_381Fp29;
+  using Q = Fp29Of<Cv>;
+  constexpr int NQ = (2 * Q::N + 3) / 4;  // 16-B stores of x, y (BN254: 18 words, zero-padded to 20)
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const Affine<Cv> a = pts[i];
   const F29<Q> x = fp_to29<Q>(a.x), y = fp_to29<Q>(a.y);
-  uint32_t w[2 * Q::N];
+  uint32_t w[4 * NQ];
 #pragma unroll
   for (int k = 0; k < Q::N; ++k) { w[k] = x.v[k]; w[Q::N + k] = y.v[k]; }
+#pragma unroll
+  for (int k = 2 * Q::N; k < 4 * NQ; ++k) w[k] = 0;
   uint4* d = reinterpret_cast<uint4*>(pts + i);
 #pragma unroll
-  for (int k = 0; k < Q::N / 2; ++k) d[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+  for (int k = 0; k < NQ; ++k) d[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
 }
 
 // ------------------------------------------------------------------------------ radix-29 XYZZ
@@ -438,7 +455,7 @@ struct X29 {
 };
 template <class Q>
 KZ_DEV X29<Q> load_x29(const uint32_t* __restrict__ acc29, size_t r) {
-  constexpr int N = Q::N;
+  constexpr int N = Q::N, W29 = kW29<Q>;
   const uint4* s4 = reinterpret_cast<const uint4*>(acc29 + r * W29);
   uint32_t w[W29];
 #pragma unroll
@@ -461,7 +478,7 @@ KZ_DEV X29<Q> load_x29(const uint32_t* __restrict__ acc29, size_t r) {
 }
 template <class Q>
 KZ_DEV void store_x29(uint32_t* __restrict__ acc29, size_t r, const X29<Q>& a) {
-  constexpr int N = Q::N;
+  constexpr int N = Q::N, W29 = kW29<Q>;
   uint32_t w[W29];
 #pragma unroll
   for (int k = 0; k < N; ++k) {
@@ -545,7 +562,8 @@ KZ_DEV X29<Q> x29_add(const X29<Q>& a, const X29<Q>& b) {
 
 
 // 2Q for an affine Q (rare path: the running sum equals the incoming point), bounds: qx < p,
-// qy < 8p in; x < 10p, y < 10p, zz, zzz < 2p out
+// qy < ACC_NEG p in; out (BLS12-381) x < 10p, y < 10p, zz, zzz < 2p -- per curve in
+// tools/gen_params29.py check_bounds, with the biases Q::DBL_*
 // out of line: its temporaries would otherwise raise the loop's register peak.  ZZ, ZZZ go
 // straight to the caller's LDS columns (stride 256 words) so that arguments and result fit the
 // 32 argument/return VGPRs of a call -- a 56-word return travelled through scratch (304 B of
@@ -557,15 +575,15 @@ struct Xy29 {
 template <class Q>
 __device__ __noinline__ Xy29<Q> dbl_affine29(const F29<Q> qx, const F29<Q> qy, uint32_t* zz, uint32_t* zzz) {
   using G = F29<Q>;
-  const G U = add3_29(qy, qy, G::zero());                             // < 16p
+  const G U = add3_29(qy, qy, G::zero());                             // BLS12-381 < 16p
   const G V = mul29(U, U);
   const G W = mul29(U, V);
   const G S = mul29(qx, V);
   const G X2 = mul29(qx, qx);
   const G M = add3_29(X2, X2, X2);                                    // < 6p
   Xy29<Q> o;
-  o.x = sub29(mul29(M, M), add3_29(S, S, G::zero()), Q::B8);         // < 10p
-  o.y = sub29(mul29(M, sub29(S, o.x, Q::B16)), mul29(W, qy), Q::B8);  // < 10p
+  o.x = sub29(mul29(M, M), add3_29(S, S, G::zero()), Q::DBL_X);         // BLS12-381 < 10p
+  o.y = sub29(mul29(M, sub29(S, o.x, Q::DBL_QX)), mul29(W, qy), Q::DBL_Y);  // BLS12-381 < 10p
 #pragma unroll
   for (int k = 0; k < Q::N; ++k) {
     zz[k * 256] = V.v[k];
@@ -574,16 +592,19 @@ __device__ __noinline__ Xy29<Q> dbl_affine29(const F29<Q> qx, const F29<Q> qy, u
   return o;
 }
 
-// The mixed-addition loop.  Bounds (values, all normalised): q.x < p, q.y < 8p; x < 10p;
-// y < 16p; zz, zzz < 2p; products < 2p.  Only two biased multiples of p (8p, 16p) are used, so
-// few constants stay live across the loop.  ZZ/ZZZ in LDS as in the 32-bit loop below.
+// The mixed-addition loop.  Bounds (values, all normalised), BLS12-381: q.x < p, q.y < 8p;
+// x < 10p; y < 16p; zz, zzz < 2p; products < 2p -- only two biased multiples of p (8p, 16p),
+// so few constants stay live across the loop.  BN254 (R29 / p ~ 169, no such headroom): q.y <
+// p, x < 5.2p, y < 3.2p, zz, zzz < 1.1p with the biases 1p..8p.  Each subtraction names its
+// bias by role (Q::ACC_*), chosen and checked per curve by tools/gen_params29.py.  ZZ/ZZZ in
+// LDS as in the 32-bit loop below.
 template <class Cv>
 KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t chunk, uint32_t cur,
                        const uint32_t* __restrict__ sorted_val, const uint32_t* __restrict__ sorted_key,
                        const uint32_t* __restrict__ pts29, uint32_t* __restrict__ acc29, uint32_t nb) {
-  using Q = Bls12_381Fp29;
+  using Q = Fp29Of<Cv>;
   using G = F29<Q>;
-  constexpr int N = Q::N;
+  constexpr int N = Q::N, W29 = kW29<Q>;
   __shared__ uint32_t s_zz[N][256], s_zzz[N][256];
   const uint32_t tx = threadIdx.x;
   const uint32_t nthreads = gridDim.x * blockDim.x;
@@ -597,9 +618,14 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
     _Pragma("unroll") for (int k = 0; k < N; ++k) a[k][tx] = v.v[k];
     asm volatile("" ::: "memory");
   };
-  // one coordinate at a time (8-B stores: a coordinate is 14 words), zz = 0 marks infinity
+  // one coordinate at a time (BLS12-381: 8-B stores, a coordinate is 14 words; BN254: 9 words,
+  // 4-B aligned), zz = 0 marks infinity
   auto put = [](uint32_t* d, const G& a) {
-    _Pragma("unroll") for (int k = 0; k < N / 2; ++k) reinterpret_cast<uint2*>(d)[k] = make_uint2(a.v[2 * k], a.v[2 * k + 1]);
+    if constexpr (N % 2 == 0) {
+      _Pragma("unroll") for (int k = 0; k < N / 2; ++k) reinterpret_cast<uint2*>(d)[k] = make_uint2(a.v[2 * k], a.v[2 * k + 1]);
+    } else {
+      _Pragma("unroll") for (int k = 0; k < N; ++k) d[k] = a.v[k];
+    }
   };
   // Where a finished bucket goes: only the chunk's first bucket can have started in an earlier
   // chunk (first piece) and only its last can continue into a later one (last piece), so both
@@ -618,16 +644,17 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
   };
   G x = G::zero(), y = G::zero();
   bool inf = true;  // running sum = O: at every bucket start, and after P + (-P)
-  // loads entry e's point (sign applied: -y as 8p - y)
+  // loads entry e's point (sign applied: -y as ACC_NEG - y; BLS12-381 8p - y)
+  constexpr int NQ = (2 * N + 3) / 4;  // 16-B loads of x, y (BN254: 18 words of a 20-word read)
   auto load_q = [&](uint32_t v, G& qx, G& qy) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(pts29 + (size_t)(v >> 1) * (sizeof(Affine<Cv>) / 4));
-    uint32_t w[2 * N];
-    _Pragma("unroll") for (int k = 0; k < N / 2; ++k) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(pts29 + (size_t)sv_point(v) * (sizeof(Affine<Cv>) / 4));
+    uint32_t w[4 * NQ];
+    _Pragma("unroll") for (int k = 0; k < NQ; ++k) {
       const uint4 q = s4[k];
       w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w;
     }
     _Pragma("unroll") for (int k = 0; k < N; ++k) { qx.v[k] = w[k]; qy.v[k] = w[N + k]; }
-    if (v & 1) qy = sub29(G::zero(), qy, Q::B8);
+    if (v & 1) qy = sub29(G::zero(), qy, Q::ACC_NEG);
   };
   // The rare doubling (running sum == incoming point) leaves the hot loop: a call or the
   // doubling's temporaries inside it would raise the loop's register peak (a call there cost
@@ -635,6 +662,7 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
   uint32_t e = start;
   for (;;) {
     bool dbl = false;
+#ifdef KZ_ACC_KEYSTREAM  // A/B reference: keys and values streamed per entry
     // entry e + 1's key and value are loaded one iteration ahead: the loop's memory chain is
     // then the point gather alone instead of key -> value -> point
     uint32_t key_n = e < end ? sorted_key[e] : 0u, val_n = e < end ? sorted_val[e] : 0u;
@@ -649,6 +677,22 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
         inf = true;
         cur = key;
       }
+#else
+    // The values stream 4 at a time (one 16-B load per 4 entries, issued an iteration ahead of
+    // their use; chunks start 16-B aligned, acc_chunk_len): each lane walks its own run, so a
+    // per-entry 4-B load re-fetched the run's sector from beyond L2 for most entries.  A bucket
+    // change is the SV_FIRST bit of the value; the key is read only then (a flush).
+    uint4 vq = *reinterpret_cast<const uint4*>(sorted_val + (e & ~3u));  // may read 3 past total: padded
+    for (; e < end; ++e) {
+      const uint32_t j = e & 3u;  // wave-uniform (every lane's chunk starts at a multiple of 4)
+      const uint32_t v = j == 0 ? vq.x : j == 1 ? vq.y : j == 2 ? vq.z : vq.w;
+      if (j == 3) vq = *reinterpret_cast<const uint4*>(sorted_val + e + 1);
+      if ((v & SV_FIRST) && e != start) {
+        flush(x, y, cur, inf, false);
+        inf = true;
+        cur = sorted_key[e];
+      }
+#endif
       G qx, qy;
       load_q(v, qx, qy);
       if (inf) {
@@ -661,8 +705,8 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
       }
       const G U2 = mul29(qx, ld(s_zz));
       const G S2 = mul29(qy, ld(s_zzz));
-      const G P = sub29(U2, x, Q::B16);  // < 18p
-      const G R = sub29(S2, y, Q::B16);  // < 18p
+      const G P = sub29(U2, x, Q::ACC_P);  // BLS12-381 < 18p
+      const G R = sub29(S2, y, Q::ACC_R);  // BLS12-381 < 18p
       if (is_zero29_mf(P)) {
         if (is_zero29_mf(R)) {
           dbl = true;
@@ -676,8 +720,8 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
       st(s_zz, mul29(ld(s_zz), PP));
       st(s_zzz, mul29(ld(s_zzz), PPP));
       const G Q2 = mul29(x, PP);
-      const G X3 = sub29(sqr29(R), add3_29(PPP, Q2, Q2), Q::B8);  // < 10p
-      y = mul2_29(R, sub29(Q2, X3, Q::B16), y, sub29(G::zero(), PPP, Q::B8));  // R (Q - X3) - Y1 PPP
+      const G X3 = sub29(sqr29(R), add3_29(PPP, Q2, Q2), Q::ACC_X3);  // BLS12-381 < 10p
+      y = mul2_29(R, sub29(Q2, X3, Q::ACC_QX), y, sub29(G::zero(), PPP, Q::ACC_PPP));  // R (Q - X3) - Y1 PPP
       x = X3;
     }
     if (!dbl) break;
@@ -726,7 +770,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
   if constexpr (kAcc29<Cv>) {
     acc_loop29<Cv>(start, end, total, chunk, cur, sorted_val, sorted_key,
                    reinterpret_cast<const uint32_t*>(pts), acc29, nb);
-  } else {  // BN254: 32-bit limbs (8 x 32 bits; radix 2^29 would need 9 limbs)
+  } else {  // A/B reference (KZ_NO_ACC29*): 32-bit limbs
   // ZZ and ZZZ of the running bucket sum live in LDS (word-major per thread: conflict-free
   // 32-bit accesses), X and Y in registers.  ZZ/ZZZ are read only at the start (U2, S2) and the
   // end (ZZ3, ZZZ3) of an addition, so taking them out of the register file keeps the loop
@@ -760,7 +804,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
       cur = key;
     }
     uint32_t v = sorted_val[e];
-    Affine<Cv> q = load_affine(pts, v >> 1);
+    Affine<Cv> q = load_affine(pts, sv_point(v));
     q.y = fp_select((v & 1) != 0, fp_rsub_mod(q.y), q.y);  // -y as p - y (see below)
     if (inf) {
       x = q.x;
@@ -829,7 +873,7 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
   uint32_t c1 = (o + cnt[key] - 1) / len;
   if constexpr (kAcc29<Cv>) {
     const size_t nthreads = (size_t)gridDim.x * blockDim.x;
-    using Q = Bls12_381Fp29;
+    using Q = Fp29Of<Cv>;
     X29<Q> acc = load_x29<Q>(acc29, nb + nthreads + c0);
     for (uint32_t cc = c; cc <= c1; ++cc) acc = x29_add<Cv, Q>(acc, load_x29<Q>(acc29, nb + cc));
     store_x29<Q>(acc29, key, acc);
@@ -857,7 +901,7 @@ __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t g = t >> 1, h = t & 1;
   if constexpr (kAcc29<Cv>) {  // BLS12-381: radix 2^29 on the records; R, U written as records
-    using Q = Bls12_381Fp29;
+    using Q = Fp29Of<Cv>;
     const X29<Q> O{F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), true};
     X29<Q> run = O, acc = O;
     if (g < nseg) {
@@ -926,8 +970,8 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
   static_assert(NSEG == 2048 && RB_PARTS == 15, "bit decomposition assumes 2^11 segments per set");
   const uint32_t set = blockIdx.x / RB_PARTS, j = blockIdx.x % RB_PARTS;
   if constexpr (kAcc29<Cv>) {  // BLS12-381: radix 2^29 on the R/U records, inline additions
-    using Q = Bls12_381Fp29;
-    constexpr int N = Q::N;
+    using Q = Fp29Of<Cv>;
+    constexpr int N = Q::N, W29 = kW29<Q>;
     __shared__ uint32_t lds29[W29 + 1][128];
     const uint32_t t = threadIdx.x;
     const uint32_t* R29 = reinterpret_cast<const uint32_t*>(R) + (size_t)set * NSEG * W29;
@@ -985,8 +1029,8 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
   // segment sum g: 32-bit XYZZ, or (BLS12-381) a radix-29 record converted as it is read
   auto seg = [&](bool r, uint32_t g) {
     if constexpr (kAcc29<Cv>) {
-      using Q = Bls12_381Fp29;
-      return x29_to32<Cv, Q>(load_x29<Q>(reinterpret_cast<const uint32_t*>(r ? R : U) + (size_t)set * NSEG * W29, g));
+      using Q = Fp29Of<Cv>;
+      return x29_to32<Cv, Q>(load_x29<Q>(reinterpret_cast<const uint32_t*>(r ? R : U) + (size_t)set * NSEG * kW29<Q>, g));
     } else {
       return load_xyzz(&(r ? Rs : Us)[g]);
     }
