@@ -10,14 +10,14 @@
 
 namespace kzgmi {
 
-// In HBM, affine points sit at a 128-B stride on both curves: each bucket-accumulation gather
-// touches exactly one 128-B line (BLS12-381's 96 B at a 96-B stride touched 1.5 on average:
-// L2-miss traffic of k_accumulate measured 211 B per window term,
-// profiles/r01/rocprof_single/pmc_accumulate_single.json), and the slot holds the point in the
-// accumulation's radix-2^29 form in place (x, y as 2 x 14 limbs = 112 B on BLS12-381, 2 x 9
-// limbs = 72 B on BN254; k_pts_to29 / k_convert_points<To29>).
+// In HBM, affine points sit at a power-of-two stride (BLS12-381: 96 -> 128 B, BN254 64 B as
+// is) so that each bucket-accumulation gather touches exactly one 128-B line (BLS12-381's 96 B
+// at a 96-B stride touched 1.5 on average: L2-miss traffic of k_accumulate measured 211 B per
+// window term, profiles/r01/rocprof_single/pmc_accumulate_single.json).  The slot also holds the
+// point in the accumulation's radix-2^29 form in place (msm.hpp store_pt29: 112 B of limbs on
+// BLS12-381, 64 B packed on BN254).
 template <class Cv>
-constexpr int kAffineAlign = 128;
+constexpr int kAffineAlign = 2 * Cv::FpP::N * 4 == 96 ? 128 : 2 * Cv::FpP::N * 4;
 
 template <class Cv>
 struct alignas(kAffineAlign<Cv>) Affine {

@@ -92,15 +92,7 @@ __global__ void __launch_bounds__(256) k_convert_points(const uint8_t* __restric
       }
       if (is_inf) x29 = y29 = F29<Q>::zero();
     }
-    constexpr int NQ = (2 * Q::N + 3) / 4;  // 16-B stores (BN254: 18 words, zero-padded to 20)
-    uint32_t w29[4 * NQ];
-#pragma unroll
-    for (int k = 0; k < Q::N; ++k) { w29[k] = x29.v[k]; w29[Q::N + k] = y29.v[k]; }
-#pragma unroll
-    for (int k = 2 * Q::N; k < 4 * NQ; ++k) w29[k] = 0;
-    uint4* d = reinterpret_cast<uint4*>(pts + i);
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) d[k] = make_uint4(w29[4 * k], w29[4 * k + 1], w29[4 * k + 2], w29[4 * k + 3]);
+    store_pt29<Cv>(pts + i, x29, y29);
   } else {
     Affine<Cv> a;
     if (is_inf) {

@@ -427,22 +427,68 @@ constexpr bool kAcc29 = true;
 template <class Q>
 constexpr int kW29 = 4 * Q::N;
 
+// A point slot in the accumulation's format.  Limbs (BLS12-381): x, y as 2 x 14 radix-29 limbs,
+// 112 B of the 128-B slot -- packing would save no 64-B sector.  Packed (BN254): x R29 and y R29
+// (both < 1.01 p < 2^254) as 2 x 8 little-endian 32-bit words, the 64-B slot of the 32-bit form:
+// one 64-B sector per gather instead of the two that 9 + 9 limbs (72 B) span, unpacked into limbs
+// with ~2 VALU per limb (limbs29); the BN254 accumulation was bound by that gather traffic.
+template <class Cv>
+constexpr bool kPackPts = sizeof(Affine<Cv>) < 2 * Fp29Of<Cv>::N * 4;
+
+template <class Cv>
+KZ_DEV void store_pt29(Affine<Cv>* slot, const F29<Fp29Of<Cv>>& x, const F29<Fp29Of<Cv>>& y) {
+  using Q = Fp29Of<Cv>;
+  uint4* d = reinterpret_cast<uint4*>(slot);
+  if constexpr (kPackPts<Cv>) {
+    constexpr int NW = Cv::FpP::N;
+    uint32_t w[2 * NW];
+    words32<Q>(x, *reinterpret_cast<uint32_t(*)[NW]>(w));
+    words32<Q>(y, *reinterpret_cast<uint32_t(*)[NW]>(w + NW));
+#pragma unroll
+    for (int k = 0; k < NW / 2; ++k) d[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+  } else {
+    static_assert(Q::N % 2 == 0, "limb slots are stored as 16-B vectors");
+    uint32_t w[2 * Q::N];
+#pragma unroll
+    for (int k = 0; k < Q::N; ++k) { w[k] = x.v[k]; w[Q::N + k] = y.v[k]; }
+#pragma unroll
+    for (int k = 0; k < Q::N / 2; ++k) d[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+  }
+}
+template <class Cv>
+KZ_DEV void load_pt29(const Affine<Cv>* slot, F29<Fp29Of<Cv>>& x, F29<Fp29Of<Cv>>& y) {
+  using Q = Fp29Of<Cv>;
+  const uint4* s4 = reinterpret_cast<const uint4*>(slot);
+  if constexpr (kPackPts<Cv>) {
+    constexpr int NW = Cv::FpP::N;
+    uint32_t wx[NW], wy[NW];
+#pragma unroll
+    for (int k = 0; k < NW / 4; ++k) {
+      const uint4 a = s4[k], b = s4[NW / 4 + k];
+      wx[4 * k] = a.x; wx[4 * k + 1] = a.y; wx[4 * k + 2] = a.z; wx[4 * k + 3] = a.w;
+      wy[4 * k] = b.x; wy[4 * k + 1] = b.y; wy[4 * k + 2] = b.z; wy[4 * k + 3] = b.w;
+    }
+    x = limbs29<Q>(wx);
+    y = limbs29<Q>(wy);
+  } else {
+    uint32_t w[2 * Q::N];
+#pragma unroll
+    for (int k = 0; k < Q::N / 2; ++k) {
+      const uint4 q = s4[k];
+      w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w;
+    }
+#pragma unroll
+    for (int k = 0; k < Q::N; ++k) { x.v[k] = w[k]; y.v[k] = w[Q::N + k]; }
+  }
+}
+
 template <class Cv>
 __global__ void __launch_bounds__(256) k_pts_to29(Affine<Cv>* __restrict__ pts, uint32_t n) {
   using Q = Fp29Of<Cv>;
-  constexpr int NQ = (2 * Q::N + 3) / 4;  // 16-B stores of x, y (BN254: 18 words, zero-padded to 20)
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const Affine<Cv> a = pts[i];
-  const F29<Q> x = fp_to29<Q>(a.x), y = fp_to29<Q>(a.y);
-  uint32_t w[4 * NQ];
-#pragma unroll
-  for (int k = 0; k < Q::N; ++k) { w[k] = x.v[k]; w[Q::N + k] = y.v[k]; }
-#pragma unroll
-  for (int k = 2 * Q::N; k < 4 * NQ; ++k) w[k] = 0;
-  uint4* d = reinterpret_cast<uint4*>(pts + i);
-#pragma unroll
-  for (int k = 0; k < NQ; ++k) d[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+  store_pt29<Cv>(pts + i, fp_to29<Q>(a.x), fp_to29<Q>(a.y));
 }
 
 // ------------------------------------------------------------------------------ radix-29 XYZZ
@@ -645,15 +691,8 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
   G x = G::zero(), y = G::zero();
   bool inf = true;  // running sum = O: at every bucket start, and after P + (-P)
   // loads entry e's point (sign applied: -y as ACC_NEG - y; BLS12-381 8p - y)
-  constexpr int NQ = (2 * N + 3) / 4;  // 16-B loads of x, y (BN254: 18 words of a 20-word read)
   auto load_q = [&](uint32_t v, G& qx, G& qy) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(pts29 + (size_t)sv_point(v) * (sizeof(Affine<Cv>) / 4));
-    uint32_t w[4 * NQ];
-    _Pragma("unroll") for (int k = 0; k < NQ; ++k) {
-      const uint4 q = s4[k];
-      w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w;
-    }
-    _Pragma("unroll") for (int k = 0; k < N; ++k) { qx.v[k] = w[k]; qy.v[k] = w[N + k]; }
+    load_pt29<Cv>(reinterpret_cast<const Affine<Cv>*>(pts29) + sv_point(v), qx, qy);
     if (v & 1) qy = sub29(G::zero(), qy, Q::ACC_NEG);
   };
   // The rare doubling (running sum == incoming point) leaves the hot loop: a call or the
