@@ -374,7 +374,9 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   Affine<Cv>* pts = s.pts.template as<Affine<Cv>>();
   uint8_t* inf = s.inf.template as<uint8_t>();
   // points that only feed the radix-29 accumulation are converted straight into its format
-  const bool pts29 = kAcc29<Cv> && !glv && !(flags & (KZGMI_FLAG_COMPRESSED | KZGMI_FLAG_SUBGROUP_CHECK));
+  // (with GLV their images too: k_endo_points29); decompression and the subgroup check work in
+  // the 32-bit form, converted afterwards by run_msm_core's k_pts_to29
+  const bool pts29 = kAcc29<Cv> && !(flags & (KZGMI_FLAG_COMPRESSED | KZGMI_FLAG_SUBGROUP_CHECK));
   const uint32_t nn = (uint32_t)n;
   uint32_t* gs = s.glv_s.template as<uint32_t>();
   uint32_t* gt = s.glv_t.template as<uint32_t>();
@@ -395,7 +397,7 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
     // the SRS's [1]_1 as the last term of MSM#1: -t [1]_1
     HIPCHK(hipMemcpyAsync(pts + 2 * n, pts29 ? srs->g1_29() : srs->g1.p, sizeof(Affine<Cv>), hipMemcpyDeviceToDevice, st));
     HIPCHK(hipMemcpyAsync(inf + 2 * n, srs->g1.template as<uint8_t>() + sizeof(Affine<Cv>), 1, hipMemcpyDeviceToDevice, st));
-    if (glv) L::endo_points(st, pts, inf, (uint32_t)PH, pts + PH, inf + PH);
+    if (glv) L::endo_points(st, pts, inf, (uint32_t)PH, pts + PH, inf + PH, pts29);
     mark(c, s, PH_CONVERT + 1);
     if (flags & KZGMI_FLAG_FIAT_SHAMIR) {  // r from the transcript of this (whole) batch
       const uint32_t* digests = nullptr;
@@ -444,7 +446,7 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
     tl.total = 0;
     for (uint32_t j = 0; j < k; ++j) tl.total += tl.c[j].count;
     const MsmWindows mw{2, {0, 8}, {8, 8}};
-    CHK(run_msm_core<Cv>(c, s, tl, 16, (size_t)(powers ? 48 : 32) * n + 16, mw, nullptr, nullptr, false, dry));
+    CHK(run_msm_core<Cv>(c, s, tl, 16, (size_t)(powers ? 48 : 32) * n + 16, mw, nullptr, nullptr, pts29, dry));
   } else if (!powers) {  // 127-bit r_i: MSM#0 in 8 windows (sets 0..7), MSM#1 in 16 (sets 8..23)
     tl.c[0] = {nn, 0, 4, 8, 0, 4, s.scal_r.template as<uint32_t>()};          // MSM#0: r_i pi_i
     tl.c[1] = {nn, nn, 4, 8, 8, 4, s.scal_r.template as<uint32_t>()};         // MSM#1: r_i C_i
@@ -851,9 +853,9 @@ int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t
   uint32_t* err = s.flags.template as<uint32_t>() + 1;
   Affine<Cv>* pts = s.pts.template as<Affine<Cv>>();
   uint8_t* inf = s.inf.template as<uint8_t>();
-  const bool pts29 = kAcc29<Cv> && !glv;
+  const bool pts29 = kAcc29<Cv>;
   Launch<Cv>::convert_points(st, (const uint8_t*)dpts, (uint32_t)n, pts, inf, err, pts29);
-  if (glv) Launch<Cv>::endo_points(st, pts, inf, (uint32_t)n, pts + n, inf + n);
+  if (glv) Launch<Cv>::endo_points(st, pts, inf, (uint32_t)n, pts + n, inf + n, pts29);
   mark(c, s, PH_CONVERT + 1);
   uint32_t* sc = s.scal_s.template as<uint32_t>();
   Launch<Cv>::convert_scalars(st, (const uint8_t*)dsc, (uint32_t)n, sc, err);
@@ -868,7 +870,7 @@ int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t
     tl.nclass = 2;
     tl.total = 2 * nn;
     const MsmWindows mw{1, {0, 0}, {8, 0}};
-    CHK(run_msm_core<Cv>(c, s, tl, 8, (size_t)16 * n + 16, mw));
+    CHK(run_msm_core<Cv>(c, s, tl, 8, (size_t)16 * n + 16, mw, nullptr, nullptr, pts29));
   } else {
     tl.c[0] = {nn, 0, 8, 16, 0, 8, sc};
     tl.nclass = 1;

@@ -39,7 +39,9 @@ struct Launch {
   static void convert_scalars(hipStream_t st, const uint8_t* bytes, uint32_t n, uint32_t* out, uint32_t* err);
   // GLV (glv.hpp): n scalars of 8 words, `stride` words apart -> half scalars h0, h1 (4 words each)
   static void glv_split(hipStream_t st, const uint32_t* scal, uint32_t stride, uint32_t n, uint32_t* h0, uint32_t* h1);
-  static void endo_points(hipStream_t st, const AF* src, const uint8_t* src_inf, uint32_t n, AF* dst, uint8_t* dst_inf);
+  // in29: src is in the accumulation's radix-29 format (and dst is written in it)
+  static void endo_points(hipStream_t st, const AF* src, const uint8_t* src_inf, uint32_t n, AF* dst, uint8_t* dst_inf,
+                          bool in29 = false);
   static void convert_g2(hipStream_t st, const uint8_t* bytes, uint32_t n, G2Aff<Cv>* out, uint8_t* inf,
                          uint32_t* err);
   static void scalar_prep(hipStream_t st, const Seed& seed, const uint32_t* seed_dev, uint64_t index_offset,

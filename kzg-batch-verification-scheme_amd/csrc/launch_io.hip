@@ -47,8 +47,15 @@ void Launch<Cv>::glv_split(hipStream_t st, const uint32_t* scal, uint32_t stride
 }
 template <class Cv>
 void Launch<Cv>::endo_points(hipStream_t st, const AF* src, const uint8_t* src_inf, uint32_t n, AF* dst,
-                             uint8_t* dst_inf) {
-  if (n) k_endo_points<Cv><<<grid_for(n, 256), 256, 0, st>>>(src, src_inf, n, dst, dst_inf);
+                             uint8_t* dst_inf, bool in29) {
+  if (!n) return;
+  if constexpr (kAcc29<Cv>) {
+    if (in29) {
+      k_endo_points29<Cv><<<grid_for(n, 256), 256, 0, st>>>(src, src_inf, n, dst, dst_inf);
+      return;
+    }
+  }
+  k_endo_points<Cv><<<grid_for(n, 256), 256, 0, st>>>(src, src_inf, n, dst, dst_inf);
 }
 template <class Cv>
 void Launch<Cv>::convert_g2(hipStream_t st, const uint8_t* bytes, uint32_t n, G2Aff<Cv>* out, uint8_t* inf,
@@ -144,7 +151,7 @@ template void Launch<C_>::scalar_prep_pow(hipStream_t, const void*, uint64_t, co
                                           uint32_t*, uint32_t*, void*, uint32_t*, uint32_t*);
 template void Launch<C_>::encode_points(hipStream_t, const Xyzz<C_>*, uint32_t, uint8_t*);
 template void Launch<C_>::glv_split(hipStream_t, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t*);
-template void Launch<C_>::endo_points(hipStream_t, const Affine<C_>*, const uint8_t*, uint32_t, Affine<C_>*, uint8_t*);
+template void Launch<C_>::endo_points(hipStream_t, const Affine<C_>*, const uint8_t*, uint32_t, Affine<C_>*, uint8_t*, bool);
 template void Launch<C_>::sum_partials(hipStream_t, const Xyzz<C_>*, uint32_t, uint32_t, uint32_t, Xyzz<C_>*);
 
 }  // namespace kzgmi

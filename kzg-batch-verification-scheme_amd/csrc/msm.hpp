@@ -482,6 +482,21 @@ KZ_DEV void load_pt29(const Affine<Cv>* slot, F29<Fp29Of<Cv>>& x, F29<Fp29Of<Cv>
   }
 }
 
+// dst[i] = phi(src[i]) = (beta x, y) on points already in the accumulation's format (GLV on
+// points converted straight into it: no 32-bit pass and no k_pts_to29 over 2 x (2n + 1) points)
+template <class Cv>
+__global__ void __launch_bounds__(256) k_endo_points29(const Affine<Cv>* __restrict__ src,
+                                                       const uint8_t* __restrict__ src_inf, uint32_t n,
+                                                       Affine<Cv>* __restrict__ dst, uint8_t* __restrict__ dst_inf) {
+  using Q = Fp29Of<Cv>;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  F29<Q> x, y;
+  load_pt29<Cv>(src + i, x, y);  // < (p / R29 + 1) p; beta R29 likewise: the product stays below it
+  store_pt29<Cv>(dst + i, mul29(x, fp_to29<Q>(Fp<typename Cv::FpP>::from_const(Cv::K::GLV_BETA_M))), y);
+  dst_inf[i] = src_inf[i];
+}
+
 template <class Cv>
 __global__ void __launch_bounds__(256) k_pts_to29(Affine<Cv>* __restrict__ pts, uint32_t n) {
   using Q = Fp29Of<Cv>;
