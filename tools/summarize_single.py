@@ -75,9 +75,9 @@ if fetch and write:
                       "profiles/r02/pmc_sq_accumulate.json).  Infinity-Cache hits are counted, so this is "
                       "L2-miss traffic, an upper bound on HBM bytes",
         "algorithmic_bytes_per_launch": 256 * n,
-        "gather_model_bytes_per_launch": entries * (112 + 8),
+        "gather_model_bytes_per_launch": entries * (112 + 4),
         "gather_model": "every window term gathers its 112-B radix-2^29 affine point (x, y: 2 x 14 words "
-                        "of a 128-B slot) and reads its 8-B sorted entry (32 terms per tuple): the traffic "
+                        "of a 128-B slot) and streams its 4-B sorted value (32 terms per tuple): the traffic "
                         "Pippenger accumulation touches by construction",
         "tcc_hit_rate": (sum(hit) / (sum(hit) + sum(miss))) if hit and miss else None,
         "k_accumulate_avg_ms": acc / 1e6,
