@@ -47,9 +47,10 @@ extern "C" {
 typedef enum { KZGMI_BLS12_381 = 0, KZGMI_BN254 = 1 } kzgmi_curve;
 
 /* ABI revision of this header.  2: kzgmi_srs_load gained the g1 argument (3rd position),
- * kzgmi_ctx_reserve / kzgmi_alloc_count / kzgmi_abi_version were added.  A caller built
+ * kzgmi_ctx_reserve / kzgmi_alloc_count / kzgmi_abi_version were added.  3: kzgmi_pairing
+ * returns the standard e(P, Q) on BLS12-381 (was its cube).  A caller built
  * against another revision must not bind the library: compare with kzgmi_abi_version(). */
-#define KZGMI_ABI_VERSION 2
+#define KZGMI_ABI_VERSION 3
 
 #define KZGMI_OK 0
 #define KZGMI_ERR_ARG (-1)
@@ -267,8 +268,10 @@ int kzgmi_commit_device(kzgmi_ctx* ctx, const kzgmi_ck* ck, const void* d_coeffs
  * commitment (G1 encoding). */
 int kzgmi_commit_device_async(kzgmi_ctx* ctx, const kzgmi_ck* ck, int slot, const void* d_coeffs, size_t m);
 
-/* Optimal-ate pairing e(P, Q) (cubed for BLS12-381, as in the oracle), 12 Fp values in
- * tower order, big-endian: 576 B (BLS12-381) / 384 B (BN254).  Test/diagnostic utility. */
+/* Optimal-ate pairing e(P, Q) for P in G1, Q in G2: 12 Fp values in tower order, big-endian:
+ * 576 B (BLS12-381) / 384 B (BN254).  Test/diagnostic utility.  (ABI 2 returned e(P, Q)^3 on
+ * BLS12-381, the value the batch check's final exponentiation computes; ABI 3 scales P by
+ * 3^-1 mod r first, so the result is the standard e(P, Q) -- for P outside G1 it is not.) */
 int kzgmi_pairing(kzgmi_ctx* ctx, kzgmi_curve curve, const uint8_t* g1, const uint8_t* g2,
                   uint8_t* out);
 

@@ -542,7 +542,7 @@ int ensure_table(kzgmi_ctx* c, hipStream_t st) {
 // ================================================================================ C ABI
 extern "C" {
 
-const char* kzgmi_version(void) { return "kzgmi 0.3 (abi 2, gfx950, HIP)"; }
+const char* kzgmi_version(void) { return "kzgmi 0.4 (abi 3, gfx950, HIP)"; }
 int kzgmi_abi_version(void) { return KZGMI_ABI_VERSION; }
 uint64_t kzgmi_alloc_count(void) { return g_allocs.load(std::memory_order_relaxed); }
 const char* kzgmi_last_error(void) { return g_err.c_str(); }
@@ -1395,6 +1395,17 @@ int kzgmi_pairing(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uint
   CHK(check_ctx(c));
   if (!g1 || !g2 || !out) return fail(KZGMI_ERR_ARG, "null argument");
   CHK(slot0_idle(c));
+  // BLS12-381: the pairing program's hard part is the x-chain of 3 (p^4 - p^2 + 1) / r, so it
+  // yields e(P, Q)^3 (as the oracle and pyspec do); e(P, Q) = e([3^-1 mod r] P, Q)^3 for P in G1,
+  // so P is first scaled by 3^-1 mod r with the library's own (exact, non-GLV) MSM
+  uint8_t g1s[96];
+  if (curve == KZGMI_BLS12_381) {
+    static const uint8_t kInv3[32] = {0x4d, 0x49, 0x1a, 0x37, 0x71, 0x13, 0xa8, 0xda, 0xcc, 0xd1, 0x3a,
+                                      0xb0, 0x06, 0x6b, 0xe5, 0x58, 0xe2, 0x7e, 0x6d, 0x57, 0x55, 0x54,
+                                      0x3d, 0x54, 0xaa, 0xaa, 0xaa, 0xaa, 0x00, 0x00, 0x00, 0x01};
+    CHK(kzgmi_msm_g1(c, curve, g1, kInv3, 1, g1s));
+    g1 = g1s;
+  }
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     Slot& s = c->slots[0];

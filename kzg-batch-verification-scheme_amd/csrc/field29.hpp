@@ -232,6 +232,35 @@ KZ_DEV F29<Q> sub29(const F29<Q>& a, const F29<Q>& b, const uint32_t (&B)[Q::N])
   return r;
 }
 
+// a + C - s - 2t in one carry pass (C: a multiple of p with limbs in [3 (2^29 - 1), 2^31),
+// params29_gen.hpp C4/C8; s, t normalised, so no limb goes negative): the accumulation's
+// X3 = R^2 - (PPP + 2 Q2), which took an add3_29 pass and a sub29 pass (5 VALU per limb instead of 8)
+template <class Q>
+KZ_DEV F29<Q> sub3_29(const F29<Q>& a, const F29<Q>& s, const F29<Q>& t, const uint32_t (&C)[Q::N]) {
+  F29<Q> r;
+  uint32_t c = 0;
+  _Pragma("unroll") for (int i = 0; i < Q::N; ++i) {
+    const uint32_t x = (a.v[i] + C[i] + c) - (s.v[i] + t.v[i] + t.v[i]);
+    if (i < Q::N - 1) {
+      r.v[i] = x & M29;
+      c = x >> 29;
+    } else {
+      r.v[i] = x;
+    }
+  }
+  return r;
+}
+
+// B - b limb by limb, no carry pass (B biased, b normalised): limbs in (0, 2^30), NOT normalised.
+// Only as one operand of a product whose column sums keep their headroom -- in the accumulation,
+// the y PPP pair of mul2_29: 14 x 2^59 + (14 + 14) x 2^58 < 2^64 (BLS12-381; BN254 9 limbs)
+template <class Q>
+KZ_DEV F29<Q> neg_lazy29(const F29<Q>& b, const uint32_t (&B)[Q::N]) {
+  F29<Q> r;
+  _Pragma("unroll") for (int i = 0; i < Q::N; ++i) r.v[i] = B[i] - b.v[i];
+  return r;
+}
+
 // a + b + e, normalised
 template <class Q>
 KZ_DEV F29<Q> add3_29(const F29<Q>& a, const F29<Q>& b, const F29<Q>& e) {

@@ -774,8 +774,14 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
       st(s_zz, mul29(ld(s_zz), PP));
       st(s_zzz, mul29(ld(s_zzz), PPP));
       const G Q2 = mul29(x, PP);
-      const G X3 = sub29(sqr29(R), add3_29(PPP, Q2, Q2), Q::ACC_X3);  // BLS12-381 < 10p
+#ifdef KZ_ACC_CARRY_PASSES  // A/B reference: X3 in two carry passes, -PPP normalised
+      const G X3 = sub29(sqr29(R), add3_29(PPP, Q2, Q2), Q::ACC_X3_B);  // BLS12-381 < 10p
       y = mul2_29(R, sub29(Q2, X3, Q::ACC_QX), y, sub29(G::zero(), PPP, Q::ACC_PPP));  // R (Q - X3) - Y1 PPP
+#else
+      const G X3 = sub3_29(sqr29(R), PPP, Q2, Q::ACC_X3);  // one carry pass; BLS12-381 < 10p
+      // R (Q - X3) - Y1 PPP, with -PPP as ACC_PPP - PPP limb by limb (no carry pass; neg_lazy29)
+      y = mul2_29(R, sub29(Q2, X3, Q::ACC_QX), y, neg_lazy29(PPP, Q::ACC_PPP));
+#endif
       x = X3;
     }
     if (!dbl) break;

@@ -22,7 +22,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # KZGMI_LIB selects an alternative build (timing experiments); default: the in-tree library
 LIB_PATH = os.environ.get("KZGMI_LIB") or os.path.join(_HERE, "libkzgmi.so")
 
-ABI_VERSION = 2  # include/kzgmi.h KZGMI_ABI_VERSION
+ABI_VERSION = 3  # include/kzgmi.h KZGMI_ABI_VERSION
 CURVES = {"bls12_381": 0, "bn254": 1}
 FP_BYTES = {"bls12_381": 48, "bn254": 32}
 PHASES = ["convert", "scalars", "sort", "accumulate", "reduce", "combine", "pairing"]

@@ -55,6 +55,19 @@ def biased(k, p, n):
     return b
 
 
+def biased3(k, p, n):
+    """k p with limbs 0..n-2 in [3 (2^29 - 1), 2^31): the bias of sub3_29 (a + B - s - 2t in one
+    carry pass, s and t normalised, so every limb's s + 2t <= 3 (2^29 - 1) <= B_i)."""
+    b = limbs(k * p, n)
+    b[0] += 3 << W
+    for i in range(1, n - 1):
+        b[i] += (3 << W) - 3
+    b[n - 1] -= 3
+    assert sum(v << (W * i) for i, v in enumerate(b)) == k * p
+    assert all(3 * ((1 << W) - 1) <= v < (1 << 31) for v in b[:n - 1]) and b[n - 1] >= 0
+    return b
+
+
 def check_bounds(p, n, nkp, roles):
     """Value bounds (units of p) of the accumulation loop (msm.hpp acc_loop29), its doubling
     (dbl_affine29), the record addition/doubling (x29_add, x29_dbl) and the on-curve test."""
@@ -93,6 +106,8 @@ def check_bounds(p, n, nkp, roles):
         assert ro["ACC_X3"] >= PPP + 2 * Q2
         X3 = mont(Rr, Rr) + ro["ACC_X3"]
         assert ro["ACC_QX"] >= X3 and ro["ACC_PPP"] >= PPP
+        # neg_lazy29 (ACC_PPP - PPP limb by limb, no carries): the top limb must not go negative
+        assert limbs(roles["ACC_PPP"] * p, n)[n - 1] - 1 >= (int(PPP * p) >> (W * (n - 1))) + 1
         Y3 = mont2(Rr, Q2 + ro["ACC_QX"], Y, ro["ACC_PPP"])
         Zn = max(Z, mont(Z, PP), mont(Z, PPP))
         Xn, Yn = max(X, X3), max(Y, Y3)
@@ -153,9 +168,15 @@ def emit(name, p, n, r32, b, nkp, roles):
     print("  static constexpr uint32_t BCURVE[N] = %s;  // %d R29 mod p (y^2 = x^3 + %d)" % (arr(limbs(b * R29 % p, n)), b, b))
     for k in (1, 2, 4, 8, 16, 32, 64):
         print("  static constexpr uint32_t B%d[N] = %s;  // %d p, biased limbs" % (k, arr(biased(k, p, n)), k))
+    for k in (4, 8):
+        print("  static constexpr uint32_t C%d[N] = %s;  // %d p, limbs in [3 (2^29 - 1), 2^31) (sub3_29)"
+              % (k, arr(biased3(k, p, n)), k))
     print("  // roles (tools/gen_params29.py check_bounds): the bias of each subtraction in acc_loop29 / dbl_affine29")
     for role, k in roles.items():
-        print("  static constexpr const uint32_t (&%s)[N] = B%d;" % (role, k))
+        kind = "C" if role == "ACC_X3" else "B"
+        print("  static constexpr const uint32_t (&%s)[N] = %s%d;" % (role, kind, k))
+    print("  static constexpr const uint32_t (&ACC_X3_B)[N] = B%d;  // ACC_X3 for two carry passes (A/B build)"
+          % roles["ACC_X3"])
     print("  static constexpr int NKP = %d;" % nkp)
     print("  static constexpr uint32_t KP_LO[NKP] = %s;  // low limb of k p" % arr([(k * p) & MASK for k in range(nkp)]))
     print("  static constexpr uint32_t KP[NKP][N] = {%s};  // k p" % ", ".join(arr(limbs(k * p, n)) for k in range(nkp)))
