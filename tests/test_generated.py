@@ -1,0 +1,47 @@
+"""The generated constant headers are what their generators produce now.
+
+tools/gen_params29.py also runs check_bounds(): the value bounds of every step of the radix-2^29
+accumulation loop, its doubling and the record addition/doubling, per curve, with the biases the
+loop uses (msm.hpp acc_loop29) -- so this test fails if a bias role, NKP or a bias constant is
+changed without the bounds still closing.
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "kzg-batch-verification-scheme_amd")
+
+
+def _stdout(gen):
+    return subprocess.run([sys.executable, os.path.join(PKG, "tools", gen)], check=True,
+                          capture_output=True, text=True).stdout
+
+
+def test_params29_in_sync_and_bounds_close():
+    with open(os.path.join(PKG, "csrc", "params29_gen.hpp")) as f:
+        assert _stdout("gen_params29.py") == f.read()
+
+
+def test_params_lp_in_sync():
+    with open(os.path.join(PKG, "csrc", "params_lp_gen.hpp")) as f:
+        assert _stdout("gen_params_lp.py") == f.read()
+
+
+def test_bound_checker_rejects_a_short_bias():
+    """BN254 with the 1p negation bias (round 3's first attempt): the Montgomery conversion
+    leaves points below (p / R29 + 1) p = 1.006 p, so 1p - y can go negative."""
+    sys.path.insert(0, os.path.join(PKG, "tools"))
+    try:
+        import gen_params29 as g
+    finally:
+        sys.path.pop(0)
+    name, p, n, r32, b, nkp, roles = g.CURVES[1]
+    assert name == "Bn254Fp29"
+    g.check_bounds(p, n, nkp, roles)
+    bad = dict(roles, ACC_NEG=1)
+    try:
+        g.check_bounds(p, n, nkp, bad)
+    except AssertionError:
+        return
+    raise AssertionError("check_bounds accepted ACC_NEG = 1p on BN254")
