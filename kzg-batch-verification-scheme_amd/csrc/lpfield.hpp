@@ -40,8 +40,11 @@ KZ_DEV int32_t lp_bcast(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0x150 + 
 KZ_DEV int32_t lp_next(int32_t x) { return __builtin_amdgcn_update_dpp(0, x, 0x101, 0xF, 0xF, true); }  // row_shl:1: lane j <- j+1, lane 15 <- 0
 KZ_DEV int32_t lp_prev(int32_t x) { return __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true); }  // row_shr:1: lane j <- j-1, lane 0 <- 0
 
-// acc += a b, signed 32 x 32 -> 64 (one v_mad_i64_i32; hipcc lowers the C++ form to two
-// unsigned mads plus sign fix-ups).  One instruction per asm statement (see field.hpp).
+// acc += a b, signed 32 x 32 -> 64: one v_mad_i64_i32.  ROCm 7.2's hipcc selects it from the C++
+// form for gfx950 (earlier compilers lowered it to two unsigned mads plus sign fix-ups, hence the
+// inline asm of rounds 1-2, KZ_LP_ASM_MADS); the C++ form also spares the s_nop hipcc pads after
+// every VGPR-writing asm statement -- 14 per lane-parallel product (lp_mul_iter).
+#ifdef KZ_LP_ASM_MADS
 KZ_DEV void lp_mad_i64(int64_t& acc, int32_t a, int32_t b) {
   uint64_t cc;
   asm("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
@@ -51,6 +54,13 @@ KZ_DEV void lp_mad_u64(int64_t& acc, int32_t a, int32_t b) {
   uint64_t cc;
   asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
 }
+#else
+KZ_DEV void lp_mad_i64(int64_t& acc, int32_t a, int32_t b) { acc += (int64_t)a * (int64_t)b; }
+// acc += a b for 0 <= a, b < 2^31 (two's complement acc: the unsigned sum wraps correctly)
+KZ_DEV void lp_mad_u64(int64_t& acc, int32_t a, int32_t b) {
+  acc = (int64_t)((uint64_t)acc + (uint64_t)(uint32_t)a * (uint64_t)(uint32_t)b);
+}
+#endif
 
 // per-lane constants of a lane-parallel kernel (lane j = threadIdx.x % 16 of row threadIdx.x / 16 % 4)
 template <class Cv>
@@ -93,8 +103,7 @@ KZ_DEV int32_t lp_norm(const LpCtx<Cv>& c, int32_t v) {
 }
 
 template <class Cv, int I>
-KZ_DEV void lp_mul_iter(int64_t& acc, int32_t a, int32_t b, int32_t pj) {
-  const int32_t ai = lp_bcast<I>(a);
+KZ_DEV void lp_mul_iter(int64_t& acc, int32_t ai, int32_t b, int32_t pj) {  // ai: limb I of a, broadcast
   lp_mad_i64(acc, ai, b);
   const int32_t mloc = (int32_t)(((uint32_t)acc * LpQ<Cv>::INV) & (uint32_t)LP_M29);
   const int32_t m = lp_bcast<0>(mloc);
@@ -103,10 +112,13 @@ KZ_DEV void lp_mul_iter(int64_t& acc, int32_t a, int32_t b, int32_t pj) {
   const int32_t hi = (int32_t)(acc >> 29);
   acc = (int64_t)(hi + lp_next(lo));
 }
+// every limb of a broadcast up front (independent DPP moves): the scheduler can place them in the
+// systolic chain's wait states instead of an s_nop before each step's dependent DPP
 template <class Cv, int... I>
 KZ_DEV int32_t lp_mul_raw(int32_t a, int32_t b, int32_t pj, std::integer_sequence<int, I...>) {
+  const int32_t ai[] = {lp_bcast<I>(a)...};
   int64_t acc = 0;
-  (lp_mul_iter<Cv, I>(acc, a, b, pj), ...);
+  (lp_mul_iter<Cv, I>(acc, ai[I], b, pj), ...);
   return (int32_t)acc;
 }
 // a b / R (mod p), each row independently
