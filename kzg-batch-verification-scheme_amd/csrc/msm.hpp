@@ -249,10 +249,72 @@ static __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const u
 // using them (the loops are latency-bound otherwise).  Bins of up to FINE_STAGE entries are
 // sorted into an LDS staging array and then written out contiguously (coalesced stores; the
 // bucket of output slot p comes from a 7-step search of the inclusive bucket scan) instead
-// of two scattered 4-byte stores per entry; larger bins (adversarial digit distributions,
-// or 16 bucket sets at n = 2^20) store directly.
+// of two scattered 4-byte stores per entry.  Larger bins (BN254 at n = 2^22: ~32 K entries,
+// the 2^24-point MSM: ~65 K) go through the same staging array a chunk of FINE_STAGE / 2 entries
+// at a time: the chunk is counting-sorted in LDS (the histogram atomics return the ranks), and each
+// bucket's run of the chunk is written at that bucket's running cursor -- runs of ~32 entries
+// instead of one scattered 4-byte store pair per entry (KZ_FINE_UNSTAGED: the direct stores).
 constexpr int FINE_ILP = 4;
 constexpr int FINE_STAGE = 8192;
+
+// Bins above FINE_STAGE entries, a chunk at a time (k_fine_sort): cursor[b] holds bucket b's
+// next free position in the bin, bstart[b] its first (SV_FIRST goes there); `stage` is the
+// kernel's staging array.  A chunk's entries stay in registers between the ranking and the
+// staging: chunks of FINE_STAGE / 2 keep the kernel within 128 VGPRs (4 workgroups per CU for
+// the staged bins, whose LDS allows 4).
+KZ_DEV void fine_sort_chunks(uint32_t g, uint32_t start, uint32_t count, const uint64_t* __restrict__ tmp,
+                             const uint32_t* bstart, uint32_t* cursor, uint32_t* stage,
+                             uint32_t* __restrict__ sorted_val, uint32_t* __restrict__ sorted_key) {
+  constexpr uint32_t CHUNK = FINE_STAGE / 2, PER = CHUNK / 256;  // 16 per thread: 147 -> <= 128 VGPRs
+  __shared__ uint32_t ccnt[FINE];   // chunk histogram
+  __shared__ uint32_t cscan[FINE];  // chunk inclusive scan
+  const uint32_t t = threadIdx.x;
+  for (uint32_t c0 = 0; c0 < count; c0 += CHUNK) {
+    const uint32_t cn = min(CHUNK, count - c0);
+    if (t < FINE) ccnt[t] = 0;
+    __syncthreads();
+    uint64_t v[PER];
+    uint32_t rank[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t e = j * 256 + t;
+      v[j] = e < cn ? tmp[start + c0 + e] : ~0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      rank[j] = v[j] != ~0ull ? atomicAdd(&ccnt[(uint32_t)(v[j] >> 32) & (FINE - 1)], 1u) : 0u;
+    __syncthreads();
+    const uint32_t tot = t < FINE ? ccnt[t] : 0u;
+    if (t < FINE) cscan[t] = tot;
+    __syncthreads();
+    for (int d = 1; d < FINE; d <<= 1) {  // Hillis-Steele, threads 0..127
+      const uint32_t x = (t < FINE && t >= (uint32_t)d) ? cscan[t - d] : 0u;
+      __syncthreads();
+      if (t < FINE) cscan[t] += x;
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (v[j] == ~0ull) continue;
+      const uint32_t b = (uint32_t)(v[j] >> 32) & (FINE - 1);
+      const uint32_t q = cscan[b] - ccnt[b] + rank[j];
+      stage[q] = (uint32_t)v[j];
+    }
+    __syncthreads();
+    for (uint32_t q = t; q < cn; q += 256) {
+      uint32_t b = 0;  // smallest b with cscan[b] > q
+#pragma unroll
+      for (int step = FINE / 2; step >= 1; step >>= 1)
+        if (cscan[b + step - 1] <= q) b += step;
+      const uint32_t p = cursor[b] + q - (cscan[b] - ccnt[b]);  // position in the bin
+      sorted_val[start + p] = stage[q] | (p == bstart[b] ? SV_FIRST : 0u);
+      sorted_key[start + p] = g * FINE + b;
+    }
+    __syncthreads();
+    if (t < FINE) cursor[t] += ccnt[t];
+    __syncthreads();
+  }
+}
 
 static __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ coarse_off,
                                                    const uint32_t* __restrict__ coarse_cnt,
@@ -299,6 +361,14 @@ static __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __rest
     cnt[key] = tot;
   }
   __syncthreads();
+#ifndef KZ_FINE_UNSTAGED
+  if (!staged) {
+    if (t < FINE) scan[t] -= fine[t];  // bucket starts (exclusive scan); cursor[] is a copy
+    __syncthreads();
+    fine_sort_chunks(g, start, count, tmp, scan, cursor, stage, sorted_val, sorted_key);
+    return;
+  }
+#endif
   for (uint32_t e0 = t; e0 < count; e0 += 256 * FINE_ILP) {
     uint64_t v[FINE_ILP];
 #pragma unroll
