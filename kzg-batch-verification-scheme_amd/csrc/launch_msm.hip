@@ -16,8 +16,20 @@ void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const 
   if (tl.total) k_digits<<<grid_for(tl.total, 256), 256, 0, st>>>(tl, inf, digits);
   if (tiles) k_bin_count<<<tiles, 256, 0, st>>>(tl, digits, ccnt);
   k_bin_scan<<<1, 1024, 0, st>>>(ccnt, nbins, coff, ccur, total);
-  if (tiles) k_bin_scatter<<<tiles, 256, 0, st>>>(tl, digits, ccur, ent);
-  k_fine_sort<<<nbins, 256, 0, st>>>(coff, ccnt, ent, off, cnt, sval, skey);
+  // 4-byte coarse-pass entries when every sorted value (point index << 1 | sign) fits CV_BITS
+  uint64_t npts = 0;
+  for (uint32_t k = 0; k < tl.nclass; ++k)
+    if (tl.c[k].count) npts = std::max<uint64_t>(npts, (uint64_t)tl.c[k].pt_base + tl.c[k].count);
+#ifndef KZ_SORT_WIDE_ENTRIES
+  if (2 * npts < (1ull << CV_BITS)) {
+    uint32_t* e32 = reinterpret_cast<uint32_t*>(ent);
+    if (tiles) k_bin_scatter<uint32_t><<<tiles, 256, 0, st>>>(tl, digits, ccur, e32);
+    k_fine_sort<uint32_t><<<nbins, 256, 0, st>>>(coff, ccnt, e32, off, cnt, sval, skey);
+    return;
+  }
+#endif
+  if (tiles) k_bin_scatter<uint64_t><<<tiles, 256, 0, st>>>(tl, digits, ccur, ent);
+  k_fine_sort<uint64_t><<<nbins, 256, 0, st>>>(coff, ccnt, ent, off, cnt, sval, skey);
 }
 
 template <class Cv>

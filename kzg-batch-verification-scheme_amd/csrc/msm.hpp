@@ -55,7 +55,7 @@ struct TermList {
 //                 coarse bins (key >> 7), then one global atomic per non-empty bin
 //   k_bin_scan    exclusive scan of the nsets*256 coarse counts (+ total entries)
 //   k_bin_scatter same digits; LDS ranks, one global atomic per bin reserves the tile's run,
-//                 entries written as (key << 32 | value) into their coarse bin
+//                 entries (key, value: make_ent) written into their coarse bin
 //   k_fine_sort   one workgroup per coarse bin (128 buckets): LDS counting sort, writes the
 //                 sorted (value, key) arrays and every bucket's offset/count; the value of
 //                 a bucket's first entry carries SV_FIRST (bit 31), so the accumulation
@@ -70,6 +70,24 @@ constexpr int TILE_TERMS = 4096;                        // terms per tile (16 pe
 // indices stay below 2^30: at most 16 x 2^26 commit-key points)
 constexpr uint32_t SV_FIRST = 1u << 31;
 KZ_DEV uint32_t sv_point(uint32_t v) { return (v & ~SV_FIRST) >> 1; }
+
+// Entries of the coarse pass (k_bin_scatter -> k_fine_sort): key << 32 | value in 8 B, or -- when
+// every value fits CV_BITS (fewer than 2^24 points: every batch up to n = 2^22 with GLV, every
+// 2^21-point MSM shard) -- fine << CV_BITS | value in 4 B, the coarse bin fixing the key's upper
+// bits: half the bytes through the scatter's stores and the fine sort's two reads.
+constexpr int CV_BITS = 25;
+template <class E>
+KZ_DEV E make_ent(uint32_t key, uint32_t val) {
+  if constexpr (sizeof(E) == 8) return ((uint64_t)key << 32) | val;
+  else return ((key & (FINE - 1)) << CV_BITS) | val;
+}
+KZ_DEV uint32_t ent_fine(uint64_t e) { return (uint32_t)(e >> 32) & (FINE - 1); }
+KZ_DEV uint32_t ent_val(uint64_t e) { return (uint32_t)e; }
+KZ_DEV uint32_t ent_fine(uint32_t e) { return e >> CV_BITS; }
+KZ_DEV uint32_t ent_val(uint32_t e) { return e & ((1u << CV_BITS) - 1); }
+// empty slot (never a real entry: compact values stay below 2^CV_BITS - 1)
+template <class E>
+constexpr E kNoEnt = ~(E)0;
 
 struct TileRef {
   int k, w;
@@ -187,13 +205,13 @@ static __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __rest
 // consecutive threads store consecutive addresses of a bin's run (the tile's run in each bin
 // is contiguous in `tmp`); writing each entry from the thread that ranked it scattered every
 // wavefront store over ~64 bins.
-static __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t* __restrict__ digits,
-                                                     uint32_t* __restrict__ coarse_cursor,
-                                                     uint64_t* __restrict__ tmp) {
+template <class E>
+__global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t* __restrict__ digits,
+                                                     uint32_t* __restrict__ coarse_cursor, E* __restrict__ tmp) {
   __shared__ uint32_t hist[BINS_PER_SET];
   __shared__ uint32_t base[BINS_PER_SET];   // global start of this tile's run in bin b
   __shared__ uint32_t lstart[BINS_PER_SET]; // local (staged) start of bin b
-  __shared__ uint64_t stage[TILE_TERMS];
+  __shared__ E stage[TILE_TERMS];
   __shared__ uint8_t stage_bin[TILE_TERMS];
   const TileRef T = tile_decode(tl, blockIdx.x);
   const TermClass& C = tl.c[T.k];
@@ -234,7 +252,7 @@ static __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const u
     if (key[j] == 0xffffffffu) continue;
     const uint32_t bin = (key[j] >> COARSE_SHIFT) & (BINS_PER_SET - 1);
     const uint32_t q = lstart[bin] + rank[j];
-    stage[q] = ((uint64_t)key[j] << 32) | ent[j];
+    stage[q] = make_ent<E>(key[j], ent[j]);
     stage_bin[q] = (uint8_t)bin;
   }
   __syncthreads();
@@ -262,7 +280,8 @@ constexpr int FINE_STAGE = 8192;
 // kernel's staging array.  A chunk's entries stay in registers between the ranking and the
 // staging: chunks of FINE_STAGE / 2 keep the kernel within 128 VGPRs (4 workgroups per CU for
 // the staged bins, whose LDS allows 4).
-KZ_DEV void fine_sort_chunks(uint32_t g, uint32_t start, uint32_t count, const uint64_t* __restrict__ tmp,
+template <class E>
+KZ_DEV void fine_sort_chunks(uint32_t g, uint32_t start, uint32_t count, const E* __restrict__ tmp,
                              const uint32_t* bstart, uint32_t* cursor, uint32_t* stage,
                              uint32_t* __restrict__ sorted_val, uint32_t* __restrict__ sorted_key) {
   constexpr uint32_t CHUNK = FINE_STAGE / 2, PER = CHUNK / 256;  // 16 per thread: 147 -> <= 128 VGPRs
@@ -273,16 +292,16 @@ KZ_DEV void fine_sort_chunks(uint32_t g, uint32_t start, uint32_t count, const u
     const uint32_t cn = min(CHUNK, count - c0);
     if (t < FINE) ccnt[t] = 0;
     __syncthreads();
-    uint64_t v[PER];
+    E v[PER];
     uint32_t rank[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const uint32_t e = j * 256 + t;
-      v[j] = e < cn ? tmp[start + c0 + e] : ~0ull;
+      v[j] = e < cn ? tmp[start + c0 + e] : kNoEnt<E>;
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j)
-      rank[j] = v[j] != ~0ull ? atomicAdd(&ccnt[(uint32_t)(v[j] >> 32) & (FINE - 1)], 1u) : 0u;
+      rank[j] = v[j] != kNoEnt<E> ? atomicAdd(&ccnt[ent_fine(v[j])], 1u) : 0u;
     __syncthreads();
     const uint32_t tot = t < FINE ? ccnt[t] : 0u;
     if (t < FINE) cscan[t] = tot;
@@ -295,10 +314,10 @@ KZ_DEV void fine_sort_chunks(uint32_t g, uint32_t start, uint32_t count, const u
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      if (v[j] == ~0ull) continue;
-      const uint32_t b = (uint32_t)(v[j] >> 32) & (FINE - 1);
+      if (v[j] == kNoEnt<E>) continue;
+      const uint32_t b = ent_fine(v[j]);
       const uint32_t q = cscan[b] - ccnt[b] + rank[j];
-      stage[q] = (uint32_t)v[j];
+      stage[q] = ent_val(v[j]);
     }
     __syncthreads();
     for (uint32_t q = t; q < cn; q += 256) {
@@ -316,9 +335,9 @@ KZ_DEV void fine_sort_chunks(uint32_t g, uint32_t start, uint32_t count, const u
   }
 }
 
-static __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ coarse_off,
-                                                   const uint32_t* __restrict__ coarse_cnt,
-                                                   const uint64_t* __restrict__ tmp,
+template <class E>
+__global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ coarse_off,
+                                                   const uint32_t* __restrict__ coarse_cnt, const E* __restrict__ tmp,
                                                    uint32_t* __restrict__ off, uint32_t* __restrict__ cnt,
                                                    uint32_t* __restrict__ sorted_val,
                                                    uint32_t* __restrict__ sorted_key) {
@@ -333,15 +352,15 @@ static __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __rest
   if (t < FINE) fine[t] = 0;
   __syncthreads();
   for (uint32_t e0 = t; e0 < count; e0 += 256 * FINE_ILP) {
-    uint32_t k[FINE_ILP];
+    uint32_t k[FINE_ILP];  // fine index, FINE = none
 #pragma unroll
     for (int j = 0; j < FINE_ILP; ++j) {
       const uint32_t e = e0 + 256 * j;
-      k[j] = e < count ? (uint32_t)(tmp[start + e] >> 32) : 0xffffffffu;
+      k[j] = e < count ? ent_fine(tmp[start + e]) : (uint32_t)FINE;
     }
 #pragma unroll
     for (int j = 0; j < FINE_ILP; ++j)
-      if (k[j] != 0xffffffffu) atomicAdd(&fine[k[j] & (FINE - 1)], 1u);
+      if (k[j] < (uint32_t)FINE) atomicAdd(&fine[k[j]], 1u);
   }
   __syncthreads();
   const uint32_t tot = t < FINE ? fine[t] : 0u;
@@ -370,23 +389,23 @@ static __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __rest
   }
 #endif
   for (uint32_t e0 = t; e0 < count; e0 += 256 * FINE_ILP) {
-    uint64_t v[FINE_ILP];
+    E v[FINE_ILP];
 #pragma unroll
     for (int j = 0; j < FINE_ILP; ++j) {
       const uint32_t e = e0 + 256 * j;
-      v[j] = e < count ? tmp[start + e] : ~0ull;
+      v[j] = e < count ? tmp[start + e] : kNoEnt<E>;
     }
 #pragma unroll
     for (int j = 0; j < FINE_ILP; ++j) {
-      if (v[j] == ~0ull) continue;
-      const uint32_t key = (uint32_t)(v[j] >> 32);
-      const uint32_t p = atomicAdd(&cursor[key & (FINE - 1)], 1u);
-      const uint32_t first = p == scan[key & (FINE - 1)] - fine[key & (FINE - 1)] ? SV_FIRST : 0u;
+      if (v[j] == kNoEnt<E>) continue;
+      const uint32_t f = ent_fine(v[j]);
+      const uint32_t p = atomicAdd(&cursor[f], 1u);
+      const uint32_t first = p == scan[f] - fine[f] ? SV_FIRST : 0u;
       if (staged) {
-        stage[p] = (uint32_t)v[j] | first;
+        stage[p] = ent_val(v[j]) | first;
       } else {
-        sorted_val[start + p] = (uint32_t)v[j] | first;
-        sorted_key[start + p] = key;
+        sorted_val[start + p] = ent_val(v[j]) | first;
+        sorted_key[start + p] = g * FINE + f;
       }
     }
   }
