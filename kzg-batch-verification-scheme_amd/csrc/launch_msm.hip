@@ -13,8 +13,12 @@ void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const 
   uint32_t* ccur = coarse + 2 * nbins;
   (void)hipMemsetAsync(ccnt, 0, (size_t)nbins * 4, st);
   const uint32_t tiles = num_tiles_host(tl);
+#ifdef KZ_SORT_SEPARATE_COUNT
   if (tl.total) k_digits<<<grid_for(tl.total, 256), 256, 0, st>>>(tl, inf, digits);
   if (tiles) k_bin_count<<<tiles, 256, 0, st>>>(tl, digits, ccnt);
+#else
+  if (tl.total) k_digits_count<<<num_digit_groups_host(tl), 256, 0, st>>>(tl, inf, digits, ccnt);
+#endif
   k_bin_scan<<<1, 1024, 0, st>>>(ccnt, nbins, coff, ccur, total);
   // 4-byte coarse-pass entries when every sorted value (point index << 1 | sign) fits CV_BITS
   uint64_t npts = 0;

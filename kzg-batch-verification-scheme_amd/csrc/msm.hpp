@@ -151,6 +151,76 @@ static __global__ void __launch_bounds__(256) k_digits(TermList tl, const uint8_
   }
 }
 
+// k_digits and k_bin_count in one pass: workgroup = 4096 terms of one class (16 per thread),
+// every window's digits written as in k_digits and counted into an LDS histogram per window,
+// then one global atomic per non-empty (window, coarse bin) -- the same atomics as k_bin_count's
+// tiles, without its second read of the digit array (KZ_SORT_SEPARATE_COUNT: the two kernels).
+inline uint32_t num_digit_groups_host(const TermList& tl) {
+  uint32_t g = 0;
+  for (uint32_t k = 0; k < tl.nclass; ++k) g += (tl.c[k].count + TILE_TERMS - 1) / TILE_TERMS;
+  return g;
+}
+static __global__ void __launch_bounds__(256) k_digits_count(TermList tl, const uint8_t* __restrict__ inf,
+                                                      uint32_t* __restrict__ digits,
+                                                      uint32_t* __restrict__ coarse_cnt) {
+  __shared__ uint32_t hist[16][BINS_PER_SET];
+  uint32_t b = blockIdx.x;
+  int k = 0;
+  for (; k < (int)tl.nclass - 1; ++k) {
+    const uint32_t nb = (tl.c[k].count + TILE_TERMS - 1) / TILE_TERMS;
+    if (b < nb) break;
+    b -= nb;
+  }
+  const TermClass& C = tl.c[k];
+  const uint32_t t = threadIdx.x;
+  const int w0 = (int)C.win_off, w1 = (int)(C.win_off + C.nwin);
+#pragma unroll
+  for (int w = 0; w < 16; ++w) hist[w][t] = 0;
+  __syncthreads();
+#pragma unroll 1
+  for (int j = 0; j < TILE_TERMS / 256; ++j) {
+    const uint32_t i = b * TILE_TERMS + j * 256 + t;
+    if (i >= C.count) break;
+    const uint32_t* sp = C.scal + (size_t)i * C.scal_stride;
+    uint32_t w8[8];
+    bool neg = false;
+    if (C.scal_words == 4) {
+      const uint4 q = *reinterpret_cast<const uint4*>(sp);
+      neg = (q.w >> 31) != 0;
+      w8[0] = q.x; w8[1] = q.y; w8[2] = q.z; w8[3] = q.w & 0x7fffffffu;
+      w8[4] = w8[5] = w8[6] = w8[7] = 0;
+    } else {
+      const uint4 q0 = *reinterpret_cast<const uint4*>(sp);
+      const uint4 q1 = *reinterpret_cast<const uint4*>(sp + 4);
+      w8[0] = q0.x; w8[1] = q0.y; w8[2] = q0.z; w8[3] = q0.w;
+      w8[4] = q1.x; w8[5] = q1.y; w8[6] = q1.z; w8[7] = q1.w;
+    }
+    const bool is_inf = inf[C.pt_base + i] != 0;
+    uint32_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      if (w >= w1) break;
+      const uint32_t raw = (w8[w >> 1] >> ((w & 1) * 16)) & 0xffffu;
+      int d = (int)(raw + carry);
+      if (d > NBUCKETS) { d -= (1 << WBITS); carry = 1; } else { carry = 0; }
+      if (w >= w0) {
+        uint32_t code = 0;
+        if (d != 0 && !is_inf) {
+          const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+          code = mag | ((d < 0) != neg ? 0x80000000u : 0u);
+          atomicAdd(&hist[w - w0][(mag - 1) >> COARSE_SHIFT], 1u);
+        }
+        digits[C.dig_base + (size_t)(w - w0) * C.count + i] = code;
+      }
+    }
+  }
+  __syncthreads();
+  for (int w = 0; w < (int)C.nwin; ++w) {
+    const uint32_t h = hist[w][t];
+    if (h) atomicAdd(&coarse_cnt[(C.set_base + w) * BINS_PER_SET + t], h);
+  }
+}
+
 static __global__ void __launch_bounds__(256) k_bin_count(TermList tl, const uint32_t* __restrict__ digits,
                                                    uint32_t* __restrict__ coarse_cnt) {
   __shared__ uint32_t hist[BINS_PER_SET];
