@@ -32,7 +32,7 @@ if acc and "SQ_INSTS_VALU" in acc:
                              "issue_stall (SQ_WAIT_INST_ANY)": acc["SQ_WAIT_INST_ANY"] / wc,
                              "parked on waitcnt/barrier (SQ_WAIT_ANY)": acc["SQ_WAIT_ANY"] / wc},
         "note": "SQ_INSTS_VALU counts wave-instructions: x 64 lanes / 32 n additions = per-addition VALU count "
-                "(3738 of them v_mad_u64_u32: 8 radix-29 products x 392 + 2 squarings x 301). Wait counters "
+                "(3544 of them v_mad_u64_u32: 8 radix-29 products x 392 + 2 squarings x 301 - 196 saved by the Y3 pair's shared reduction). Wait counters "
                 "overlap across the 4 waves per SIMD (a parked wave's SIMD issues for the others)."}
 json.dump(out, open(dst, "w"), indent=1)
 print(json.dumps(out.get("k_accumulate"), indent=1))
