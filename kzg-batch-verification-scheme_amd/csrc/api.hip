@@ -263,7 +263,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
       if (tl.c[k].count) npts = std::max(npts, tl.c[k].pt_base + tl.c[k].count);
     L::pts_to29(st, s.pts.template as<Affine<Cv>>(), npts);
   }
-  L::sort(st, tl, nsets, inf, s.digits.template as<uint32_t>(), s.coarse.template as<uint32_t>(), s.ent.template as<uint64_t>(),
+  L::sort(st, tl, nsets, inf, s.digits.template as<uint32_t>(), s.coarse.template as<uint32_t>(), s.ent.template as<uint64_t>(), emax,
           s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.total.template as<uint32_t>(),
           s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>());
   mark(c, s, PH_SORT + 1);

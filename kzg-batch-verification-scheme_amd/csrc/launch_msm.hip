@@ -5,7 +5,7 @@ namespace kzgmi {
 
 template <class Cv>
 void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const uint8_t* inf, uint32_t* digits,
-                      uint32_t* coarse, uint64_t* ent, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
+                      uint32_t* coarse, uint64_t* ent, size_t emax, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
                       uint32_t* skey) {
   const uint32_t nbins = nsets * BINS_PER_SET;
   uint32_t* ccnt = coarse;
@@ -20,20 +20,20 @@ void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const 
   if (tl.total) k_digits_count<<<num_digit_groups_host(tl), 256, 0, st>>>(tl, inf, digits, ccnt);
 #endif
   k_bin_scan<<<1, 1024, 0, st>>>(ccnt, nbins, coff, ccur, total);
-  // 4-byte coarse-pass entries when every sorted value (point index << 1 | sign) fits CV_BITS
+  // coarse-pass entries (msm.hpp EntPacked / EntSplit): packed 4 B when every sorted value (point
+  // index << 1 | sign) fits CV_BITS, else 4 B values + 1 B fine indices (ent holds emax x 8 B)
   uint64_t npts = 0;
   for (uint32_t k = 0; k < tl.nclass; ++k)
     if (tl.c[k].count) npts = std::max<uint64_t>(npts, (uint64_t)tl.c[k].pt_base + tl.c[k].count);
-#ifndef KZ_SORT_WIDE_ENTRIES
   if (2 * npts < (1ull << CV_BITS)) {
-    uint32_t* e32 = reinterpret_cast<uint32_t*>(ent);
-    if (tiles) k_bin_scatter<uint32_t><<<tiles, 256, 0, st>>>(tl, digits, ccur, e32);
-    k_fine_sort<uint32_t><<<nbins, 256, 0, st>>>(coff, ccnt, e32, off, cnt, sval, skey);
-    return;
+    const EntPacked e{reinterpret_cast<uint32_t*>(ent)};
+    if (tiles) k_bin_scatter<EntPacked><<<tiles, 256, 0, st>>>(tl, digits, ccur, e);
+    k_fine_sort<EntPacked><<<nbins, 256, 0, st>>>(coff, ccnt, e, off, cnt, sval, skey);
+  } else {
+    const EntSplit e{reinterpret_cast<uint32_t*>(ent), reinterpret_cast<uint8_t*>(ent) + 4 * emax};
+    if (tiles) k_bin_scatter<EntSplit><<<tiles, 256, 0, st>>>(tl, digits, ccur, e);
+    k_fine_sort<EntSplit><<<nbins, 256, 0, st>>>(coff, ccnt, e, off, cnt, sval, skey);
   }
-#endif
-  if (tiles) k_bin_scatter<uint64_t><<<tiles, 256, 0, st>>>(tl, digits, ccur, ent);
-  k_fine_sort<uint64_t><<<nbins, 256, 0, st>>>(coff, ccnt, ent, off, cnt, sval, skey);
 }
 
 template <class Cv>
@@ -70,7 +70,7 @@ void Launch<Cv>::window_combine(hipStream_t st, const MsmWindows& mw, const XY* 
 }
 
 template void Launch<KZ_CURVE_T>::sort(hipStream_t, const TermList&, uint32_t, const uint8_t*, uint32_t*, uint32_t*,
-                                       uint64_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*);
+                                       uint64_t*, size_t, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*);
 template void Launch<KZ_CURVE_T>::accumulate(hipStream_t, size_t, const uint32_t*, const uint32_t*, const uint32_t*,
                                              const uint32_t*, const uint32_t*, const Affine<KZ_CURVE_T>*,
                                              Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, uint32_t*,

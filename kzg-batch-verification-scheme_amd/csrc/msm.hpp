@@ -55,7 +55,7 @@ struct TermList {
 //                 coarse bins (key >> 7), then one global atomic per non-empty bin
 //   k_bin_scan    exclusive scan of the nsets*256 coarse counts (+ total entries)
 //   k_bin_scatter same digits; LDS ranks, one global atomic per bin reserves the tile's run,
-//                 entries (key, value: make_ent) written into their coarse bin
+//                 entries (fine index, value: EntPacked / EntSplit) written into their coarse bin
 //   k_fine_sort   one workgroup per coarse bin (128 buckets): LDS counting sort, writes the
 //                 sorted (value, key) arrays and every bucket's offset/count; the value of
 //                 a bucket's first entry carries SV_FIRST (bit 31), so the accumulation
@@ -71,23 +71,41 @@ constexpr int TILE_TERMS = 4096;                        // terms per tile (16 pe
 constexpr uint32_t SV_FIRST = 1u << 31;
 KZ_DEV uint32_t sv_point(uint32_t v) { return (v & ~SV_FIRST) >> 1; }
 
-// Entries of the coarse pass (k_bin_scatter -> k_fine_sort): key << 32 | value in 8 B, or -- when
-// every value fits CV_BITS (fewer than 2^24 points: every batch up to n = 2^22 with GLV, every
-// 2^21-point MSM shard) -- fine << CV_BITS | value in 4 B, the coarse bin fixing the key's upper
-// bits: half the bytes through the scatter's stores and the fine sort's two reads.
+// Entries of the coarse pass (k_bin_scatter -> k_fine_sort): the coarse bin fixes a key's upper
+// bits, so an entry is its 7-bit fine index and its sorted value.  Packed: fine << CV_BITS |
+// value in 4 B, when every value fits CV_BITS (fewer than 2^24 points: every BLS12-381 batch up to
+// n = 2^23, every 2^21-point MSM shard).  Split: the value (4 B) and the fine index (1 B) in two
+// arrays, for any size (BN254 2^22 with its GLV images, the 2^24-point MSM, the commit key) --
+// the fine sort's histogram pass then reads 1 B per entry.  (The round-2 form, key << 32 |
+// value in 8 B, moved 16 B per entry through the fine sort's two reads.)
 constexpr int CV_BITS = 25;
-template <class E>
-KZ_DEV E make_ent(uint32_t key, uint32_t val) {
-  if constexpr (sizeof(E) == 8) return ((uint64_t)key << 32) | val;
-  else return ((key & (FINE - 1)) << CV_BITS) | val;
-}
-KZ_DEV uint32_t ent_fine(uint64_t e) { return (uint32_t)(e >> 32) & (FINE - 1); }
-KZ_DEV uint32_t ent_val(uint64_t e) { return (uint32_t)e; }
-KZ_DEV uint32_t ent_fine(uint32_t e) { return e >> CV_BITS; }
-KZ_DEV uint32_t ent_val(uint32_t e) { return e & ((1u << CV_BITS) - 1); }
-// empty slot (never a real entry: compact values stay below 2^CV_BITS - 1)
-template <class E>
-constexpr E kNoEnt = ~(E)0;
+struct EntPacked {
+  uint32_t* p;
+  using R = uint32_t;  // register form
+  KZ_DEV R load(size_t i) const { return p[i]; }
+  KZ_DEV uint32_t fine_at(size_t i) const { return p[i] >> CV_BITS; }
+  KZ_DEV void store(size_t i, R r) const { p[i] = r; }
+  KZ_DEV static uint32_t fine(R r) { return r >> CV_BITS; }
+  KZ_DEV static uint32_t val(R r) { return r & ((1u << CV_BITS) - 1); }
+  KZ_DEV static R make(uint32_t key, uint32_t v) { return ((key & (FINE - 1)) << CV_BITS) | v; }
+};
+struct EntSplit {
+  uint32_t* p;
+  uint8_t* f;
+  using R = uint64_t;  // fine << 32 | value
+  KZ_DEV R load(size_t i) const { return ((uint64_t)f[i] << 32) | p[i]; }
+  KZ_DEV uint32_t fine_at(size_t i) const { return f[i]; }
+  KZ_DEV void store(size_t i, R r) const {
+    p[i] = (uint32_t)r;
+    f[i] = (uint8_t)(r >> 32);
+  }
+  KZ_DEV static uint32_t fine(R r) { return (uint32_t)(r >> 32); }
+  KZ_DEV static uint32_t val(R r) { return (uint32_t)r; }
+  KZ_DEV static R make(uint32_t key, uint32_t v) { return ((uint64_t)(key & (FINE - 1)) << 32) | v; }
+};
+// empty register slot (never a real entry: packed values stay below 2^CV_BITS - 1, fine < 128)
+template <class R>
+constexpr R kNoEnt = ~(R)0;
 
 struct TileRef {
   int k, w;
@@ -277,11 +295,11 @@ static __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __rest
 // wavefront store over ~64 bins.
 template <class E>
 __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t* __restrict__ digits,
-                                                     uint32_t* __restrict__ coarse_cursor, E* __restrict__ tmp) {
+                                                     uint32_t* __restrict__ coarse_cursor, E tmp) {
   __shared__ uint32_t hist[BINS_PER_SET];
   __shared__ uint32_t base[BINS_PER_SET];   // global start of this tile's run in bin b
   __shared__ uint32_t lstart[BINS_PER_SET]; // local (staged) start of bin b
-  __shared__ E stage[TILE_TERMS];
+  __shared__ typename E::R stage[TILE_TERMS];
   __shared__ uint8_t stage_bin[TILE_TERMS];
   const TileRef T = tile_decode(tl, blockIdx.x);
   const TermClass& C = tl.c[T.k];
@@ -322,13 +340,13 @@ __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t
     if (key[j] == 0xffffffffu) continue;
     const uint32_t bin = (key[j] >> COARSE_SHIFT) & (BINS_PER_SET - 1);
     const uint32_t q = lstart[bin] + rank[j];
-    stage[q] = make_ent<E>(key[j], ent[j]);
+    stage[q] = E::make(key[j], ent[j]);
     stage_bin[q] = (uint8_t)bin;
   }
   __syncthreads();
   for (uint32_t q = t; q < ntile; q += 256) {
     const uint32_t bin = stage_bin[q];
-    tmp[base[bin] + (q - lstart[bin])] = stage[q];
+    tmp.store(base[bin] + (q - lstart[bin]), stage[q]);
   }
 }
 
@@ -351,7 +369,7 @@ constexpr int FINE_STAGE = 8192;
 // staging: chunks of FINE_STAGE / 2 keep the kernel within 128 VGPRs (4 workgroups per CU for
 // the staged bins, whose LDS allows 4).
 template <class E>
-KZ_DEV void fine_sort_chunks(uint32_t g, uint32_t start, uint32_t count, const E* __restrict__ tmp,
+KZ_DEV void fine_sort_chunks(uint32_t g, uint32_t start, uint32_t count, const E tmp,
                              const uint32_t* bstart, uint32_t* cursor, uint32_t* stage,
                              uint32_t* __restrict__ sorted_val, uint32_t* __restrict__ sorted_key) {
   constexpr uint32_t CHUNK = FINE_STAGE / 2, PER = CHUNK / 256;  // 16 per thread: 147 -> <= 128 VGPRs
@@ -362,16 +380,17 @@ KZ_DEV void fine_sort_chunks(uint32_t g, uint32_t start, uint32_t count, const E
     const uint32_t cn = min(CHUNK, count - c0);
     if (t < FINE) ccnt[t] = 0;
     __syncthreads();
-    E v[PER];
+    using R = typename E::R;
+    R v[PER];
     uint32_t rank[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const uint32_t e = j * 256 + t;
-      v[j] = e < cn ? tmp[start + c0 + e] : kNoEnt<E>;
+      v[j] = e < cn ? tmp.load(start + c0 + e) : kNoEnt<R>;
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j)
-      rank[j] = v[j] != kNoEnt<E> ? atomicAdd(&ccnt[ent_fine(v[j])], 1u) : 0u;
+      rank[j] = v[j] != kNoEnt<R> ? atomicAdd(&ccnt[E::fine(v[j])], 1u) : 0u;
     __syncthreads();
     const uint32_t tot = t < FINE ? ccnt[t] : 0u;
     if (t < FINE) cscan[t] = tot;
@@ -384,10 +403,10 @@ KZ_DEV void fine_sort_chunks(uint32_t g, uint32_t start, uint32_t count, const E
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      if (v[j] == kNoEnt<E>) continue;
-      const uint32_t b = ent_fine(v[j]);
+      if (v[j] == kNoEnt<R>) continue;
+      const uint32_t b = E::fine(v[j]);
       const uint32_t q = cscan[b] - ccnt[b] + rank[j];
-      stage[q] = ent_val(v[j]);
+      stage[q] = E::val(v[j]);
     }
     __syncthreads();
     for (uint32_t q = t; q < cn; q += 256) {
@@ -407,7 +426,7 @@ KZ_DEV void fine_sort_chunks(uint32_t g, uint32_t start, uint32_t count, const E
 
 template <class E>
 __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ coarse_off,
-                                                   const uint32_t* __restrict__ coarse_cnt, const E* __restrict__ tmp,
+                                                   const uint32_t* __restrict__ coarse_cnt, const E tmp,
                                                    uint32_t* __restrict__ off, uint32_t* __restrict__ cnt,
                                                    uint32_t* __restrict__ sorted_val,
                                                    uint32_t* __restrict__ sorted_key) {
@@ -426,7 +445,7 @@ __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ 
 #pragma unroll
     for (int j = 0; j < FINE_ILP; ++j) {
       const uint32_t e = e0 + 256 * j;
-      k[j] = e < count ? ent_fine(tmp[start + e]) : (uint32_t)FINE;
+      k[j] = e < count ? tmp.fine_at(start + e) : (uint32_t)FINE;
     }
 #pragma unroll
     for (int j = 0; j < FINE_ILP; ++j)
@@ -459,22 +478,23 @@ __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ 
   }
 #endif
   for (uint32_t e0 = t; e0 < count; e0 += 256 * FINE_ILP) {
-    E v[FINE_ILP];
+    using R = typename E::R;
+    R v[FINE_ILP];
 #pragma unroll
     for (int j = 0; j < FINE_ILP; ++j) {
       const uint32_t e = e0 + 256 * j;
-      v[j] = e < count ? tmp[start + e] : kNoEnt<E>;
+      v[j] = e < count ? tmp.load(start + e) : kNoEnt<R>;
     }
 #pragma unroll
     for (int j = 0; j < FINE_ILP; ++j) {
-      if (v[j] == kNoEnt<E>) continue;
-      const uint32_t f = ent_fine(v[j]);
+      if (v[j] == kNoEnt<R>) continue;
+      const uint32_t f = E::fine(v[j]);
       const uint32_t p = atomicAdd(&cursor[f], 1u);
       const uint32_t first = p == scan[f] - fine[f] ? SV_FIRST : 0u;
       if (staged) {
-        stage[p] = ent_val(v[j]) | first;
+        stage[p] = E::val(v[j]) | first;
       } else {
-        sorted_val[start + p] = ent_val(v[j]) | first;
+        sorted_val[start + p] = E::val(v[j]) | first;
         sorted_key[start + p] = g * FINE + f;
       }
     }
