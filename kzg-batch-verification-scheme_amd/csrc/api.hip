@@ -249,7 +249,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   if constexpr (kAcc29<Cv>) CHK(s.acc29.ensure(((size_t)NB + 2 * nchunks) * W29 * 4));
   const size_t seg_rec = std::max(sizeof(XY), (size_t)W29 * 4);  // 32-bit XYZZ or a radix-29 record
   CHK(s.R.ensure((size_t)NB / SEG * seg_rec));
-  CHK(s.U.ensure((size_t)NB / SEG * seg_rec));
+  CHK(s.U.ensure((size_t)NB / SEG * seg_rec * (kSegV ? 2 : 1)));  // U records, then the V records
   CHK(s.scratch.ensure((size_t)nsets * RB_PARTS * sizeof(XY)));  // k_reduce_bits partial sums
   CHK(s.winsum.ensure((size_t)nsets * sizeof(XY)));
   CHK(s.res.ensure(2 * sizeof(XY)));

@@ -1124,12 +1124,19 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
 }
 
 // ------------------------------------------------------------------------------ reduction
-// Segment g covers buckets [g*SEG, (g+1)*SEG) of one set (SEG divides NBUCKETS).
-//   R_g = sum_{i} i * S_{g*SEG+i},  U_g = sum_i S_{g*SEG+i}
-// Two threads per segment (adjacent lanes): half h runs the running sums over buckets
-// [8h, 8h + 8) of the segment -- R_h = sum_{i<8} i S_{8h+i}, U_h = sum_{i<8} S_{8h+i} -- then
-// R_g = R_0 + (R_1 + 8 U_1), U_g = U_0 + U_1 after one LDS exchange: a chain of ~20 point
-// operations instead of 31 (the kernel is latency-bound at < 1 wave per SIMD; 1.14 ms before).
+// Segment g covers buckets [g*SEG, (g+1)*SEG) of one set (SEG divides NBUCKETS).  Two threads
+// per segment (adjacent lanes): half h runs the running sums over buckets [8h, 8h + 8) of the
+// segment -- R_h = sum_{i<8} i S_{8h+i}, U_h = sum_{i<8} S_{8h+i} -- and after one exchange
+//   R'_g = R_0 + R_1,  U_g = U_0 + U_1,  V_g = U_1  (records R, U and V = U + nseg)
+// so that sum_i i S_{g*SEG+i} = R'_g + 8 V_g; the 8 V_g term is summed over all segments in
+// k_reduce_bits and scaled once in k_reduce_bits_finish.  (Forming R_1 + 8 U_1 here put three
+// doublings on the upper half's chain while the lower half idled: ~20 point operations per
+// wave instead of ~16; the kernel is latency-bound at 1.5 waves per SIMD.)
+#ifndef KZ_REDUCE_R8U
+constexpr bool kSegV = true;
+#else  // A/B reference: R_g = R_0 + (R_1 + 8 U_1) per segment, no V records
+constexpr bool kSegV = false;
+#endif
 template <class Cv>
 __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const uint32_t* __restrict__ cnt,
                                                          const Xyzz<Cv>* __restrict__ buckets,
@@ -1150,13 +1157,17 @@ __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const
         acc = x29_add<Cv, Q>(acc, run);
       }
       if (cnt[base]) run = x29_add<Cv, Q>(run, load_x29<Q>(acc29, base));
-      if (h == 1) acc = x29_add<Cv, Q>(acc, x29_dbl<Q>(x29_dbl<Q>(x29_dbl<Q>(run))));  // R_1 + 8 U_1
+      if (!kSegV && h == 1) acc = x29_add<Cv, Q>(acc, x29_dbl<Q>(x29_dbl<Q>(x29_dbl<Q>(run))));  // R_1 + 8 U_1
     }
-    // h = 0 needs the partner's R_1 + 8 U_1, h = 1 the partner's U_0 (adjacent lanes, whole wave)
+    // h = 0 needs the partner's R_1, h = 1 the partner's U_0 (adjacent lanes, whole wave)
     const X29<Q> other = x29_swap_pair<Q>(h ? acc : run);
     if (g >= nseg) return;
-    if (h == 0) store_x29<Q>(reinterpret_cast<uint32_t*>(R), g, x29_add<Cv, Q>(acc, other));
-    else store_x29<Q>(reinterpret_cast<uint32_t*>(U), g, x29_add<Cv, Q>(run, other));
+    if (h == 0) {
+      store_x29<Q>(reinterpret_cast<uint32_t*>(R), g, x29_add<Cv, Q>(acc, other));
+    } else {
+      store_x29<Q>(reinterpret_cast<uint32_t*>(U), g, x29_add<Cv, Q>(run, other));
+      if (kSegV) store_x29<Q>(reinterpret_cast<uint32_t*>(U), (size_t)nseg + g, run);  // V_g = U_1
+    }
   } else {
     __shared__ __attribute__((aligned(16))) Xyzz<Cv> xch[256];
     Xyzz<Cv> run = Xyzz<Cv>::inf(), acc = Xyzz<Cv>::inf();
@@ -1167,15 +1178,19 @@ __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const
         acc = xyzz_add(acc, run);
       }
       if (cnt[base]) run = xyzz_add(run, load_xyzz(&buckets[base]));
-      if (h == 1) acc = xyzz_add(acc, xyzz_dbl(xyzz_dbl(xyzz_dbl(run))));  // R_1 + 8 U_1
+      if (!kSegV && h == 1) acc = xyzz_add(acc, xyzz_dbl(xyzz_dbl(xyzz_dbl(run))));  // R_1 + 8 U_1
     }
     // h = 0 needs the partner's R_1 + 8 U_1, h = 1 the partner's U_0
     store_xyzz(&xch[threadIdx.x], h ? acc : run);
     __syncthreads();
     if (g >= nseg) return;
     const Xyzz<Cv> other = load_xyzz(&xch[threadIdx.x ^ 1]);
-    if (h == 0) store_xyzz(&R[g], xyzz_add(acc, other));
-    else store_xyzz(&U[g], xyzz_add(run, other));
+    if (h == 0) {
+      store_xyzz(&R[g], xyzz_add(acc, other));
+    } else {
+      store_xyzz(&U[g], xyzz_add(run, other));
+      if (kSegV) store_xyzz(&U[nseg + g], run);  // V_g = U_1
+    }
   }
 }
 
@@ -1194,19 +1209,20 @@ KZ_DEV Xyzz<Cv> block_sum256(Xyzz<Cv> v, Xyzz<Cv>* lds) {
 
 // Window sums with a short dependency chain (~40 point operations per set; the earlier one
 // workgroup per set with three serial 16-term segment levels needed ~130, 3.8 vs 1.2 ms):
-//   W = sum_g (R_g + U_g) + SEG * sum_g g U_g,   sum_g g U_g = sum_j 2^j B_j,
+//   W = sum_g (R'_g + U_g) + 8 sum_g V_g + SEG * sum_g g U_g,   sum_g g U_g = sum_j 2^j B_j,
 //   B_j = sum of the 1024 U_g whose index g has bit j set (j < 11, NSEG = 2^11).
 // k_reduce_bits: RB_PARTS workgroups per set -- 11 compute B_j, 4 compute quarter sums of
-// R_g + U_g -- each 4 points per thread + an 8-level LDS tree.  k_reduce_bits_finish: one thread
-// per set, Horner over the 11 bit sums (10 doublings + 10 additions) + 4 doublings.
-constexpr int RB_PARTS = 15;
+// R'_g + U_g, 2 compute half sums of V_g -- each 4 points per thread + an 8-level LDS tree.
+// k_reduce_bits_finish: one wave per set, Horner over the 11 bit sums (10 doublings + 10
+// additions), then 2 H + sum V, 3 doublings: 16 H + 8 sum V.
+constexpr int RB_PARTS = kSegV ? 17 : 15;
 
 template <class Cv>
 __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict__ R, const Xyzz<Cv>* __restrict__ U,
                                                      Xyzz<Cv>* __restrict__ parts) {
   KZ_TAIL_PRIO();
   constexpr uint32_t NSEG = NBUCKETS / SEG;  // 2048 = 2^11
-  static_assert(NSEG == 2048 && RB_PARTS == 15, "bit decomposition assumes 2^11 segments per set");
+  static_assert(NSEG == 2048 && RB_PARTS == (kSegV ? 17 : 15), "bit decomposition assumes 2^11 segments per set");
   const uint32_t set = blockIdx.x / RB_PARTS, j = blockIdx.x % RB_PARTS;
   if constexpr (kAcc29<Cv>) {  // BLS12-381: radix 2^29 on the R/U records, inline additions
     using Q = Fp29Of<Cv>;
@@ -1215,8 +1231,13 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
     const uint32_t t = threadIdx.x;
     const uint32_t* R29 = reinterpret_cast<const uint32_t*>(R) + (size_t)set * NSEG * W29;
     const uint32_t* U29 = reinterpret_cast<const uint32_t*>(U) + (size_t)set * NSEG * W29;
+    const uint32_t nsets = gridDim.x / RB_PARTS;  // V records follow the nsets * NSEG U records
+    const uint32_t* V29 = reinterpret_cast<const uint32_t*>(U) + ((size_t)nsets + set) * NSEG * W29;
     X29<Q> v{F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), true};
-    if (j < 11) {
+    if (j >= 15) {  // kSegV: half sums of V_g
+#pragma unroll 1
+      for (uint32_t i = 0; i < 4; ++i) v = x29_add<Cv, Q>(v, load_x29<Q>(V29, (j - 15) * (NSEG / 2) + t + 256 * i));
+    } else if (j < 11) {
 #pragma unroll 1
       for (uint32_t i = 0; i < 4; ++i) {  // q: 10-bit rank among the g with bit j set
         const uint32_t q = t + 256 * i;
@@ -1264,6 +1285,7 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
   __shared__ __attribute__((aligned(16))) Xyzz<Cv> lds[128];
   const Xyzz<Cv>* Rs = R + (size_t)set * NSEG;
   const Xyzz<Cv>* Us = U + (size_t)set * NSEG;
+  const Xyzz<Cv>* Vs = U + ((size_t)gridDim.x / RB_PARTS + set) * NSEG;
   const uint32_t t = threadIdx.x;
   // segment sum g: 32-bit XYZZ, or (BLS12-381) a radix-29 record converted as it is read
   auto seg = [&](bool r, uint32_t g) {
@@ -1275,7 +1297,10 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
     }
   };
   Xyzz<Cv> s = Xyzz<Cv>::inf();
-  if (j < 11) {
+  if (j >= 15) {  // kSegV: half sums of V_g
+#pragma unroll 1
+    for (uint32_t i = 0; i < 4; ++i) s = xyzz_add(s, load_xyzz(&Vs[(j - 15) * (NSEG / 2) + t + 256 * i]));
+  } else if (j < 11) {
 #pragma unroll 1
     for (uint32_t i = 0; i < 4; ++i) {  // q: 10-bit rank among the g with bit j set
       const uint32_t q = t + 256 * i;
@@ -1310,8 +1335,14 @@ __global__ void __launch_bounds__(64) k_reduce_bits_finish(const Xyzz<Cv>* __res
   for (int j = 9; j >= 0; --j) V = lp_xyzz_add(c, lp_xyzz_dbl(c, V), lp_load_xyzz(c, &P[j]));
   LpXyzz<Cv> W = lp_xyzz_add(c, lp_xyzz_add(c, lp_load_xyzz(c, &P[11]), lp_load_xyzz(c, &P[12])),
                              lp_xyzz_add(c, lp_load_xyzz(c, &P[13]), lp_load_xyzz(c, &P[14])));
+  if constexpr (kSegV) {  // 16 H + 8 sum V = 8 (2 H + sum V)
+    V = lp_xyzz_add(c, lp_xyzz_dbl(c, V), lp_xyzz_add(c, lp_load_xyzz(c, &P[15]), lp_load_xyzz(c, &P[16])));
 #pragma unroll 1
-  for (int i = 0; i < 4; ++i) V = lp_xyzz_dbl(c, V);
+    for (int i = 0; i < 3; ++i) V = lp_xyzz_dbl(c, V);
+  } else {
+#pragma unroll 1
+    for (int i = 0; i < 4; ++i) V = lp_xyzz_dbl(c, V);
+  }
   lp_store_xyzz(c, &winsum[set], lp_xyzz_add(c, W, V));
 }
 
