@@ -118,6 +118,7 @@ struct kzgmi_ctx {
   // batch-verifies/s pipelined when introduced (tools/ab_env.sh).
   int ncu = 0;                // compute units: the accumulation grid cap (kAccWaves, msm.hpp)
   size_t acc_threads_env = 0;  // KZGMI_ACC_THREADS override of that cap (0 = none)
+  bool sort_split = false;     // KZGMI_SORT_SPLIT: split coarse-pass entries at every size (tests)
   double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
   int phase_calls = 0;
   DevBuf table[2], table_base[2];
@@ -263,7 +264,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
       if (tl.c[k].count) npts = std::max(npts, tl.c[k].pt_base + tl.c[k].count);
     L::pts_to29(st, s.pts.template as<Affine<Cv>>(), npts);
   }
-  L::sort(st, tl, nsets, inf, s.digits.template as<uint32_t>(), s.coarse.template as<uint32_t>(), s.ent.template as<uint64_t>(), emax,
+  L::sort(st, tl, nsets, inf, s.digits.template as<uint32_t>(), s.coarse.template as<uint32_t>(), s.ent.template as<uint64_t>(), emax, c->sort_split,
           s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.total.template as<uint32_t>(),
           s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>());
   mark(c, s, PH_SORT + 1);
@@ -561,6 +562,7 @@ int kzgmi_ctx_create(kzgmi_ctx** out, int device_id, int pipeline_slots) {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_id) == hipSuccess && ncu > 0)
     c->ncu = ncu;
   if (const char* e = getenv("KZGMI_ACC_THREADS")) c->acc_threads_env = (size_t)strtoull(e, nullptr, 10);
+  if (const char* e = getenv("KZGMI_SORT_SPLIT")) c->sort_split = atoi(e) != 0;
   c->slots.resize(pipeline_slots);
   for (auto& s : c->slots) {
     if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||

@@ -14,7 +14,7 @@ struct Launch {
   // digits: sum_k count_k * nwin_k u32 (tl.c[k].dig_base set), coarse: 3 * nsets * 256 u32
   // (counts, offsets, cursors), ent: emax x 8 B (coarse-pass entries: msm.hpp EntPacked / EntSplit)
   static void sort(hipStream_t st, const TermList& tl, uint32_t nsets, const uint8_t* inf, uint32_t* digits,
-                   uint32_t* coarse, uint64_t* ent, size_t emax, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
+                   uint32_t* coarse, uint64_t* ent, size_t emax, bool force_split, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
                    uint32_t* skey);
   // both curves accumulate in radix 2^29: pts in that format (convert_points(to29) or
   // pts_to29), acc29 = (nb + 2 x launched threads) records of W29 words that stay the bucket

@@ -5,7 +5,7 @@ namespace kzgmi {
 
 template <class Cv>
 void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const uint8_t* inf, uint32_t* digits,
-                      uint32_t* coarse, uint64_t* ent, size_t emax, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
+                      uint32_t* coarse, uint64_t* ent, size_t emax, bool force_split, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
                       uint32_t* skey) {
   const uint32_t nbins = nsets * BINS_PER_SET;
   uint32_t* ccnt = coarse;
@@ -25,7 +25,7 @@ void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const 
   uint64_t npts = 0;
   for (uint32_t k = 0; k < tl.nclass; ++k)
     if (tl.c[k].count) npts = std::max<uint64_t>(npts, (uint64_t)tl.c[k].pt_base + tl.c[k].count);
-  if (2 * npts < (1ull << CV_BITS)) {
+  if (!force_split && 2 * npts < (1ull << CV_BITS)) {
     const EntPacked e{reinterpret_cast<uint32_t*>(ent)};
     if (tiles) k_bin_scatter<EntPacked><<<tiles, 256, 0, st>>>(tl, digits, ccur, e);
     k_fine_sort<EntPacked><<<nbins, 256, 0, st>>>(coff, ccnt, e, off, cnt, sval, skey);
@@ -70,7 +70,7 @@ void Launch<Cv>::window_combine(hipStream_t st, const MsmWindows& mw, const XY* 
 }
 
 template void Launch<KZ_CURVE_T>::sort(hipStream_t, const TermList&, uint32_t, const uint8_t*, uint32_t*, uint32_t*,
-                                       uint64_t*, size_t, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*);
+                                       uint64_t*, size_t, bool, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*);
 template void Launch<KZ_CURVE_T>::accumulate(hipStream_t, size_t, const uint32_t*, const uint32_t*, const uint32_t*,
                                              const uint32_t*, const uint32_t*, const Affine<KZ_CURVE_T>*,
                                              Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, uint32_t*,

@@ -215,6 +215,59 @@ def test_msm_skewed_buckets(ctx, curve):
 
 
 @pytest.mark.parametrize("curve", CURVES)
+def test_msm_skewed_large_bins(ctx, curve):
+    """Coarse bins above the fine sort's 8192-entry staging array (k_fine_sort's chunked path):
+    one bucket per window holding every term (it spans several 4096-entry chunks, so its
+    first-of-bucket flag and running cursor cross chunk boundaries), and a few heavy buckets
+    sharing one coarse bin (digits 1..5)."""
+    C = pc.CURVES[curve]
+    rng = random.Random(41)
+    n = 20000
+    ks = [rng.randrange(C.r) for _ in range(64)]
+    base = O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(k) for k in ks), 64)
+    g1b = 2 * C.fp_bytes
+    pts = b"".join(base[(i % 64) * g1b:(i % 64 + 1) * g1b] for i in range(n))
+    for sc in [b"".join(pk.fr_to_bytes(0x1234567) for _ in range(n)),
+               b"".join(pk.fr_to_bytes(rng.choice([1, 2, 3, 4, 5])) for _ in range(n))]:
+        assert ctx.msm_g1(curve, pts, sc) == O.msm_g1(curve, pts, sc, n)
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_split_sort_entries(curve, golden):
+    """The sort's split coarse-pass entries (4-B value + 1-B fine index, used from 2^24 points
+    on) at small sizes: a context made with KZGMI_SORT_SPLIT=1 uses them for every call.  Golden
+    batches (A, B, verdict) and the large-bin skewed MSMs against the oracle."""
+    import kzgmi
+    old = os.environ.get("KZGMI_SORT_SPLIT")
+    os.environ["KZGMI_SORT_SPLIT"] = "1"
+    try:
+        c = kzgmi.Context(0, 1)
+    finally:
+        if old is None:
+            del os.environ["KZGMI_SORT_SPLIT"]
+        else:
+            os.environ["KZGMI_SORT_SPLIT"] = old
+    try:
+        for n in SIZES[curve]:
+            g = golden("%s_batch_n%d.json" % (curve, n))
+            srs = c.load_srs(curve, h(g["g2"]), h(g["tau_g2"]))
+            ok = c.batch_verify(srs, h(g["commitments"]), h(g["zs"]), h(g["ys"]), h(g["proofs"]), seed=h(g["seed"]))
+            A, B = c.last_combination(curve)
+            assert (A.hex(), B.hex(), ok) == (g["valid"]["A"], g["valid"]["B"], g["valid"]["ok"]), n
+        C = pc.CURVES[curve]
+        g1b = 2 * C.fp_bytes
+        base = O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(k) for k in range(3, 67)), 64)
+        n = 20000
+        pts = b"".join(base[(i % 64) * g1b:(i % 64 + 1) * g1b] for i in range(n))
+        rng = random.Random(43)
+        for sc in [b"".join(pk.fr_to_bytes(0x1234567) for _ in range(n)),
+                   b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(n))]:
+            assert c.msm_g1(curve, pts, sc) == O.msm_g1(curve, pts, sc, n)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("curve", CURVES)
 def test_msm_cancelling_buckets(ctx, curve):
     """Buckets whose running sum returns to infinity mid-chunk (P + (-P)), then keeps adding
     (the accumulation's infinity flag, csrc/g1.hpp xyzz_acc_affine_lazy), doubling (P + P),
