@@ -223,7 +223,9 @@ def main():
     ap.add_argument("--curve", default="bls12_381", choices=["bls12_381", "bn254"])
     ap.add_argument("--slots", type=int, default=0,
                     help="batches in flight (default 16 single-GPU; sharded 8 + 2 combine lanes)")
-    ap.add_argument("--msm-steps", type=int, default=24)
+    ap.add_argument("--msm-steps", type=int, default=96,
+                    help="configs[1]: pipelined 2^20 MSMs timed (the drain of the last in-flight MSMs is "
+                         "inside the region: 24 steps read 356-358 M pts/s, 96 steps 372-374, tools/msm_steps_check.sh; 0 = skip)")
     ap.add_argument("--trusted-steps", type=int, default=96,
                     help="secondary: pipelined batches with KZGMI_FLAG_TRUSTED_G1 (GLV on BLS12-381; 0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
