@@ -39,6 +39,8 @@ __constant__ static const uint32_t kSha256K[64] = {
     0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
 
 KZ_DEV uint32_t ror32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+// a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96); hipcc emits two v_xor_b32 for it
+KZ_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
 
 KZ_DEV void sha256_init(uint32_t (&h)[8]) {
   h[0] = 0x6a09e667; h[1] = 0xbb67ae85; h[2] = 0x3c6ef372; h[3] = 0xa54ff53a;
@@ -59,15 +61,15 @@ KZ_DEV void sha256_compress(const uint32_t (&blk)[16], uint32_t (&h)[8]) {
       wi = w[i];
     } else {
       uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      uint32_t s0 = ror32(w15, 7) ^ ror32(w15, 18) ^ (w15 >> 3);
-      uint32_t s1 = ror32(w2, 17) ^ ror32(w2, 19) ^ (w2 >> 10);
+      uint32_t s0 = xor3(ror32(w15, 7), ror32(w15, 18), w15 >> 3);
+      uint32_t s1 = xor3(ror32(w2, 17), ror32(w2, 19), w2 >> 10);
       wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
       w[i & 15] = wi;
     }
-    uint32_t S1 = ror32(e, 6) ^ ror32(e, 11) ^ ror32(e, 25);
+    uint32_t S1 = xor3(ror32(e, 6), ror32(e, 11), ror32(e, 25));
     uint32_t ch = (e & f) ^ (~e & g);
     uint32_t t1 = hh + S1 + ch + kSha256K[i] + wi;
-    uint32_t S0 = ror32(a, 2) ^ ror32(a, 13) ^ ror32(a, 22);
+    uint32_t S0 = xor3(ror32(a, 2), ror32(a, 13), ror32(a, 22));
     uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
     uint32_t t2 = S0 + mj;
     hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
