@@ -390,6 +390,9 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
     if (flags & KZGMI_FLAG_COMPRESSED) {
       L::decompress_points(st, (const uint8_t*)dpi, (uint32_t)n, pts, inf, err);
       L::decompress_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err);
+    } else if (glv && pts29) {  // with phi(P) stored by the same pass (no k_endo_points29 over 2n points)
+      L::convert_points(st, (const uint8_t*)dpi, (uint32_t)n, pts, inf, err, true, pts + PH, inf + PH);
+      L::convert_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err, true, pts + PH + n, inf + PH + n);
     } else {
       L::convert_points(st, (const uint8_t*)dpi, (uint32_t)n, pts, inf, err, pts29);
       L::convert_points(st, (const uint8_t*)dC, (uint32_t)n, pts + n, inf + n, err, pts29);
@@ -398,7 +401,10 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
     // the SRS's [1]_1 as the last term of MSM#1: -t [1]_1
     HIPCHK(hipMemcpyAsync(pts + 2 * n, pts29 ? srs->g1_29() : srs->g1.p, sizeof(Affine<Cv>), hipMemcpyDeviceToDevice, st));
     HIPCHK(hipMemcpyAsync(inf + 2 * n, srs->g1.template as<uint8_t>() + sizeof(Affine<Cv>), 1, hipMemcpyDeviceToDevice, st));
-    if (glv) L::endo_points(st, pts, inf, (uint32_t)PH, pts + PH, inf + PH, pts29);
+    if (glv && pts29)  // the converts stored the 2n images: G1's alone
+      L::endo_points(st, pts + 2 * n, inf + 2 * n, 1, pts + PH + 2 * n, inf + PH + 2 * n, true);
+    else if (glv)
+      L::endo_points(st, pts, inf, (uint32_t)PH, pts + PH, inf + PH, pts29);
     mark(c, s, PH_CONVERT + 1);
     if (flags & KZGMI_FLAG_FIAT_SHAMIR) {  // r from the transcript of this (whole) batch
       const uint32_t* digests = nullptr;
@@ -856,8 +862,11 @@ int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t
   Affine<Cv>* pts = s.pts.template as<Affine<Cv>>();
   uint8_t* inf = s.inf.template as<uint8_t>();
   const bool pts29 = kAcc29<Cv>;
-  Launch<Cv>::convert_points(st, (const uint8_t*)dpts, (uint32_t)n, pts, inf, err, pts29);
-  if (glv) Launch<Cv>::endo_points(st, pts, inf, (uint32_t)n, pts + n, inf + n, pts29);
+  if (glv && pts29)  // phi(P) stored by the converting pass
+    Launch<Cv>::convert_points(st, (const uint8_t*)dpts, (uint32_t)n, pts, inf, err, true, pts + n, inf + n);
+  else
+    Launch<Cv>::convert_points(st, (const uint8_t*)dpts, (uint32_t)n, pts, inf, err, pts29);
+  if (glv && !pts29) Launch<Cv>::endo_points(st, pts, inf, (uint32_t)n, pts + n, inf + n, pts29);
   mark(c, s, PH_CONVERT + 1);
   uint32_t* sc = s.scal_s.template as<uint32_t>();
   Launch<Cv>::convert_scalars(st, (const uint8_t*)dsc, (uint32_t)n, sc, err);

@@ -48,10 +48,13 @@ KZ_DEV void fp_to_be_words(const Fp<P>& a, uint32_t (&w)[NW], int o) {
 // G1 encoding -> affine Montgomery point + infinity flag (errors into *err)
 // To29: the validated point is stored directly in the accumulation's radix-29
 // format (what k_pts_to29 would make of it), saving that kernel's pass over the points.
+// img != nullptr (To29, GLV batches): phi(P) = (beta x, y) is stored at img[i] too -- what
+// k_endo_points29 would compute from pts[i] after a second pass over the points.
 template <class Cv, bool To29 = false>
 __global__ void __launch_bounds__(256) k_convert_points(const uint8_t* __restrict__ bytes, uint32_t n,
                                                         Affine<Cv>* __restrict__ pts, uint8_t* __restrict__ inf,
-                                                        uint32_t* __restrict__ err) {
+                                                        uint32_t* __restrict__ err, Affine<Cv>* __restrict__ img = nullptr,
+                                                        uint8_t* __restrict__ img_inf = nullptr) {
   using P = typename Cv::FpP;
   constexpr int NW = 2 * P::N;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -93,6 +96,10 @@ __global__ void __launch_bounds__(256) k_convert_points(const uint8_t* __restric
       if (is_inf) x29 = y29 = F29<Q>::zero();
     }
     store_pt29<Cv>(pts + i, x29, y29);
+    if (img) {  // x29 < (p / R29 + 1) p; beta R29 likewise: the product stays below it (k_endo_points29)
+      store_pt29<Cv>(img + i, mul29(x29, fp_to29<Q>(Fp<P>::from_const(Cv::K::GLV_BETA_M))), y29);
+      img_inf[i] = is_inf ? 1 : 0;
+    }
   } else {
     Affine<Cv> a;
     if (is_inf) {

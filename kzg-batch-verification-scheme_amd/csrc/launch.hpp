@@ -30,7 +30,7 @@ struct Launch {
   // to29: store in the accumulation's radix-29 format, for
   // points that go straight into run_msm_core(..., pts29 = true)
   static void convert_points(hipStream_t st, const uint8_t* bytes, uint32_t n, AF* pts, uint8_t* inf, uint32_t* err,
-                             bool to29 = false);
+                             bool to29 = false, AF* img = nullptr, uint8_t* img_inf = nullptr);
   static void set_generator(hipStream_t st, AF* pt, uint8_t* inf);
   static void decompress_points(hipStream_t st, const uint8_t* bytes, uint32_t n, AF* pts, uint8_t* inf,
                                 uint32_t* err);

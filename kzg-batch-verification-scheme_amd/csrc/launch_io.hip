@@ -7,11 +7,11 @@ namespace kzgmi {
 
 template <class Cv>
 void Launch<Cv>::convert_points(hipStream_t st, const uint8_t* bytes, uint32_t n, AF* pts, uint8_t* inf, uint32_t* err,
-                                bool to29) {
+                                bool to29, AF* img, uint8_t* img_inf) {
   if (!n) return;
   if constexpr (kAcc29<Cv>) {
     if (to29) {
-      k_convert_points<Cv, true><<<grid_for(n, 256), 256, 0, st>>>(bytes, n, pts, inf, err);
+      k_convert_points<Cv, true><<<grid_for(n, 256), 256, 0, st>>>(bytes, n, pts, inf, err, img, img_inf);
       return;
     }
   }
@@ -131,7 +131,8 @@ void Launch<Cv>::sum_partials(hipStream_t st, const XY* parts, uint32_t nparts, 
 }
 
 using C_ = KZ_CURVE_T;
-template void Launch<C_>::convert_points(hipStream_t, const uint8_t*, uint32_t, Affine<C_>*, uint8_t*, uint32_t*, bool);
+template void Launch<C_>::convert_points(hipStream_t, const uint8_t*, uint32_t, Affine<C_>*, uint8_t*, uint32_t*, bool, Affine<C_>*,
+                                         uint8_t*);
 template void Launch<C_>::set_generator(hipStream_t, Affine<C_>*, uint8_t*);
 template void Launch<C_>::decompress_points(hipStream_t, const uint8_t*, uint32_t, Affine<C_>*, uint8_t*, uint32_t*);
 template void Launch<C_>::compress_points(hipStream_t, const uint8_t*, uint32_t, uint8_t*);
