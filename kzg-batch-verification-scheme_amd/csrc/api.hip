@@ -421,9 +421,9 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
     else
       L::scalar_prep(st, seed, (flags & KZGMI_FLAG_FIAT_SHAMIR) ? s.chal.template as<uint32_t>() : nullptr, offset, (const uint8_t*)dz, (const uint8_t*)dy, (uint32_t)n,
                      s.scal_r.template as<uint32_t>(), s.scal_s.template as<uint32_t>(), s.tpart.p,
-                     s.scal_t.template as<uint32_t>(), err);
-    if (glv) {
-      L::glv_split(st, s.scal_s.template as<uint32_t>(), 8, nn, gs, gs + 4 * (size_t)n);
+                     s.scal_t.template as<uint32_t>(), err, glv ? gs : nullptr, glv ? gs + 4 * (size_t)n : nullptr);
+    if (glv) {  // (s_i split by k_scalar_prep itself unless the powers form produced it)
+      if (powers) L::glv_split(st, s.scal_s.template as<uint32_t>(), 8, nn, gs, gs + 4 * (size_t)n);
       L::glv_split(st, s.scal_t.template as<uint32_t>(), 8, 1, gt, gt + 4);
       if (powers) L::glv_split(st, s.scal_r.template as<uint32_t>(), 8, nn, gr, gr + 4 * (size_t)n);
     }

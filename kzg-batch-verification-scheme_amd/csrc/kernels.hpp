@@ -187,6 +187,8 @@ __global__ void k_convert_g2(const uint8_t* __restrict__ bytes, uint32_t n, G2Af
 // r_i (127-bit, 4 words), s_i = r_i z_i mod r (8 words), per-block partial sum of r_i y_i.
 // seed_dev != null: the seed's 8 big-endian words are read from device memory (the
 // Fiat-Shamir challenge r computed on the GPU by k_fs_challenge) instead of `seed`.
+// h0 != null (GLV batches): s_i leaves as its GLV half scalars (h0[i], h1[i], k_glv_split's
+// output) instead of 8 words -- no second kernel reading s back.
 constexpr int PREP_BLOCK = 256;
 
 template <class Cv>
@@ -195,7 +197,8 @@ __global__ void __launch_bounds__(PREP_BLOCK) k_scalar_prep(Seed seed, const uin
                                                             const uint8_t* __restrict__ zs, const uint8_t* __restrict__ ys,
                                                             uint32_t n, uint32_t* __restrict__ r_out,
                                                             uint32_t* __restrict__ s_out, Fp<typename Cv::FrP>* __restrict__ tpart,
-                                                            uint32_t* __restrict__ err) {
+                                                            uint32_t* __restrict__ err, uint32_t* __restrict__ h0 = nullptr,
+                                                            uint32_t* __restrict__ h1 = nullptr) {
   using R = typename Cv::FrP;
   using F = Fp<R>;
   __shared__ F lds[PREP_BLOCK];
@@ -220,7 +223,16 @@ __global__ void __launch_bounds__(PREP_BLOCK) k_scalar_prep(Seed seed, const uin
     F s = fp_mul(rm, z);  // r z (standard form)
     acc = fp_mul(rm, y);  // r y (standard form)
     *reinterpret_cast<uint4*>(r_out + 4 * (size_t)i) = make_uint4(r4[0], r4[1], r4[2], r4[3]);
-    store_words(reinterpret_cast<uint8_t*>(s_out + 8 * (size_t)i), s.v);
+    if (h0) {
+      uint32_t k[8], a[4], b[4];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) k[j] = s.v[j];
+      glv_split<Cv>(k, a, b);
+      reinterpret_cast<uint4*>(h0)[i] = make_uint4(a[0], a[1], a[2], a[3]);
+      reinterpret_cast<uint4*>(h1)[i] = make_uint4(b[0], b[1], b[2], b[3]);
+    } else {
+      store_words(reinterpret_cast<uint8_t*>(s_out + 8 * (size_t)i), s.v);
+    }
   }
   lds[threadIdx.x] = acc;
   __syncthreads();

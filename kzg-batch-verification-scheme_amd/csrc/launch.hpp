@@ -47,7 +47,7 @@ struct Launch {
   static void scalar_prep(hipStream_t st, const Seed& seed, const uint32_t* seed_dev, uint64_t index_offset,
                           const uint8_t* zs,
                           const uint8_t* ys, uint32_t n, uint32_t* r_out, uint32_t* s_out, void* tpart,
-                          uint32_t* negt, uint32_t* err);
+                          uint32_t* negt, uint32_t* err, uint32_t* h0 = nullptr, uint32_t* h1 = nullptr);
   static size_t tpart_bytes(uint32_t n);
   // ---- Fiat-Shamir / powers-of-r randomisers (fs.hpp)
   static void fs_leaves(hipStream_t st, const uint8_t* dC, const uint8_t* dpi, const uint8_t* dz, const uint8_t* dy,

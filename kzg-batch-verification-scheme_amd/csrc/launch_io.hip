@@ -70,10 +70,11 @@ template <class Cv>
 void Launch<Cv>::scalar_prep(hipStream_t st, const Seed& seed, const uint32_t* seed_dev, uint64_t index_offset,
                              const uint8_t* zs,
                              const uint8_t* ys, uint32_t n, uint32_t* r_out, uint32_t* s_out, void* tpart,
-                             uint32_t* negt, uint32_t* err) {
+                             uint32_t* negt, uint32_t* err, uint32_t* h0, uint32_t* h1) {
   using FrF = Fp<typename Cv::FrP>;
   const uint32_t nblk = grid_for(n, PREP_BLOCK);
-  k_scalar_prep<Cv><<<nblk, PREP_BLOCK, 0, st>>>(seed, seed_dev, index_offset, zs, ys, n, r_out, s_out, (FrF*)tpart, err);
+  k_scalar_prep<Cv><<<nblk, PREP_BLOCK, 0, st>>>(seed, seed_dev, index_offset, zs, ys, n, r_out, s_out, (FrF*)tpart, err,
+                                                 h0, h1);
   k_tsum<Cv><<<1, 256, 0, st>>>((const FrF*)tpart, nblk, negt);
 }
 template <class Cv>
@@ -141,7 +142,7 @@ template void Launch<C_>::convert_scalars(hipStream_t, const uint8_t*, uint32_t,
 template void Launch<C_>::convert_g2(hipStream_t, const uint8_t*, uint32_t, G2Aff<C_>*, uint8_t*, uint32_t*);
 template size_t Launch<C_>::tpart_bytes(uint32_t);
 template void Launch<C_>::scalar_prep(hipStream_t, const Seed&, const uint32_t*, uint64_t, const uint8_t*, const uint8_t*, uint32_t,
-                                      uint32_t*, uint32_t*, void*, uint32_t*, uint32_t*);
+                                      uint32_t*, uint32_t*, void*, uint32_t*, uint32_t*, uint32_t*, uint32_t*);
 template void Launch<C_>::fs_leaves(hipStream_t, const uint8_t*, const uint8_t*, const uint8_t*, const uint8_t*,
                                      uint32_t, uint64_t, bool, uint32_t*);
 template const uint32_t* Launch<C_>::fs_reduce(hipStream_t, const uint32_t*, uint32_t, uint32_t, uint32_t*);
