@@ -229,8 +229,10 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   if (!pts) pts = s.pts.template as<Affine<Cv>>();  // default: the slot's converted points
   if (!inf) inf = s.inf.template as<uint8_t>();
   const uint32_t NB = nsets * NBUCKETS;
-  // accumulation threads: 64-entry chunks, at most acc_threads of them (then equal longer chunks)
-  size_t nchunks = (emax + ACC_CHUNK - 1) / ACC_CHUNK + 1;
+  // accumulation threads: 64-entry chunks (16 for small calls, msm.hpp ACC_CHUNK_SMALL), at most
+  // one resident round of them (then equal longer chunks)
+  const size_t chunk = emax <= ACC_SMALL_ENTRIES ? ACC_CHUNK_SMALL : ACC_CHUNK;
+  size_t nchunks = (emax + chunk - 1) / chunk + 1;
   const size_t cap = c->acc_threads_env ? c->acc_threads_env : (size_t)c->ncu * 4 * kAccWaves<Cv> * 64;
   if (cap && nchunks > cap) nchunks = cap;
   nchunks = (nchunks + 255) / 256 * 256;  // = the launched thread count (part arrays indexed by thread)

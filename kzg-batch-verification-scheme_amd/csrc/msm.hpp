@@ -25,7 +25,16 @@ namespace kzgmi {
 
 constexpr int WBITS = 16;                      // window width c
 constexpr int NBUCKETS = 1 << (WBITS - 1);     // signed digits: |d| in [1, 2^15]
-constexpr int ACC_CHUNK = 64;                  // entries per accumulation thread
+// Accumulation chunk (entries per thread) the host sizes the grid for (run_msm_core): ACC_CHUNK,
+// or ACC_CHUNK_SMALL for calls of at most ACC_SMALL_ENTRIES entries.  The grid is capped at one
+// resident round (CUs x 4 SIMDs x 4 waves), so from n ~ 2^18 on every chunk is longer anyway.
+// Below that, shorter chunks mean more waves and shorter chains (a 256-tuple batch: 128 threads
+// of 64 sequential additions, 0.43 ms, vs 768 of 12, 0.15 ms) but more flushed pieces: at 2^17
+// the pipelined rate was 869/s with 64-entry chunks, 850 with 16 and 830 with 8
+// (profiles/r03/misc_ab_r03.txt) -- so only small calls take the short chunks.
+constexpr int ACC_CHUNK = 64;
+constexpr int ACC_CHUNK_SMALL = 16;
+constexpr size_t ACC_SMALL_ENTRIES = size_t(1) << 20;
 constexpr int SEG = 16;                        // buckets per reduction segment
 constexpr int MAX_CLASSES = 16;
 
@@ -560,14 +569,14 @@ KZ_DEV Xyzz<Cv> load_xyzz(const Xyzz<Cv>* src) {
 
 // ------------------------------------------------------------------------------ accumulation
 // Chunk length: every accumulation thread owns `len` consecutive sorted entries, len =
-// max(ACC_CHUNK, ceil(total / nthreads)) rounded up to a multiple of 4 (chunks start on 16-B
-// boundaries: the radix-29 loop reads its values 4 at a time) for the launched thread count
-// nthreads (the same value in k_accumulate and k_fixup).  nthreads >= total / ACC_CHUNK gives
-// the fixed 64-entry chunks; a smaller grid gives longer, equal chunks (fewer pieces, no
+// ceil(total / nthreads) rounded up to a multiple of 4 (chunks start on 16-B boundaries: the
+// radix-29 loop reads its values 4 at a time) for the launched thread count nthreads (the same
+// value in k_accumulate and k_fixup).  The host picks nthreads ~ (entry bound) / ACC_CHUNK(_SMALL),
+// capped at one resident round: the capped grid gives longer, equal chunks (fewer pieces, no
 // partial last round).
 KZ_DEV uint32_t acc_chunk_len(uint32_t total, uint32_t nthreads) {
   const uint32_t per = ((total + nthreads - 1) / nthreads + 3) & ~3u;
-  return per > (uint32_t)ACC_CHUNK ? per : (uint32_t)ACC_CHUNK;
+  return per > 4u ? per : 4u;
 }
 
 template <class Cv>
