@@ -1232,8 +1232,9 @@ int kzgmi_g1_validate_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_poin
   });
 }
 
-int kzgmi_fs_chunk_digests_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dC, const void* dz, const void* dy,
-                                  const void* dpi, size_t n, uint64_t index_offset, uint32_t flags, void* d_out) {
+// the chunk digests of kzgmi_fs_chunk_digests_device, enqueued on slot 0's stream (no wait)
+static int fs_chunk_digests_enqueue(kzgmi_ctx* c, kzgmi_curve curve, const void* dC, const void* dz, const void* dy,
+                                    const void* dpi, size_t n, uint64_t index_offset, uint32_t flags, void* d_out) {
   CHK(check_ctx(c));
   if (!d_out || (n && (!dC || !dz || !dy || !dpi)) || n == 0) return fail(KZGMI_ERR_ARG, "bad argument");
   if (index_offset % FS_CHUNK) return fail(KZGMI_ERR_ARG, "index_offset must be a multiple of 4096");
@@ -1247,9 +1248,15 @@ int kzgmi_fs_chunk_digests_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d
     const size_t nch = (n + FS_CHUNK - 1) / FS_CHUNK;
     HIPCHK(hipMemcpyAsync(d_out, dg, nch * 32, hipMemcpyDeviceToDevice, s.stream));
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(s.stream));
     return 0;
   });
+}
+
+int kzgmi_fs_chunk_digests_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dC, const void* dz, const void* dy,
+                                  const void* dpi, size_t n, uint64_t index_offset, uint32_t flags, void* d_out) {
+  CHK(fs_chunk_digests_enqueue(c, curve, dC, dz, dy, dpi, n, index_offset, flags, d_out));
+  HIPCHK(hipStreamSynchronize(c->slots[0].stream));
+  return 0;
 }
 
 int kzgmi_fs_challenge_from_digests_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_digests, size_t nchunks,
@@ -1709,7 +1716,9 @@ int batch_multi(kzgmi_ctx* c, const kzgmi_srs* srs, const void* const* dC, const
     }
     const size_t nch_tot = (ntot + FS_CHUNK - 1) / FS_CHUNK;
     CHK(c->mdig_all.ensure(nch_tot * 32));
-    size_t at = 0;
+    // every device hashes its subtrees concurrently (enqueued first), then each device's
+    // digests are waited for and copied to the primary, ordered before the challenge derivation
+    // on the primary's slot-0 stream
     for (int d = 0; d < D; ++d) {
       if (!nd[d]) continue;
       if (off[d] % FS_CHUNK) return fail(KZGMI_ERR_ARG, "Fiat-Shamir shards must start at multiples of 4096 tuples");
@@ -1717,10 +1726,16 @@ int batch_multi(kzgmi_ctx* c, const kzgmi_srs* srs, const void* const* dC, const
       const size_t nch = (nd[d] + FS_CHUNK - 1) / FS_CHUNK;
       CHK(set_dev(p));
       CHK(p->mdig.ensure(nch * 32));
-      CHK(kzgmi_fs_chunk_digests_device(p, curve, dC[d], dz[d], dy[d], dpi[d], nd[d], off[d],
-                                        flags & KZGMI_FLAG_COMPRESSED, p->mdig.p));
-      // kzgmi_fs_chunk_digests_device returned with p's digests complete; the copy is ordered
-      // before the challenge derivation on the primary's slot-0 stream
+      CHK(fs_chunk_digests_enqueue(p, curve, dC[d], dz[d], dy[d], dpi[d], nd[d], off[d],
+                                   flags & KZGMI_FLAG_COMPRESSED, p->mdig.p));
+    }
+    size_t at = 0;
+    for (int d = 0; d < D; ++d) {
+      if (!nd[d]) continue;
+      kzgmi_ctx* p = dev_ctx(c, d);
+      const size_t nch = (nd[d] + FS_CHUNK - 1) / FS_CHUNK;
+      CHK(set_dev(p));
+      HIPCHK(hipStreamSynchronize(p->slots[0].stream));
       CHK(set_dev(c));
       HIPCHK(hipMemcpyPeerAsync((uint8_t*)c->mdig_all.p + at * 32, c->device, p->mdig.p, p->device, nch * 32,
                                 c->slots[0].stream));
