@@ -178,7 +178,8 @@ def test_msm_reduction_special_cases(ctx, curve):
     """Adjacent buckets whose sums cancel or coincide, so that the bucket-sum reduction's running
     sums hit P + (-P) = O and P + P (the doubling branch of its general addition):
     digits 8, 7, 6, 5 on P, -P, P, P (buckets 7..4 of the first segment half) = 12 P, plus the
-    same pattern repeated in a high window and a lone top-bucket digit (acc + run = 2 run)."""
+    same pattern repeated in a high window and a lone top-bucket digit (acc + run = 2 run), and
+    digits in the upper halves of segments (the V records)."""
     C = pc.CURVES[curve]
     rng = random.Random(83)
     k = rng.randrange(1, C.r)
@@ -191,6 +192,13 @@ def test_msm_reduction_special_cases(ctx, curve):
         ([P], [8]),
         ([P, P], [8, 7]),
         ([P, nP], [16, 15]),
+        # upper segment halves (buckets 8..15): their sums leave k_reduce_segments as V records,
+        # scaled by 8 once per set in k_reduce_bits_finish
+        ([P], [9]),
+        ([P, P], [9, 1]),
+        ([P, P, nP, P], [16, 12, 11, 9]),
+        ([P, nP, P, P, P], [24, 23, 9, 17, 32]),
+        ([P, P, P], [16 << 16, 9 << 16, 8 << 16]),
     ]
     for pts, sc in cases:
         pb = b"".join(pts)
