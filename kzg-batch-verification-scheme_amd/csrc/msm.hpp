@@ -132,21 +132,12 @@ KZ_DEV TileRef tile_decode(const TermList& tl, uint32_t t) {
   return {k, (int)(t / chunks), t % chunks};
 }
 
-// All signed digits of every term, once: one thread per term reads its scalar once and walks
-// the carry chain over its windows (the count and scatter passes used to recompute the chain
-// from the scalar for every window: nwin scalar reads per term per pass).  Code = 0 for a zero
-// digit or a point at infinity, else |d| | (entry sign << 31) with entry sign = (d < 0) xor the
-// half-scalar's sign flag.
-static __global__ void __launch_bounds__(256) k_digits(TermList tl, const uint8_t* __restrict__ inf,
-                                                uint32_t* __restrict__ digits) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  int k = 0;
-  for (; k < (int)tl.nclass; ++k) {
-    if (i < tl.c[k].count) break;
-    i -= tl.c[k].count;
-  }
-  if (k >= (int)tl.nclass) return;
-  const TermClass& C = tl.c[k];
+// The signed window digits of term i of class C: the scalar read once, the carry chain walked
+// over its windows; emit(local window, code) for windows win_off .. win_off + nwin - 1.  Code = 0
+// for a zero digit or a point at infinity, else |d| | (entry sign << 31) with entry sign =
+// (d < 0) xor the half-scalar's sign flag.
+template <class Emit>
+KZ_DEV void term_digits(const TermClass& C, uint32_t i, const uint8_t* __restrict__ inf, Emit&& emit) {
   const uint32_t* sp = C.scal + (size_t)i * C.scal_stride;
   uint32_t w8[8];
   bool neg = false;
@@ -173,9 +164,25 @@ static __global__ void __launch_bounds__(256) k_digits(TermList tl, const uint8_
     if (w >= w0) {
       uint32_t code = 0;
       if (d != 0 && !is_inf) code = (uint32_t)(d < 0 ? -d : d) | ((d < 0) != neg ? 0x80000000u : 0u);
-      digits[C.dig_base + (size_t)(w - w0) * C.count + i] = code;
+      emit(w - w0, code);
     }
   }
+}
+
+// All signed digits of every term, once: one thread per term (the count and scatter passes used
+// to recompute the chain from the scalar for every window: nwin scalar reads per term per pass).
+// A/B reference of k_digits_count (KZ_SORT_SEPARATE_COUNT).
+static __global__ void __launch_bounds__(256) k_digits(TermList tl, const uint8_t* __restrict__ inf,
+                                                uint32_t* __restrict__ digits) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  int k = 0;
+  for (; k < (int)tl.nclass; ++k) {
+    if (i < tl.c[k].count) break;
+    i -= tl.c[k].count;
+  }
+  if (k >= (int)tl.nclass) return;
+  const TermClass& C = tl.c[k];
+  term_digits(C, i, inf, [&](int w, uint32_t code) { digits[C.dig_base + (size_t)w * C.count + i] = code; });
 }
 
 // k_digits and k_bin_count in one pass: workgroup = 4096 terms of one class (16 per thread),
@@ -200,7 +207,6 @@ static __global__ void __launch_bounds__(256) k_digits_count(TermList tl, const 
   }
   const TermClass& C = tl.c[k];
   const uint32_t t = threadIdx.x;
-  const int w0 = (int)C.win_off, w1 = (int)(C.win_off + C.nwin);
 #pragma unroll
   for (int w = 0; w < 16; ++w) hist[w][t] = 0;
   __syncthreads();
@@ -208,38 +214,10 @@ static __global__ void __launch_bounds__(256) k_digits_count(TermList tl, const 
   for (int j = 0; j < TILE_TERMS / 256; ++j) {
     const uint32_t i = b * TILE_TERMS + j * 256 + t;
     if (i >= C.count) break;
-    const uint32_t* sp = C.scal + (size_t)i * C.scal_stride;
-    uint32_t w8[8];
-    bool neg = false;
-    if (C.scal_words == 4) {
-      const uint4 q = *reinterpret_cast<const uint4*>(sp);
-      neg = (q.w >> 31) != 0;
-      w8[0] = q.x; w8[1] = q.y; w8[2] = q.z; w8[3] = q.w & 0x7fffffffu;
-      w8[4] = w8[5] = w8[6] = w8[7] = 0;
-    } else {
-      const uint4 q0 = *reinterpret_cast<const uint4*>(sp);
-      const uint4 q1 = *reinterpret_cast<const uint4*>(sp + 4);
-      w8[0] = q0.x; w8[1] = q0.y; w8[2] = q0.z; w8[3] = q0.w;
-      w8[4] = q1.x; w8[5] = q1.y; w8[6] = q1.z; w8[7] = q1.w;
-    }
-    const bool is_inf = inf[C.pt_base + i] != 0;
-    uint32_t carry = 0;
-#pragma unroll
-    for (int w = 0; w < 16; ++w) {
-      if (w >= w1) break;
-      const uint32_t raw = (w8[w >> 1] >> ((w & 1) * 16)) & 0xffffu;
-      int d = (int)(raw + carry);
-      if (d > NBUCKETS) { d -= (1 << WBITS); carry = 1; } else { carry = 0; }
-      if (w >= w0) {
-        uint32_t code = 0;
-        if (d != 0 && !is_inf) {
-          const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-          code = mag | ((d < 0) != neg ? 0x80000000u : 0u);
-          atomicAdd(&hist[w - w0][(mag - 1) >> COARSE_SHIFT], 1u);
-        }
-        digits[C.dig_base + (size_t)(w - w0) * C.count + i] = code;
-      }
-    }
+    term_digits(C, i, inf, [&](int w, uint32_t code) {
+      if (code) atomicAdd(&hist[w][((code & 0x7fffffffu) - 1) >> COARSE_SHIFT], 1u);
+      digits[C.dig_base + (size_t)w * C.count + i] = code;
+    });
   }
   __syncthreads();
   for (int w = 0; w < (int)C.nwin; ++w) {
