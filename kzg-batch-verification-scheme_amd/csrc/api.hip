@@ -119,6 +119,7 @@ struct kzgmi_ctx {
   int ncu = 0;                // compute units: the accumulation grid cap (kAccWaves, msm.hpp)
   size_t acc_threads_env = 0;  // KZGMI_ACC_THREADS override of that cap (0 = none)
   bool sort_split = false;     // KZGMI_SORT_SPLIT: split coarse-pass entries at every size (tests)
+  int wbits_env = 0;           // KZGMI_WBITS: 13 or 16 forces the window width (tests, A/B)
   double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
   int phase_calls = 0;
   DevBuf table[2], table_base[2];
@@ -212,7 +213,10 @@ int map_device_err(uint32_t e) {
 template <class Cv>
 int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, size_t emax, const MsmWindows& mw,
                  const Affine<Cv>* pts = nullptr, const uint8_t* inf = nullptr, bool pts29 = false,
-                 bool dry = false) {
+                 bool dry = false, int wbits = WBITS) {
+  const uint32_t nbuckets = wbits == 13 ? Win<13>::NBUCKETS : Win<WBITS>::NBUCKETS;
+  const uint32_t bins = wbits == 13 ? Win<13>::BINS : Win<WBITS>::BINS;
+  const uint32_t rb_parts = wbits == 13 ? Win<13>::RB_PARTS : Win<WBITS>::RB_PARTS;
   // pts == nullptr: the slot's freshly converted points, put into the accumulation's format
   // here unless convert_points stored them in it already (pts29); explicit pts (commit-key
   // rows) are stored in that format already (kzgmi_ck_load)
@@ -228,7 +232,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   using XY = Xyzz<Cv>;
   if (!pts) pts = s.pts.template as<Affine<Cv>>();  // default: the slot's converted points
   if (!inf) inf = s.inf.template as<uint8_t>();
-  const uint32_t NB = nsets * NBUCKETS;
+  const uint32_t NB = nsets * nbuckets;
   // accumulation threads: 64-entry chunks (16 for small calls, msm.hpp ACC_CHUNK_SMALL), at most
   // one resident round of them (then equal longer chunks)
   const size_t chunk = emax <= ACC_SMALL_ENTRIES ? ACC_CHUNK_SMALL : ACC_CHUNK;
@@ -238,7 +242,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   nchunks = (nchunks + 255) / 256 * 256;  // = the launched thread count (part arrays indexed by thread)
   CHK(s.cnt.ensure((size_t)NB * 4));
   CHK(s.off.ensure((size_t)NB * 4));
-  CHK(s.coarse.ensure((size_t)3 * nsets * BINS_PER_SET * 4));
+  CHK(s.coarse.ensure((size_t)3 * nsets * bins * 4));
   CHK(s.ent.ensure(emax * 8));
   CHK(s.total.ensure(16));
   CHK(s.sval.ensure(emax * 4 + 16));  // + 16: k_accumulate reads values 4 at a time, up to 3 past the end
@@ -253,7 +257,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   const size_t seg_rec = std::max(sizeof(XY), (size_t)W29 * 4);  // 32-bit XYZZ or a radix-29 record
   CHK(s.R.ensure((size_t)NB / SEG * seg_rec));
   CHK(s.U.ensure((size_t)NB / SEG * seg_rec * (kSegV ? 2 : 1)));  // U records, then the V records
-  CHK(s.scratch.ensure((size_t)nsets * RB_PARTS * sizeof(XY)));  // k_reduce_bits partial sums
+  CHK(s.scratch.ensure((size_t)nsets * rb_parts * sizeof(XY)));  // k_reduce_bits partial sums
   CHK(s.winsum.ensure((size_t)nsets * sizeof(XY)));
   CHK(s.res.ensure(2 * sizeof(XY)));
   if (dry) return 0;  // kzgmi_ctx_reserve: workspace sized, nothing enqueued
@@ -268,7 +272,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   }
   L::sort(st, tl, nsets, inf, s.digits.template as<uint32_t>(), s.coarse.template as<uint32_t>(), s.ent.template as<uint64_t>(), emax, c->sort_split,
           s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.total.template as<uint32_t>(),
-          s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>());
+          s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(), wbits);
   mark(c, s, PH_SORT + 1);
   L::accumulate(st, nchunks, s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
                 s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts,
@@ -277,9 +281,9 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   mark(c, s, PH_ACCUM + 1);
   L::reduce(st, nsets, s.cnt.template as<uint32_t>(), s.buckets.template as<XY>(), s.acc29.template as<uint32_t>(),
             s.R.template as<XY>(),
-            s.U.template as<XY>(), s.scratch.template as<XY>(), s.winsum.template as<XY>());
+            s.U.template as<XY>(), s.scratch.template as<XY>(), s.winsum.template as<XY>(), wbits);
   mark(c, s, PH_REDUCE + 1);
-  L::window_combine(st, mw, s.winsum.template as<XY>(), s.res.template as<XY>());
+  L::window_combine(st, mw, s.winsum.template as<XY>(), s.res.template as<XY>(), wbits);
   mark(c, s, PH_COMBINE + 1);
   HIPCHK(hipGetLastError());
   return 0;
@@ -340,6 +344,24 @@ int reserve_fs(Slot& s, size_t n) {
   CHK(s.chal.ensure(32));
   return 0;
 }
+
+// Window width of a call from its entry count at c = 16 (msm.hpp Win): c = 13 for mid-size calls,
+// 2^20 < entries <= max13 (batches: 2^15 < n <= 2^17, max13 = 2^22; MSMs: 2^16 < n <= 2^17,
+// max13 = 2^21) -- 8x fewer buckets for 5/4 the terms, where the bucket-sum reduction is a large
+// share of the pipelined work (2^17-tuple batches 875 -> 1024/s, 2^17-point MSMs 193 -> 224 M
+// pts/s; profiles/r03/misc_ab_r03.txt).  Not for larger calls (a 2^18-point MSM: 270 -> 242)
+// nor tiny ones, whose latency it raises: the top window of a 10 x 13-bit split of a 128-bit
+// magnitude holds 11 bits (of a 20 x 13 split of 256 bits, 9), so its terms crowd into a few
+// hundred buckets whose pieces k_fixup joins serially (n = 256: 3.0 -> 3.3 ms).  At 14 bits the
+// top windows keep 2 and 4 bits: a 2^17 batch took 19 ms.  KZGMI_WBITS=13/16 forces one.
+int call_wbits(const kzgmi_ctx* c, size_t entries16, size_t max13) {
+  if (c->wbits_env == 13 || c->wbits_env == WBITS) return c->wbits_env;
+  return entries16 > (size_t(1) << 20) && entries16 <= max13 ? 13 : WBITS;
+}
+// windows of a 127-bit magnitude (randomisers, GLV halves) and of a full 255-bit scalar at width c
+// (signed digits: the top window takes the last carry)
+inline uint32_t windows_half(int wb) { return (uint32_t)((128 + wb - 1) / wb); }
+inline uint32_t windows_full(int wb) { return (uint32_t)((256 + wb - 1) / wb); }
 
 // ------------------------------------------------------------------------------ batch
 template <class Cv>
@@ -435,45 +457,49 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   if (!dry) CHK(front());
   TermList tl{};
   const uint32_t ph = (uint32_t)PH;
-  if (glv) {  // every MSM in 8 windows of half scalars: sets 0..7 (MSM#0), 8..15 (MSM#1)
+  // c = 16: H = 8 windows for 127-bit magnitudes, F = 16 for full scalars; c = 13: 10 and 20
+  const int wb = call_wbits(c, (size_t)(powers ? 48 : 32) * n, size_t(1) << 22);
+  const uint32_t H = windows_half(wb), F = windows_full(wb);
+  if (glv) {  // every MSM in H windows of half scalars: sets 0..H-1 (MSM#0), H..2H-1 (MSM#1)
     const uint32_t* rr = s.scal_r.template as<uint32_t>();
     uint32_t k = 0;
     if (!powers) {
-      tl.c[k++] = {nn, 0, 4, 8, 0, 4, rr};                     // MSM#0: r_i pi_i
-      tl.c[k++] = {nn, nn, 4, 8, 8, 4, rr};                    // MSM#1: r_i C_i
+      tl.c[k++] = {nn, 0, 4, H, 0, 4, rr};                     // MSM#0: r_i pi_i
+      tl.c[k++] = {nn, nn, 4, H, H, 4, rr};                    // MSM#1: r_i C_i
     } else {
-      tl.c[k++] = {nn, 0, 4, 8, 0, 4, gr};                     // MSM#0: r_i pi_i = h0 pi + h1 phi(pi)
-      tl.c[k++] = {nn, ph, 4, 8, 0, 4, gr + 4 * (size_t)n};
-      tl.c[k++] = {nn, nn, 4, 8, 8, 4, gr};                    // MSM#1: r_i C_i
-      tl.c[k++] = {nn, ph + nn, 4, 8, 8, 4, gr + 4 * (size_t)n};
+      tl.c[k++] = {nn, 0, 4, H, 0, 4, gr};                     // MSM#0: r_i pi_i = h0 pi + h1 phi(pi)
+      tl.c[k++] = {nn, ph, 4, H, 0, 4, gr + 4 * (size_t)n};
+      tl.c[k++] = {nn, nn, 4, H, H, 4, gr};                    // MSM#1: r_i C_i
+      tl.c[k++] = {nn, ph + nn, 4, H, H, 4, gr + 4 * (size_t)n};
     }
-    tl.c[k++] = {nn, 0, 4, 8, 8, 4, gs};                       //        s_i pi_i
-    tl.c[k++] = {nn, ph, 4, 8, 8, 4, gs + 4 * (size_t)n};
-    tl.c[k++] = {1, 2 * nn, 4, 8, 8, 0, gt};                   //        -t G1
-    tl.c[k++] = {1, ph + 2 * nn, 4, 8, 8, 0, gt + 4};
+    tl.c[k++] = {nn, 0, 4, H, H, 4, gs};                       //        s_i pi_i
+    tl.c[k++] = {nn, ph, 4, H, H, 4, gs + 4 * (size_t)n};
+    tl.c[k++] = {1, 2 * nn, 4, H, H, 0, gt};                   //        -t G1
+    tl.c[k++] = {1, ph + 2 * nn, 4, H, H, 0, gt + 4};
     tl.nclass = k;
     tl.total = 0;
     for (uint32_t j = 0; j < k; ++j) tl.total += tl.c[j].count;
-    const MsmWindows mw{2, {0, 8}, {8, 8}};
-    CHK(run_msm_core<Cv>(c, s, tl, 16, (size_t)(powers ? 48 : 32) * n + 16, mw, nullptr, nullptr, pts29, dry));
-  } else if (!powers) {  // 127-bit r_i: MSM#0 in 8 windows (sets 0..7), MSM#1 in 16 (sets 8..23)
-    tl.c[0] = {nn, 0, 4, 8, 0, 4, s.scal_r.template as<uint32_t>()};          // MSM#0: r_i pi_i
-    tl.c[1] = {nn, nn, 4, 8, 8, 4, s.scal_r.template as<uint32_t>()};         // MSM#1: r_i C_i
-    tl.c[2] = {nn, 0, 8, 16, 8, 8, s.scal_s.template as<uint32_t>()};         //        s_i pi_i
-    tl.c[3] = {1, 2 * nn, 8, 16, 8, 0, s.scal_t.template as<uint32_t>()};     //        -t G1
+    const MsmWindows mw{2, {0, H}, {H, H}};
+    CHK(run_msm_core<Cv>(c, s, tl, 2 * H, (size_t)(powers ? 6 : 4) * H * n + 2 * H + 16, mw, nullptr, nullptr,
+                         pts29, dry, wb));
+  } else if (!powers) {  // 127-bit r_i: MSM#0 in H windows (sets 0..H-1), MSM#1 in F (sets H..H+F-1)
+    tl.c[0] = {nn, 0, 4, H, 0, 4, s.scal_r.template as<uint32_t>()};          // MSM#0: r_i pi_i
+    tl.c[1] = {nn, nn, 4, H, H, 4, s.scal_r.template as<uint32_t>()};         // MSM#1: r_i C_i
+    tl.c[2] = {nn, 0, 8, F, H, 8, s.scal_s.template as<uint32_t>()};          //        s_i pi_i
+    tl.c[3] = {1, 2 * nn, 8, F, H, 0, s.scal_t.template as<uint32_t>()};      //        -t G1
   }
-  if (!glv && powers) {  // r_i = r^i, full Fr: both MSMs in 16 windows (sets 0..15, 16..31)
-    tl.c[0] = {nn, 0, 8, 16, 0, 8, s.scal_r.template as<uint32_t>()};
-    tl.c[1] = {nn, nn, 8, 16, 16, 8, s.scal_r.template as<uint32_t>()};
-    tl.c[2] = {nn, 0, 8, 16, 16, 8, s.scal_s.template as<uint32_t>()};
-    tl.c[3] = {1, 2 * nn, 8, 16, 16, 0, s.scal_t.template as<uint32_t>()};
+  if (!glv && powers) {  // r_i = r^i, full Fr: both MSMs in F windows (sets 0..F-1, F..2F-1)
+    tl.c[0] = {nn, 0, 8, F, 0, 8, s.scal_r.template as<uint32_t>()};
+    tl.c[1] = {nn, nn, 8, F, F, 8, s.scal_r.template as<uint32_t>()};
+    tl.c[2] = {nn, 0, 8, F, F, 8, s.scal_s.template as<uint32_t>()};
+    tl.c[3] = {1, 2 * nn, 8, F, F, 0, s.scal_t.template as<uint32_t>()};
   }
   if (!glv) {
     tl.nclass = 4;
     tl.total = 3 * nn + 1;
-    const MsmWindows mw = powers ? MsmWindows{2, {0, 16}, {16, 16}} : MsmWindows{2, {0, 8}, {8, 16}};
-    CHK(run_msm_core<Cv>(c, s, tl, powers ? 32 : 24, (size_t)(powers ? 48 : 32) * n + 16, mw, nullptr, nullptr, pts29,
-                         dry));
+    const MsmWindows mw = powers ? MsmWindows{2, {0, F}, {F, F}} : MsmWindows{2, {0, H}, {H, F}};
+    CHK(run_msm_core<Cv>(c, s, tl, powers ? 2 * F : H + F, (size_t)(powers ? 3 * F : 2 * H + F) * n + F + 16, mw,
+                         nullptr, nullptr, pts29, dry, wb));
   }
   if (dry) return 0;
   Roctx rx("kzgmi.batch.pairing");
@@ -571,6 +597,7 @@ int kzgmi_ctx_create(kzgmi_ctx** out, int device_id, int pipeline_slots) {
     c->ncu = ncu;
   if (const char* e = getenv("KZGMI_ACC_THREADS")) c->acc_threads_env = (size_t)strtoull(e, nullptr, 10);
   if (const char* e = getenv("KZGMI_SORT_SPLIT")) c->sort_split = atoi(e) != 0;
+  if (const char* e = getenv("KZGMI_WBITS")) c->wbits_env = atoi(e);
   c->slots.resize(pipeline_slots);
   for (auto& s : c->slots) {
     if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
@@ -877,19 +904,21 @@ int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t
   mark(c, s, PH_SCALARS + 1);
   TermList tl{};
   const uint32_t nn = (uint32_t)n;
-  if (glv) {  // sum k_i P_i = sum h0_i P_i + h1_i phi(P_i): 8 windows, 8 bucket sets
-    tl.c[0] = {nn, 0, 4, 8, 0, 4, gs};
-    tl.c[1] = {nn, nn, 4, 8, 0, 4, gs + 4 * n};
+  const int wb = call_wbits(c, (size_t)16 * n, size_t(1) << 21);
+  const uint32_t H = windows_half(wb), F = windows_full(wb);
+  if (glv) {  // sum k_i P_i = sum h0_i P_i + h1_i phi(P_i): H windows, H bucket sets
+    tl.c[0] = {nn, 0, 4, H, 0, 4, gs};
+    tl.c[1] = {nn, nn, 4, H, 0, 4, gs + 4 * n};
     tl.nclass = 2;
     tl.total = 2 * nn;
-    const MsmWindows mw{1, {0, 0}, {8, 0}};
-    CHK(run_msm_core<Cv>(c, s, tl, 8, (size_t)16 * n + 16, mw, nullptr, nullptr, pts29));
+    const MsmWindows mw{1, {0, 0}, {H, 0}};
+    CHK(run_msm_core<Cv>(c, s, tl, H, (size_t)2 * H * n + 16, mw, nullptr, nullptr, pts29, false, wb));
   } else {
-    tl.c[0] = {nn, 0, 8, 16, 0, 8, sc};
+    tl.c[0] = {nn, 0, 8, F, 0, 8, sc};
     tl.nclass = 1;
     tl.total = nn;
-    const MsmWindows mw{1, {0, 0}, {16, 0}};
-    CHK(run_msm_core<Cv>(c, s, tl, 16, (size_t)16 * n + 16, mw, nullptr, nullptr, pts29));
+    const MsmWindows mw{1, {0, 0}, {F, 0}};
+    CHK(run_msm_core<Cv>(c, s, tl, F, (size_t)F * n + 16, mw, nullptr, nullptr, pts29, false, wb));
   }
   s.curve = Cv::ID;
   return 0;

@@ -15,7 +15,7 @@ struct Launch {
   // (counts, offsets, cursors), ent: emax x 8 B (coarse-pass entries: msm.hpp EntPacked / EntSplit)
   static void sort(hipStream_t st, const TermList& tl, uint32_t nsets, const uint8_t* inf, uint32_t* digits,
                    uint32_t* coarse, uint64_t* ent, size_t emax, bool force_split, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
-                   uint32_t* skey);
+                   uint32_t* skey, int wbits = WBITS);
   // both curves accumulate in radix 2^29: pts in that format (convert_points(to29) or
   // pts_to29), acc29 = (nb + 2 x launched threads) records of W29 words that stay the bucket
   // store (k_fixup joins pieces into them; reduce reads them); BN254 uses buckets/pfirst/plast
@@ -24,8 +24,8 @@ struct Launch {
                          XY* pfirst, XY* plast, uint32_t* acc29, uint32_t nb);
   static void pts_to29(hipStream_t st, AF* pts, uint32_t n);  // in place
   static void reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const XY* buckets, const uint32_t* acc29,
-                     XY* R, XY* U, XY* scratch, XY* winsum);
-  static void window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res);
+                     XY* R, XY* U, XY* scratch, XY* winsum, int wbits = WBITS);
+  static void window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res, int wbits = WBITS);
   // ---- I/O and scalars (launch_io.hip)
   // to29: store in the accumulation's radix-29 format, for
   // points that go straight into run_msm_core(..., pts29 = true)

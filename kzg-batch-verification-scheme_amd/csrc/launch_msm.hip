@@ -3,37 +3,51 @@
 
 namespace kzgmi {
 
+// the window widths a call may use (msm.hpp Win): c = 16, and c = 13 for small calls
+template <class F>
+void with_wbits(int wbits, F&& f) {
+  if (wbits == 13) f(std::integral_constant<int, 13>{});
+  else f(std::integral_constant<int, WBITS>{});
+}
+
 template <class Cv>
 void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const uint8_t* inf, uint32_t* digits,
                       uint32_t* coarse, uint64_t* ent, size_t emax, bool force_split, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
-                      uint32_t* skey) {
-  const uint32_t nbins = nsets * BINS_PER_SET;
-  uint32_t* ccnt = coarse;
-  uint32_t* coff = coarse + nbins;
-  uint32_t* ccur = coarse + 2 * nbins;
-  (void)hipMemsetAsync(ccnt, 0, (size_t)nbins * 4, st);
-  const uint32_t tiles = num_tiles_host(tl);
+                      uint32_t* skey, int wbits) {
+  with_wbits(wbits, [&](auto wb) {
+    constexpr int WB = decltype(wb)::value;
+    const uint32_t nbins = nsets * Win<WB>::BINS;
+    uint32_t* ccnt = coarse;
+    uint32_t* coff = coarse + nbins;
+    uint32_t* ccur = coarse + 2 * nbins;
+    (void)hipMemsetAsync(ccnt, 0, (size_t)nbins * 4, st);
+    const uint32_t tiles = num_tiles_host(tl);
 #ifdef KZ_SORT_SEPARATE_COUNT
-  if (tl.total) k_digits<<<grid_for(tl.total, 256), 256, 0, st>>>(tl, inf, digits);
-  if (tiles) k_bin_count<<<tiles, 256, 0, st>>>(tl, digits, ccnt);
+    if constexpr (WB == WBITS) {
+      if (tl.total) k_digits<<<grid_for(tl.total, 256), 256, 0, st>>>(tl, inf, digits);
+      if (tiles) k_bin_count<<<tiles, 256, 0, st>>>(tl, digits, ccnt);
+    } else {
+      if (tl.total) k_digits_count<WB><<<num_digit_groups_host(tl), 256, 0, st>>>(tl, inf, digits, ccnt);
+    }
 #else
-  if (tl.total) k_digits_count<<<num_digit_groups_host(tl), 256, 0, st>>>(tl, inf, digits, ccnt);
+    if (tl.total) k_digits_count<WB><<<num_digit_groups_host(tl), 256, 0, st>>>(tl, inf, digits, ccnt);
 #endif
-  k_bin_scan<<<1, 1024, 0, st>>>(ccnt, nbins, coff, ccur, total);
-  // coarse-pass entries (msm.hpp EntPacked / EntSplit): packed 4 B when every sorted value (point
-  // index << 1 | sign) fits CV_BITS, else 4 B values + 1 B fine indices (ent holds emax x 8 B)
-  uint64_t npts = 0;
-  for (uint32_t k = 0; k < tl.nclass; ++k)
-    if (tl.c[k].count) npts = std::max<uint64_t>(npts, (uint64_t)tl.c[k].pt_base + tl.c[k].count);
-  if (!force_split && 2 * npts < (1ull << CV_BITS)) {
-    const EntPacked e{reinterpret_cast<uint32_t*>(ent)};
-    if (tiles) k_bin_scatter<EntPacked><<<tiles, 256, 0, st>>>(tl, digits, ccur, e);
-    k_fine_sort<EntPacked><<<nbins, 256, 0, st>>>(coff, ccnt, e, off, cnt, sval, skey);
-  } else {
-    const EntSplit e{reinterpret_cast<uint32_t*>(ent), reinterpret_cast<uint8_t*>(ent) + 4 * emax};
-    if (tiles) k_bin_scatter<EntSplit><<<tiles, 256, 0, st>>>(tl, digits, ccur, e);
-    k_fine_sort<EntSplit><<<nbins, 256, 0, st>>>(coff, ccnt, e, off, cnt, sval, skey);
-  }
+    k_bin_scan<<<1, 1024, 0, st>>>(ccnt, nbins, coff, ccur, total);
+    // coarse-pass entries (msm.hpp EntPacked / EntSplit): packed 4 B when every sorted value (point
+    // index << 1 | sign) fits CV_BITS, else 4 B values + 1 B fine indices (ent holds emax x 8 B)
+    uint64_t npts = 0;
+    for (uint32_t k = 0; k < tl.nclass; ++k)
+      if (tl.c[k].count) npts = std::max<uint64_t>(npts, (uint64_t)tl.c[k].pt_base + tl.c[k].count);
+    if (!force_split && 2 * npts < (1ull << CV_BITS)) {
+      const EntPacked e{reinterpret_cast<uint32_t*>(ent)};
+      if (tiles) k_bin_scatter<EntPacked, WB><<<tiles, 256, 0, st>>>(tl, digits, ccur, e);
+      k_fine_sort<EntPacked><<<nbins, 256, 0, st>>>(coff, ccnt, e, off, cnt, sval, skey);
+    } else {
+      const EntSplit e{reinterpret_cast<uint32_t*>(ent), reinterpret_cast<uint8_t*>(ent) + 4 * emax};
+      if (tiles) k_bin_scatter<EntSplit, WB><<<tiles, 256, 0, st>>>(tl, digits, ccur, e);
+      k_fine_sort<EntSplit><<<nbins, 256, 0, st>>>(coff, ccnt, e, off, cnt, sval, skey);
+    }
+  });
 }
 
 template <class Cv>
@@ -56,29 +70,36 @@ void Launch<Cv>::pts_to29(hipStream_t st, AF* pts, uint32_t n) {
 
 template <class Cv>
 void Launch<Cv>::reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const XY* buckets,
-                        const uint32_t* acc29, XY* R, XY* U, XY* scratch, XY* winsum) {
-  const uint32_t nseg = nsets * (NBUCKETS / SEG);
-  k_reduce_segments<Cv><<<grid_for(2 * (size_t)nseg, 256), 256, 0, st>>>(nseg, cnt, buckets, acc29, R, U);  // 2 threads per segment
-  // scratch: nsets * RB_PARTS partial sums
-  k_reduce_bits<Cv><<<nsets * RB_PARTS, 256, 0, st>>>(R, U, scratch);
-  k_reduce_bits_finish<Cv><<<nsets, 64, 0, st>>>(scratch, winsum);
+                        const uint32_t* acc29, XY* R, XY* U, XY* scratch, XY* winsum, int wbits) {
+  with_wbits(wbits, [&](auto wb) {
+    constexpr int WB = decltype(wb)::value;
+    const uint32_t nseg = nsets * Win<WB>::NSEG;
+    k_reduce_segments<Cv><<<grid_for(2 * (size_t)nseg, 256), 256, 0, st>>>(nseg, cnt, buckets, acc29, R, U);  // 2 threads per segment
+    // scratch: nsets * RB_PARTS partial sums
+    k_reduce_bits<Cv, WB><<<nsets * Win<WB>::RB_PARTS, 256, 0, st>>>(R, U, scratch);
+    k_reduce_bits_finish<Cv, WB><<<nsets, 64, 0, st>>>(scratch, winsum);
+  });
 }
 
 template <class Cv>
-void Launch<Cv>::window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res) {
-  k_window_combine<Cv><<<mw.nmsm, 64, 0, st>>>(mw, winsum, res);
+void Launch<Cv>::window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res, int wbits) {
+  with_wbits(wbits, [&](auto wb) {
+    constexpr int WB = decltype(wb)::value;
+    k_window_combine<Cv, WB><<<mw.nmsm, 64, 0, st>>>(mw, winsum, res);
+  });
 }
 
 template void Launch<KZ_CURVE_T>::sort(hipStream_t, const TermList&, uint32_t, const uint8_t*, uint32_t*, uint32_t*,
-                                       uint64_t*, size_t, bool, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*);
+                                       uint64_t*, size_t, bool, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
 template void Launch<KZ_CURVE_T>::accumulate(hipStream_t, size_t, const uint32_t*, const uint32_t*, const uint32_t*,
                                              const uint32_t*, const uint32_t*, const Affine<KZ_CURVE_T>*,
                                              Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, uint32_t*,
                                              uint32_t);
 template void Launch<KZ_CURVE_T>::pts_to29(hipStream_t, Affine<KZ_CURVE_T>*, uint32_t);
 template void Launch<KZ_CURVE_T>::reduce(hipStream_t, uint32_t, const uint32_t*, const Xyzz<KZ_CURVE_T>*,
-                                         const uint32_t*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*);
+                                         const uint32_t*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*,
+                                         int);
 template void Launch<KZ_CURVE_T>::window_combine(hipStream_t, const MsmWindows&, const Xyzz<KZ_CURVE_T>*,
-                                                 Xyzz<KZ_CURVE_T>*);
+                                                 Xyzz<KZ_CURVE_T>*, int);
 
 }  // namespace kzgmi

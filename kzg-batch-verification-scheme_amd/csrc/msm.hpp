@@ -75,6 +75,26 @@ constexpr int COARSE_SHIFT = 7;
 constexpr int FINE = 1 << COARSE_SHIFT;                 // buckets per coarse bin
 constexpr int BINS_PER_SET = NBUCKETS >> COARSE_SHIFT;  // 256
 constexpr int TILE_TERMS = 4096;                        // terms per tile (16 per thread)
+#ifndef KZ_REDUCE_R8U  // (k_reduce_segments: V records, see there)
+constexpr bool kSegV = true;
+#else  // A/B reference: R_g = R_0 + (R_1 + 8 U_1) per segment, no V records
+constexpr bool kSegV = false;
+#endif
+// Window width c of a call (WBITS, NBUCKETS, BINS_PER_SET above are c = 16's): large calls use
+// c = 16; small ones (few entries per bucket) c = 13 -- 8x fewer buckets to reduce for 5/4 the
+// terms (api.hip call_wbits).  The sort, the window-sum reduction and the combination are
+// instantiated per c.
+template <int C>
+struct Win {
+  static constexpr int WBITS = C;
+  static constexpr int NBUCKETS = 1 << (C - 1);         // signed digits |d| in [1, 2^(c-1)]
+  static constexpr int BINS = NBUCKETS >> COARSE_SHIFT;  // coarse bins per set (<= 256 = block)
+  static constexpr int NSEG = NBUCKETS / SEG;            // reduction segments per set
+  static constexpr int SEG_BITS = C - 1 - 4;             // log2(NSEG)
+  static constexpr int MAXW = 256 / C + 1;               // windows of a 256-bit scalar (+ carry)
+  static constexpr int RB_PARTS = SEG_BITS + (kSegV ? 6 : 4);  // k_reduce_bits parts per set
+  static_assert(NSEG == (1 << SEG_BITS) && BINS <= 256 && BINS >= 1, "window width");
+};
 // sorted value = point index << 1 | sign, | SV_FIRST on the first entry of each bucket (point
 // indices stay below 2^30: at most 16 x 2^26 commit-key points)
 constexpr uint32_t SV_FIRST = 1u << 31;
@@ -136,8 +156,9 @@ KZ_DEV TileRef tile_decode(const TermList& tl, uint32_t t) {
 // over its windows; emit(local window, code) for windows win_off .. win_off + nwin - 1.  Code = 0
 // for a zero digit or a point at infinity, else |d| | (entry sign << 31) with entry sign =
 // (d < 0) xor the half-scalar's sign flag.
-template <class Emit>
+template <int WB, class Emit>
 KZ_DEV void term_digits(const TermClass& C, uint32_t i, const uint8_t* __restrict__ inf, Emit&& emit) {
+  using W = Win<WB>;
   const uint32_t* sp = C.scal + (size_t)i * C.scal_stride;
   uint32_t w8[8];
   bool neg = false;
@@ -156,11 +177,15 @@ KZ_DEV void term_digits(const TermClass& C, uint32_t i, const uint8_t* __restric
   const int w0 = (int)C.win_off, w1 = (int)(C.win_off + C.nwin);
   uint32_t carry = 0;
 #pragma unroll
-  for (int w = 0; w < 16; ++w) {
+  for (int w = 0; w < W::MAXW; ++w) {
     if (w >= w1) break;
-    const uint32_t raw = (w8[w >> 1] >> ((w & 1) * 16)) & 0xffffu;
+    // bits [w c, w c + c) of the scalar (compile-time word index and shift)
+    const int bit = w * WB, wi = bit >> 5, sh = bit & 31;
+    uint32_t raw = wi < 8 ? w8[wi] >> sh : 0u;
+    if (sh + WB > 32 && wi + 1 < 8) raw |= w8[wi + 1] << (32 - sh);
+    raw &= (1u << WB) - 1;
     int d = (int)(raw + carry);
-    if (d > NBUCKETS) { d -= (1 << WBITS); carry = 1; } else { carry = 0; }
+    if (d > W::NBUCKETS) { d -= (1 << WB); carry = 1; } else { carry = 0; }
     if (w >= w0) {
       uint32_t code = 0;
       if (d != 0 && !is_inf) code = (uint32_t)(d < 0 ? -d : d) | ((d < 0) != neg ? 0x80000000u : 0u);
@@ -182,7 +207,7 @@ static __global__ void __launch_bounds__(256) k_digits(TermList tl, const uint8_
   }
   if (k >= (int)tl.nclass) return;
   const TermClass& C = tl.c[k];
-  term_digits(C, i, inf, [&](int w, uint32_t code) { digits[C.dig_base + (size_t)w * C.count + i] = code; });
+  term_digits<WBITS>(C, i, inf, [&](int w, uint32_t code) { digits[C.dig_base + (size_t)w * C.count + i] = code; });
 }
 
 // k_digits and k_bin_count in one pass: workgroup = 4096 terms of one class (16 per thread),
@@ -194,10 +219,12 @@ inline uint32_t num_digit_groups_host(const TermList& tl) {
   for (uint32_t k = 0; k < tl.nclass; ++k) g += (tl.c[k].count + TILE_TERMS - 1) / TILE_TERMS;
   return g;
 }
-static __global__ void __launch_bounds__(256) k_digits_count(TermList tl, const uint8_t* __restrict__ inf,
+template <int WB>
+__global__ void __launch_bounds__(256) k_digits_count(TermList tl, const uint8_t* __restrict__ inf,
                                                       uint32_t* __restrict__ digits,
                                                       uint32_t* __restrict__ coarse_cnt) {
-  __shared__ uint32_t hist[16][BINS_PER_SET];
+  using W = Win<WB>;
+  __shared__ uint32_t hist[W::MAXW][W::BINS];
   uint32_t b = blockIdx.x;
   int k = 0;
   for (; k < (int)tl.nclass - 1; ++k) {
@@ -207,22 +234,25 @@ static __global__ void __launch_bounds__(256) k_digits_count(TermList tl, const 
   }
   const TermClass& C = tl.c[k];
   const uint32_t t = threadIdx.x;
+  if (t < (uint32_t)W::BINS) {
 #pragma unroll
-  for (int w = 0; w < 16; ++w) hist[w][t] = 0;
+    for (int w = 0; w < W::MAXW; ++w) hist[w][t] = 0;
+  }
   __syncthreads();
 #pragma unroll 1
   for (int j = 0; j < TILE_TERMS / 256; ++j) {
     const uint32_t i = b * TILE_TERMS + j * 256 + t;
     if (i >= C.count) break;
-    term_digits(C, i, inf, [&](int w, uint32_t code) {
+    term_digits<WB>(C, i, inf, [&](int w, uint32_t code) {
       if (code) atomicAdd(&hist[w][((code & 0x7fffffffu) - 1) >> COARSE_SHIFT], 1u);
       digits[C.dig_base + (size_t)w * C.count + i] = code;
     });
   }
   __syncthreads();
+  if (t >= (uint32_t)W::BINS) return;
   for (int w = 0; w < (int)C.nwin; ++w) {
     const uint32_t h = hist[w][t];
-    if (h) atomicAdd(&coarse_cnt[(C.set_base + w) * BINS_PER_SET + t], h);
+    if (h) atomicAdd(&coarse_cnt[(C.set_base + w) * W::BINS + t], h);
   }
 }
 
@@ -280,12 +310,14 @@ static __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __rest
 // consecutive threads store consecutive addresses of a bin's run (the tile's run in each bin
 // is contiguous in `tmp`); writing each entry from the thread that ranked it scattered every
 // wavefront store over ~64 bins.
-template <class E>
+template <class E, int WB = WBITS>
 __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t* __restrict__ digits,
                                                      uint32_t* __restrict__ coarse_cursor, E tmp) {
-  __shared__ uint32_t hist[BINS_PER_SET];
-  __shared__ uint32_t base[BINS_PER_SET];   // global start of this tile's run in bin b
-  __shared__ uint32_t lstart[BINS_PER_SET]; // local (staged) start of bin b
+  using W = Win<WB>;
+  constexpr uint32_t NBIN = W::BINS;        // coarse bins per set (threads >= NBIN only rank)
+  __shared__ uint32_t hist[NBIN];
+  __shared__ uint32_t base[NBIN];   // global start of this tile's run in bin b
+  __shared__ uint32_t lstart[NBIN]; // local (staged) start of bin b
   __shared__ typename E::R stage[TILE_TERMS];
   __shared__ uint8_t stage_bin[TILE_TERMS];
   const TileRef T = tile_decode(tl, blockIdx.x);
@@ -293,7 +325,7 @@ __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t
   const uint32_t set = C.set_base + T.w;
   const uint32_t* dg = digits + C.dig_base + (size_t)T.w * C.count;
   const uint32_t t = threadIdx.x;
-  hist[t] = 0;
+  if (t < NBIN) hist[t] = 0;
   __syncthreads();
   uint32_t rank[TILE_TERMS / 256], key[TILE_TERMS / 256], ent[TILE_TERMS / 256];
 #pragma unroll
@@ -303,29 +335,31 @@ __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t
     const uint32_t code = local < C.count ? dg[local] : 0u;
     if (!code) continue;
     const uint32_t mag = code & 0x7fffffffu;
-    key[j] = set * NBUCKETS + (mag - 1);
+    key[j] = set * W::NBUCKETS + (mag - 1);
     ent[j] = ((C.pt_base + local) << 1) | (code >> 31);
     rank[j] = atomicAdd(&hist[(mag - 1) >> COARSE_SHIFT], 1u);
   }
   __syncthreads();
-  const uint32_t h = hist[t];
-  base[t] = h ? atomicAdd(&coarse_cursor[set * BINS_PER_SET + t], h) : 0u;
-  lstart[t] = h;
+  const uint32_t h = t < NBIN ? hist[t] : 0u;
+  if (t < NBIN) {
+    base[t] = h ? atomicAdd(&coarse_cursor[set * NBIN + t], h) : 0u;
+    lstart[t] = h;
+  }
   __syncthreads();
-  for (int d = 1; d < BINS_PER_SET; d <<= 1) {  // inclusive scan of the tile's bin counts
-    const uint32_t x = t >= (uint32_t)d ? lstart[t - d] : 0u;
+  for (uint32_t d = 1; d < NBIN; d <<= 1) {  // inclusive scan of the tile's bin counts
+    const uint32_t x = (t < NBIN && t >= d) ? lstart[t - d] : 0u;
     __syncthreads();
-    lstart[t] += x;
+    if (t < NBIN) lstart[t] += x;
     __syncthreads();
   }
-  const uint32_t ntile = lstart[BINS_PER_SET - 1];
+  const uint32_t ntile = lstart[NBIN - 1];
   __syncthreads();
-  lstart[t] -= h;  // exclusive
+  if (t < NBIN) lstart[t] -= h;  // exclusive
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < TILE_TERMS / 256; ++j) {
     if (key[j] == 0xffffffffu) continue;
-    const uint32_t bin = (key[j] >> COARSE_SHIFT) & (BINS_PER_SET - 1);
+    const uint32_t bin = (key[j] >> COARSE_SHIFT) & (NBIN - 1);
     const uint32_t q = lstart[bin] + rank[j];
     stage[q] = E::make(key[j], ent[j]);
     stage_bin[q] = (uint8_t)bin;
@@ -1119,11 +1153,6 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
 // k_reduce_bits and scaled once in k_reduce_bits_finish.  (Forming R_1 + 8 U_1 here put three
 // doublings on the upper half's chain while the lower half idled: ~20 point operations per
 // wave instead of ~16; the kernel is latency-bound at 1.5 waves per SIMD.)
-#ifndef KZ_REDUCE_R8U
-constexpr bool kSegV = true;
-#else  // A/B reference: R_g = R_0 + (R_1 + 8 U_1) per segment, no V records
-constexpr bool kSegV = false;
-#endif
 template <class Cv>
 __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const uint32_t* __restrict__ cnt,
                                                          const Xyzz<Cv>* __restrict__ buckets,
@@ -1197,47 +1226,44 @@ KZ_DEV Xyzz<Cv> block_sum256(Xyzz<Cv> v, Xyzz<Cv>* lds) {
 // Window sums with a short dependency chain (~40 point operations per set; the earlier one
 // workgroup per set with three serial 16-term segment levels needed ~130, 3.8 vs 1.2 ms):
 //   W = sum_g (R'_g + U_g) + 8 sum_g V_g + SEG * sum_g g U_g,   sum_g g U_g = sum_j 2^j B_j,
-//   B_j = sum of the 1024 U_g whose index g has bit j set (j < 11, NSEG = 2^11).
-// k_reduce_bits: RB_PARTS workgroups per set -- 11 compute B_j, 4 compute quarter sums of
-// R'_g + U_g, 2 compute half sums of V_g -- each 4 points per thread + an 8-level LDS tree.
-// k_reduce_bits_finish: one wave per set, Horner over the 11 bit sums (10 doublings + 10
-// additions), then 2 H + sum V, 3 doublings: 16 H + 8 sum V.
-constexpr int RB_PARTS = kSegV ? 17 : 15;
+//   B_j = sum of the NSEG / 2 U_g whose index g has bit j set (j < SEG_BITS: 11 for c = 16).
+// k_reduce_bits: RB_PARTS workgroups per set -- SEG_BITS compute B_j, 4 compute quarter sums of
+// R'_g + U_g, 2 compute half sums of V_g -- each a few points per thread (c = 16: 4) + an
+// 8-level LDS tree.  k_reduce_bits_finish: one wave per set, Horner over the bit sums, then
+// 2 H + sum V, 3 doublings: 16 H + 8 sum V.
+constexpr int RB_PARTS = Win<WBITS>::RB_PARTS;  // c = 16 (the most parts per set)
 
-template <class Cv>
+template <class Cv, int WB = WBITS>
 __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict__ R, const Xyzz<Cv>* __restrict__ U,
                                                      Xyzz<Cv>* __restrict__ parts) {
   KZ_TAIL_PRIO();
-  constexpr uint32_t NSEG = NBUCKETS / SEG;  // 2048 = 2^11
-  static_assert(NSEG == 2048 && RB_PARTS == (kSegV ? 17 : 15), "bit decomposition assumes 2^11 segments per set");
-  const uint32_t set = blockIdx.x / RB_PARTS, j = blockIdx.x % RB_PARTS;
-  if constexpr (kAcc29<Cv>) {  // BLS12-381: radix 2^29 on the R/U records, inline additions
+  using Wn = Win<WB>;
+  constexpr uint32_t NSEG = Wn::NSEG, SB = Wn::SEG_BITS, RBP = Wn::RB_PARTS;
+  const uint32_t set = blockIdx.x / RBP, j = blockIdx.x % RBP;
+  const uint32_t t = threadIdx.x;
+  // the segment index of the q-th g (q < NSEG / 2) whose bit j is set
+  auto bit_g = [j](uint32_t q) { return ((q >> j) << (j + 1)) | (1u << j) | (q & ((1u << j) - 1)); };
+  if constexpr (kAcc29<Cv>) {  // radix 2^29 on the R/U/V records, inline additions
     using Q = Fp29Of<Cv>;
     constexpr int N = Q::N, W29 = kW29<Q>;
     __shared__ uint32_t lds29[W29 + 1][128];
-    const uint32_t t = threadIdx.x;
     const uint32_t* R29 = reinterpret_cast<const uint32_t*>(R) + (size_t)set * NSEG * W29;
     const uint32_t* U29 = reinterpret_cast<const uint32_t*>(U) + (size_t)set * NSEG * W29;
-    const uint32_t nsets = gridDim.x / RB_PARTS;  // V records follow the nsets * NSEG U records
+    const uint32_t nsets = gridDim.x / RBP;  // V records follow the nsets * NSEG U records
     const uint32_t* V29 = reinterpret_cast<const uint32_t*>(U) + ((size_t)nsets + set) * NSEG * W29;
     X29<Q> v{F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), true};
-    if (j >= 15) {  // kSegV: half sums of V_g
+    if (j >= SB + 4) {  // kSegV: half sums of V_g
 #pragma unroll 1
-      for (uint32_t i = 0; i < 4; ++i) v = x29_add<Cv, Q>(v, load_x29<Q>(V29, (j - 15) * (NSEG / 2) + t + 256 * i));
-    } else if (j < 11) {
+      for (uint32_t q = t; q < NSEG / 2; q += 256) v = x29_add<Cv, Q>(v, load_x29<Q>(V29, (j - SB - 4) * (NSEG / 2) + q));
+    } else if (j < SB) {
 #pragma unroll 1
-      for (uint32_t i = 0; i < 4; ++i) {  // q: 10-bit rank among the g with bit j set
-        const uint32_t q = t + 256 * i;
-        const uint32_t g = ((q >> j) << (j + 1)) | (1u << j) | (q & ((1u << j) - 1));
-        v = x29_add<Cv, Q>(v, load_x29<Q>(U29, g));
-      }
+      for (uint32_t q = t; q < NSEG / 2; q += 256) v = x29_add<Cv, Q>(v, load_x29<Q>(U29, bit_g(q)));
     } else {
-      const uint32_t base = (j - 11) * (NSEG / 4);
+      const uint32_t base = (j - SB) * (NSEG / 4);
 #pragma unroll 1
-      for (uint32_t i = 0; i < 2; ++i) {
-        const uint32_t g = base + t + 256 * i;
-        v = x29_add<Cv, Q>(v, load_x29<Q>(R29, g));
-        v = x29_add<Cv, Q>(v, load_x29<Q>(U29, g));
+      for (uint32_t q = t; q < NSEG / 4; q += 256) {
+        v = x29_add<Cv, Q>(v, load_x29<Q>(R29, base + q));
+        v = x29_add<Cv, Q>(v, load_x29<Q>(U29, base + q));
       }
     }
     for (int st = 128; st >= 1; st >>= 1) {  // LDS tree, one coordinate word per row
@@ -1266,64 +1292,51 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
       }
       __syncthreads();
     }
-    if (t == 0) store_xyzz(&parts[(size_t)set * RB_PARTS + j], x29_to32<Cv, Q>(v));
+    if (t == 0) store_xyzz(&parts[(size_t)set * RBP + j], x29_to32<Cv, Q>(v));
     return;
   }
   __shared__ __attribute__((aligned(16))) Xyzz<Cv> lds[128];
   const Xyzz<Cv>* Rs = R + (size_t)set * NSEG;
   const Xyzz<Cv>* Us = U + (size_t)set * NSEG;
-  const Xyzz<Cv>* Vs = U + ((size_t)gridDim.x / RB_PARTS + set) * NSEG;
-  const uint32_t t = threadIdx.x;
-  // segment sum g: 32-bit XYZZ, or (BLS12-381) a radix-29 record converted as it is read
-  auto seg = [&](bool r, uint32_t g) {
-    if constexpr (kAcc29<Cv>) {
-      using Q = Fp29Of<Cv>;
-      return x29_to32<Cv, Q>(load_x29<Q>(reinterpret_cast<const uint32_t*>(r ? R : U) + (size_t)set * NSEG * kW29<Q>, g));
-    } else {
-      return load_xyzz(&(r ? Rs : Us)[g]);
-    }
-  };
+  const Xyzz<Cv>* Vs = U + ((size_t)gridDim.x / RBP + set) * NSEG;
   Xyzz<Cv> s = Xyzz<Cv>::inf();
-  if (j >= 15) {  // kSegV: half sums of V_g
+  if (j >= SB + 4) {  // kSegV: half sums of V_g
 #pragma unroll 1
-    for (uint32_t i = 0; i < 4; ++i) s = xyzz_add(s, load_xyzz(&Vs[(j - 15) * (NSEG / 2) + t + 256 * i]));
-  } else if (j < 11) {
+    for (uint32_t q = t; q < NSEG / 2; q += 256) s = xyzz_add(s, load_xyzz(&Vs[(j - SB - 4) * (NSEG / 2) + q]));
+  } else if (j < SB) {
 #pragma unroll 1
-    for (uint32_t i = 0; i < 4; ++i) {  // q: 10-bit rank among the g with bit j set
-      const uint32_t q = t + 256 * i;
-      const uint32_t g = ((q >> j) << (j + 1)) | (1u << j) | (q & ((1u << j) - 1));
-      s = xyzz_add(s, seg(false, g));
-    }
+    for (uint32_t q = t; q < NSEG / 2; q += 256) s = xyzz_add(s, load_xyzz(&Us[bit_g(q)]));
   } else {
-    const uint32_t base = (j - 11) * (NSEG / 4);
+    const uint32_t base = (j - SB) * (NSEG / 4);
 #pragma unroll 1
-    for (uint32_t i = 0; i < 2; ++i) {
-      const uint32_t g = base + t + 256 * i;
-      s = xyzz_add(s, seg(true, g));
-      s = xyzz_add(s, seg(false, g));
+    for (uint32_t q = t; q < NSEG / 4; q += 256) {
+      s = xyzz_add(s, load_xyzz(&Rs[base + q]));
+      s = xyzz_add(s, load_xyzz(&Us[base + q]));
     }
   }
   const Xyzz<Cv> v = block_sum256(s, lds);
-  if (t == 0) store_xyzz(&parts[(size_t)set * RB_PARTS + j], v);
+  if (t == 0) store_xyzz(&parts[(size_t)set * RBP + j], v);
 }
 
-// One wave per set, lane-parallel arithmetic (lpfield.hpp): Horner over the 11 bit sums
-// (10 XYZZ doublings + 10 additions), the 4 quarter sums, 4 doublings -- ~80 row-parallel
+// One wave per set, lane-parallel arithmetic (lpfield.hpp): Horner over the bit sums (c = 16:
+// 10 XYZZ doublings + 10 additions), the 4 quarter sums, 4 doublings -- ~80 row-parallel
 // product steps instead of ~330 serial products on one lane (0.71 ms before).
-template <class Cv>
+template <class Cv, int WB = WBITS>
 __global__ void __launch_bounds__(64) k_reduce_bits_finish(const Xyzz<Cv>* __restrict__ parts,
                                                            Xyzz<Cv>* __restrict__ winsum) {
   KZ_TAIL_PRIO();
+  using Wn = Win<WB>;
+  constexpr int SB = Wn::SEG_BITS;
   const uint32_t set = blockIdx.x;
   const LpCtx<Cv> c = lp_ctx<Cv>();
-  const Xyzz<Cv>* P = parts + (size_t)set * RB_PARTS;
-  LpXyzz<Cv> V = lp_load_xyzz(c, &P[10]);
+  const Xyzz<Cv>* P = parts + (size_t)set * Wn::RB_PARTS;
+  LpXyzz<Cv> V = lp_load_xyzz(c, &P[SB - 1]);
 #pragma unroll 1
-  for (int j = 9; j >= 0; --j) V = lp_xyzz_add(c, lp_xyzz_dbl(c, V), lp_load_xyzz(c, &P[j]));
-  LpXyzz<Cv> W = lp_xyzz_add(c, lp_xyzz_add(c, lp_load_xyzz(c, &P[11]), lp_load_xyzz(c, &P[12])),
-                             lp_xyzz_add(c, lp_load_xyzz(c, &P[13]), lp_load_xyzz(c, &P[14])));
+  for (int j = SB - 2; j >= 0; --j) V = lp_xyzz_add(c, lp_xyzz_dbl(c, V), lp_load_xyzz(c, &P[j]));
+  LpXyzz<Cv> W = lp_xyzz_add(c, lp_xyzz_add(c, lp_load_xyzz(c, &P[SB]), lp_load_xyzz(c, &P[SB + 1])),
+                             lp_xyzz_add(c, lp_load_xyzz(c, &P[SB + 2]), lp_load_xyzz(c, &P[SB + 3])));
   if constexpr (kSegV) {  // 16 H + 8 sum V = 8 (2 H + sum V)
-    V = lp_xyzz_add(c, lp_xyzz_dbl(c, V), lp_xyzz_add(c, lp_load_xyzz(c, &P[15]), lp_load_xyzz(c, &P[16])));
+    V = lp_xyzz_add(c, lp_xyzz_dbl(c, V), lp_xyzz_add(c, lp_load_xyzz(c, &P[SB + 4]), lp_load_xyzz(c, &P[SB + 5])));
 #pragma unroll 1
     for (int i = 0; i < 3; ++i) V = lp_xyzz_dbl(c, V);
   } else {
@@ -1333,17 +1346,17 @@ __global__ void __launch_bounds__(64) k_reduce_bits_finish(const Xyzz<Cv>* __res
   lp_store_xyzz(c, &winsum[set], lp_xyzz_add(c, W, V));
 }
 
-// Horner over windows for each MSM: res[m] = sum_w 2^(16 w) winsum[set_base_m + w]
+// Horner over windows for each MSM: res[m] = sum_w 2^(c w) winsum[set_base_m + w]
 struct MsmWindows {
   uint32_t nmsm;
   uint32_t set_base[2];
   uint32_t nwin[2];
 };
 // One wave per MSM, lane-parallel arithmetic (lpfield.hpp): the running sum stays in a = 0
-// Jacobian coordinates through the 16 doublings of a step (3 row-parallel product steps each);
+// Jacobian coordinates through the c doublings of a step (3 row-parallel product steps each);
 // the window sum is added in XYZZ.  ~57 product steps per window instead of ~134 serial
 // products (3.9 ms for 16 windows before).
-template <class Cv>
+template <class Cv, int WB = WBITS>
 __global__ void __launch_bounds__(64) k_window_combine(MsmWindows mw, const Xyzz<Cv>* __restrict__ winsum,
                                                        Xyzz<Cv>* __restrict__ res) {
   KZ_TAIL_PRIO();
@@ -1354,7 +1367,7 @@ __global__ void __launch_bounds__(64) k_window_combine(MsmWindows mw, const Xyzz
 #pragma unroll 1
   for (int w = (int)mw.nwin[m] - 2; w >= 0; --w) {
 #pragma unroll 1
-    for (int i = 0; i < WBITS; ++i) acc = lp_jac_dbl(c, acc);
+    for (int i = 0; i < WB; ++i) acc = lp_jac_dbl(c, acc);
     acc = lp_jac_from_xyzz(c, lp_xyzz_add(c, lp_xyzz_from_jac(c, acc), lp_load_xyzz(c, &W[w])));
   }
   lp_store_xyzz(c, &res[m], lp_xyzz_from_jac(c, acc));

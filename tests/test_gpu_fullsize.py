@@ -161,12 +161,15 @@ def test_sharded_batch_cfg5_bn254(ctx):
 
 
 @pytest.mark.parametrize("curve,n,trusted", [("bls12_381", 300007, False), ("bls12_381", 262143, True),
-                                             ("bn254", 524289, False)])
+                                             ("bn254", 524289, False),
+                                             # 2^15 < n <= 2^17: 13-bit windows (api.hip call_wbits)
+                                             ("bls12_381", 100003, False), ("bls12_381", 70001, True),
+                                             ("bn254", 90001, False)])
 def test_ragged_batch_vs_oracle(ctx, curve, n, trusted):
     """Non-power-of-two batches: the accumulation's per-thread runs, the last partial round and
     the bucket pieces joined by k_fixup do not divide evenly.  A, B and the verdict bit-exact vs
     the oracle (with and without the GLV split that trusted_g1 enables), then one corrupted
-    proof flips the verdict."""
+    proof flips the verdict.  The mid sizes run the 13-bit window width."""
     C = pc.CURVES[curve]
     tau = 0xBADC0DE + n
     Cm, z, y, P = _gen_batch(ctx, curve, n, tau, hashlib.sha256(b"ragged%d" % n).digest())
@@ -188,10 +191,14 @@ def test_ragged_batch_vs_oracle(ctx, curve, n, trusted):
 
 
 @pytest.mark.parametrize("curve,n,trusted", [("bls12_381", 393213, False), ("bls12_381", 393213, True),
-                                             ("bn254", 655361, False)])
+                                             ("bn254", 655361, False),
+                                             # 2^16 < n <= 2^17: 13-bit windows (20; 10 with GLV)
+                                             ("bls12_381", 100003, False), ("bls12_381", 120001, True),
+                                             ("bn254", 131071, False)])
 def test_ragged_msm_vs_oracle(ctx, curve, n, trusted):
     """Mid-size, non-power-of-two MSMs with uniform 255-bit scalars (16 windows; 8 with GLV on
-    trusted BLS12-381 points): bit-exact vs the oracle."""
+    trusted BLS12-381 points; 20 and 10 for the 13-bit width of the smaller sizes): bit-exact vs
+    the oracle."""
     import numpy as np
     import torch
     C = pc.CURVES[curve]
