@@ -239,6 +239,20 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   size_t nchunks = (emax + chunk - 1) / chunk + 1;
   const size_t cap = c->acc_threads_env ? c->acc_threads_env : (size_t)c->ncu * 4 * kAccWaves<Cv> * 64;
   if (cap && nchunks > cap) nchunks = cap;
+#if !defined(KZ_NO_ACC_BALANCE)
+  // A call with no other slot of the context in flight is latency-bound: below the cap, give
+  // every SIMD the same whole number of waves (shorter equal chunks).  A 2^17 batch at 13 bits
+  // is 1.25 waves per SIMD, and its SIMDs with two waves ran 1.5x longer than those with one:
+  // 4.36 -> 3.99 ms per batch.  Pipelined calls keep the longer chunks (fewer pieces to join:
+  // 2^17 batches 1014 vs 966/s with the rounding; profiles/r03/misc_ab_r03.txt).
+  // (kzgmi_ctx_reserve sizes the piece arrays for the rounded count)
+  bool alone = true;
+  for (const Slot& o : c->slots) alone &= &o == &s || !o.pending;
+  alone |= dry;
+  const size_t simd_lanes = (size_t)c->ncu * 4 * 64;
+  if (alone && !c->acc_threads_env && emax > ACC_SMALL_ENTRIES && simd_lanes && nchunks < cap)
+    nchunks = std::min(cap, (nchunks + simd_lanes - 1) / simd_lanes * simd_lanes);
+#endif
   nchunks = (nchunks + 255) / 256 * 256;  // = the launched thread count (part arrays indexed by thread)
   CHK(s.cnt.ensure((size_t)NB * 4));
   CHK(s.off.ensure((size_t)NB * 4));

@@ -58,6 +58,7 @@ void Launch<Cv>::accumulate(hipStream_t st, size_t nchunks, const uint32_t* tota
   // length from the same grid
   const unsigned blocks = grid_for(nchunks, 256);
   k_accumulate<Cv><<<blocks, 256, 0, st>>>(total, sval, skey, off, cnt, pts, buckets, pfirst, plast, acc29, nb);
+  if (kFixGroups) k_fixup_groups<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, pfirst, acc29, nb);
   k_fixup<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, pfirst, plast, buckets, acc29, nb);
 }
 

@@ -1105,8 +1105,70 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
   }
 }
 
+// A bucket cut into k + 1 pieces (its last piece in chunk c0, first pieces of chunks c0+1..c1,
+// k = c1 - c0) is joined by one thread with k dependent additions of ~20 us each.  Narrow top
+// windows crowd thousands of entries into a bucket (13-bit windows of a 255-bit scalar keep 8
+// bits in the top one: 2^17 terms in ~116 buckets, k ~ 18), so for k > 3 the join is two-level:
+// k_fixup_groups sums groups of G = ceil(sqrt k) consecutive first pieces into the group's first
+// slot, k_fixup adds the ceil(k / G) group sums -- G - 1 + ceil(k / G) dependent additions.
+#if defined(KZ_NO_FIX_GROUPS)  // A/B reference: one serial chain per bucket
+constexpr bool kFixGroups = false;
+#else
+constexpr bool kFixGroups = true;
+#endif
+KZ_DEV uint32_t fix_group(uint32_t k) {
+  if (k <= 3) return 1;
+  uint32_t g = (uint32_t)sqrtf((float)k);
+  while (g * g < k) ++g;
+  return g;
+}
+
+// (bucket, continuation range) of chunk c when its first entry continues a bucket begun in an
+// earlier chunk: false otherwise.  c0 = the bucket's first chunk, c1 = its last.
+KZ_DEV bool fix_range(uint32_t c, uint32_t len, uint32_t total, const uint32_t* __restrict__ sorted_key,
+                      const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt, uint32_t& key,
+                      uint32_t& c0, uint32_t& c1) {
+  const uint32_t start = c * len;
+  if (start >= total) return false;
+  key = sorted_key[start];
+  const uint32_t o = off[key];
+  if (o >= start) return false;  // bucket starts inside this chunk
+  c0 = o / len;
+  c1 = (o + cnt[key] - 1) / len;
+  return true;
+}
+
+// first level of the two-level join: chunk c heads a group when (c - c0 - 1) % G == 0
+template <class Cv>
+__global__ void __launch_bounds__(256) k_fixup_groups(const uint32_t* __restrict__ total_p,
+                                                      const uint32_t* __restrict__ sorted_key,
+                                                      const uint32_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ cnt,
+                                                      Xyzz<Cv>* __restrict__ part_first, uint32_t* __restrict__ acc29,
+                                                      uint32_t nb) {
+  KZ_TAIL_PRIO();
+  const uint32_t total = *total_p;
+  const uint32_t len = acc_chunk_len(total, gridDim.x * blockDim.x);
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x + 1;
+  uint32_t key, c0, c1;
+  if (!fix_range(c, len, total, sorted_key, off, cnt, key, c0, c1)) return;
+  const uint32_t g = fix_group(c1 - c0);
+  if (g == 1 || (c - c0 - 1) % g) return;
+  const uint32_t last = c + g - 1 < c1 ? c + g - 1 : c1;
+  if constexpr (kAcc29<Cv>) {
+    using Q = Fp29Of<Cv>;
+    X29<Q> acc = load_x29<Q>(acc29, nb + c);
+    for (uint32_t cc = c + 1; cc <= last; ++cc) acc = x29_add<Cv, Q>(acc, load_x29<Q>(acc29, nb + cc));
+    store_x29<Q>(acc29, nb + c, acc);
+  } else {
+    Xyzz<Cv> acc = load_xyzz(&part_first[c]);
+    for (uint32_t cc = c + 1; cc <= last; ++cc) acc = xyzz_add(acc, load_xyzz(&part_first[cc]));
+    store_xyzz(&part_first[c], acc);
+  }
+}
+
 // joins the pieces of buckets that cross chunk boundaries (launched with the same grid as
-// k_accumulate, so acc_chunk_len agrees)
+// k_accumulate, so acc_chunk_len agrees), after k_fixup_groups
 // BLS12-381 (kAcc29): the pieces and the bucket are radix-29 records of acc29 = [nb buckets |
 // nthreads first pieces | nthreads last pieces], joined with the radix-29 XYZZ addition and
 // written back as the record k_reduce_segments reads.
@@ -1123,23 +1185,19 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
   const uint32_t total = *total_p;
   const uint32_t len = acc_chunk_len(total, gridDim.x * blockDim.x);
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x + 1;
-  const uint32_t start = c * len;
-  if (start >= total) return;
-  uint32_t key = sorted_key[start];
-  uint32_t o = off[key];
-  if (o >= start) return;                 // bucket starts inside this chunk
-  uint32_t c0 = o / len;
+  uint32_t key, c0, c1;
+  if (!fix_range(c, len, total, sorted_key, off, cnt, key, c0, c1)) return;
   if (c0 != c - 1) return;                // a later continuation chunk: handled by c0+1
-  uint32_t c1 = (o + cnt[key] - 1) / len;
+  const uint32_t g = kFixGroups ? fix_group(c1 - c0) : 1;  // group sums at c, c + g, ...
   if constexpr (kAcc29<Cv>) {
     const size_t nthreads = (size_t)gridDim.x * blockDim.x;
     using Q = Fp29Of<Cv>;
     X29<Q> acc = load_x29<Q>(acc29, nb + nthreads + c0);
-    for (uint32_t cc = c; cc <= c1; ++cc) acc = x29_add<Cv, Q>(acc, load_x29<Q>(acc29, nb + cc));
+    for (uint32_t cc = c; cc <= c1; cc += g) acc = x29_add<Cv, Q>(acc, load_x29<Q>(acc29, nb + cc));
     store_x29<Q>(acc29, key, acc);
   } else {
     Xyzz<Cv> acc = load_xyzz(&part_last[c0]);
-    for (uint32_t cc = c; cc <= c1; ++cc) acc = xyzz_add(acc, load_xyzz(&part_first[cc]));
+    for (uint32_t cc = c; cc <= c1; cc += g) acc = xyzz_add(acc, load_xyzz(&part_first[cc]));
     store_xyzz(&buckets[key], acc);
   }
 }
