@@ -86,6 +86,7 @@ struct Slot {
   DevBuf pts, inf, scal_r, scal_s, scal_t, tpart, cnt, off, coarse, ent, total, sval, skey;
   DevBuf buckets, pfirst, plast, R, U, scratch, winsum, res, flags, stage, outb;
   DevBuf acc29;                                  // radix-29 bucket records (msm.hpp)
+  DevBuf accq;                                   // k_accumulate's work-queue counter (large calls)
   DevBuf fs_leaves, fs_tmp, fs_top, pow, chal;  // Fiat-Shamir / powers-of-r randomisers
   DevBuf glv_r, glv_s, glv_t;                    // GLV half scalars (glv.hpp): [h0 x n | h1 x n]
   DevBuf digits;                                 // signed window digit codes of every term (msm.hpp)
@@ -118,6 +119,7 @@ struct kzgmi_ctx {
   // batch-verifies/s pipelined when introduced (tools/ab_env.sh).
   int ncu = 0;                // compute units: the accumulation grid cap (kAccWaves, msm.hpp)
   size_t acc_threads_env = 0;  // KZGMI_ACC_THREADS override of that cap (0 = none)
+  int acc_queue = ACC_QUEUE_FACTOR;  // KZGMI_ACC_QUEUE: chunks per capped thread (<= 1: static grid)
   bool sort_split = false;     // KZGMI_SORT_SPLIT: split coarse-pass entries at every size (tests)
   int wbits_env = 0;           // KZGMI_WBITS: 13 or 16 forces the window width (tests, A/B)
   double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
@@ -253,12 +255,23 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   if (alone && !c->acc_threads_env && emax > ACC_SMALL_ENTRIES && simd_lanes && nchunks < cap)
     nchunks = std::min(cap, (nchunks + simd_lanes - 1) / simd_lanes * simd_lanes);
 #endif
+  // Large radix-29 calls (the grid at its cap): c->acc_queue x cap shorter chunks taken from a
+  // work queue by the cap's threads (msm.hpp k_accumulate), so an accumulation that starts behind
+  // another slot's still ends on every CU at about the same time.  The part arrays and k_fixup
+  // are sized for the chunk count.
+  size_t acc_threads = 0;
+  if (kAcc29<Cv> && c->acc_queue > 1 && cap && nchunks == cap && cap % 256 == 0) {
+    acc_threads = cap;
+    nchunks = std::min(cap * (size_t)c->acc_queue, std::max(cap, emax / ACC_QUEUE_MIN_LEN));
+    if (nchunks <= cap) acc_threads = 0;
+  }
   nchunks = (nchunks + 255) / 256 * 256;  // = the launched thread count (part arrays indexed by thread)
   CHK(s.cnt.ensure((size_t)NB * 4));
   CHK(s.off.ensure((size_t)NB * 4));
   CHK(s.coarse.ensure((size_t)3 * nsets * bins * 4));
   CHK(s.ent.ensure(emax * 8));
   CHK(s.total.ensure(16));
+  if (acc_threads) CHK(s.accq.ensure(16));
   CHK(s.sval.ensure(emax * 4 + 16));  // + 16: k_accumulate reads values 4 at a time, up to 3 past the end
   CHK(s.skey.ensure(emax * 4));
   constexpr int W29 = kW29<Fp29Of<Cv>>;
@@ -291,7 +304,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   L::accumulate(st, nchunks, s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
                 s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts,
                 s.buckets.template as<XY>(), s.pfirst.template as<XY>(), s.plast.template as<XY>(),
-                s.acc29.template as<uint32_t>(), NB);
+                s.acc29.template as<uint32_t>(), NB, acc_threads, acc_threads ? s.accq.template as<uint32_t>() : nullptr);
   mark(c, s, PH_ACCUM + 1);
   L::reduce(st, nsets, s.cnt.template as<uint32_t>(), s.buckets.template as<XY>(), s.acc29.template as<uint32_t>(),
             s.R.template as<XY>(),
@@ -610,6 +623,7 @@ int kzgmi_ctx_create(kzgmi_ctx** out, int device_id, int pipeline_slots) {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_id) == hipSuccess && ncu > 0)
     c->ncu = ncu;
   if (const char* e = getenv("KZGMI_ACC_THREADS")) c->acc_threads_env = (size_t)strtoull(e, nullptr, 10);
+  if (const char* e = getenv("KZGMI_ACC_QUEUE")) c->acc_queue = atoi(e);
   if (const char* e = getenv("KZGMI_SORT_SPLIT")) c->sort_split = atoi(e) != 0;
   if (const char* e = getenv("KZGMI_WBITS")) c->wbits_env = atoi(e);
   c->slots.resize(pipeline_slots);
@@ -631,7 +645,7 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
   for (auto& s : c->slots) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     DevBuf* bufs[] = {&s.pts, &s.inf, &s.scal_r, &s.scal_s, &s.scal_t, &s.tpart, &s.cnt, &s.off, &s.coarse, &s.ent,
-                      &s.total, &s.sval, &s.skey, &s.buckets, &s.pfirst, &s.plast, &s.acc29, &s.R, &s.U, &s.scratch,
+                      &s.total, &s.sval, &s.skey, &s.buckets, &s.pfirst, &s.plast, &s.acc29, &s.accq, &s.R, &s.U, &s.scratch,
                       &s.winsum, &s.res, &s.flags, &s.stage, &s.outb, &s.fs_leaves, &s.fs_tmp,
                       &s.fs_top, &s.pow, &s.chal, &s.glv_r, &s.glv_s, &s.glv_t, &s.digits};
     for (DevBuf* b : bufs) b->release();

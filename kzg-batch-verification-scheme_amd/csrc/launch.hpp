@@ -21,7 +21,8 @@ struct Launch {
   // store (k_fixup joins pieces into them; reduce reads them); BN254 uses buckets/pfirst/plast
   static void accumulate(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* sval,
                          const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts, XY* buckets,
-                         XY* pfirst, XY* plast, uint32_t* acc29, uint32_t nb);
+                         XY* pfirst, XY* plast, uint32_t* acc29, uint32_t nb, size_t acc_threads = 0,
+                         uint32_t* next_chunk = nullptr);
   static void pts_to29(hipStream_t st, AF* pts, uint32_t n);  // in place
   static void reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const XY* buckets, const uint32_t* acc29,
                      XY* R, XY* U, XY* scratch, XY* winsum, int wbits = WBITS);

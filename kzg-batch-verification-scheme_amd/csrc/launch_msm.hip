@@ -53,11 +53,20 @@ void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const 
 template <class Cv>
 void Launch<Cv>::accumulate(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* sval,
                             const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts, XY* buckets,
-                            XY* pfirst, XY* plast, uint32_t* acc29, uint32_t nb) {
+                            XY* pfirst, XY* plast, uint32_t* acc29, uint32_t nb, size_t acc_threads,
+                            uint32_t* next_chunk) {
   // nchunks threads (rounded up to whole 256-thread blocks); both kernels derive the chunk
-  // length from the same grid
+  // length from the same grid -- except the radix-29 work-queue form: acc_threads (< nchunks,
+  // whole blocks) threads take the nchunks chunks from the counter next_chunk, zeroed here
   const unsigned blocks = grid_for(nchunks, 256);
-  k_accumulate<Cv><<<blocks, 256, 0, st>>>(total, sval, skey, off, cnt, pts, buckets, pfirst, plast, acc29, nb);
+  if (kAcc29<Cv> && next_chunk && acc_threads && acc_threads < nchunks) {
+    (void)hipMemsetAsync(next_chunk, 0, 4, st);
+    k_accumulate<Cv><<<grid_for(acc_threads, 256), 256, 0, st>>>(total, sval, skey, off, cnt, pts, buckets, pfirst,
+                                                                  plast, acc29, nb, (uint32_t)(blocks * 256u), next_chunk);
+  } else {
+    k_accumulate<Cv><<<blocks, 256, 0, st>>>(total, sval, skey, off, cnt, pts, buckets, pfirst, plast, acc29, nb, 0u,
+                                             nullptr);
+  }
   if (kFixGroups) k_fixup_groups<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, pfirst, acc29, nb);
   k_fixup<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, pfirst, plast, buckets, acc29, nb);
 }
@@ -95,7 +104,7 @@ template void Launch<KZ_CURVE_T>::sort(hipStream_t, const TermList&, uint32_t, c
 template void Launch<KZ_CURVE_T>::accumulate(hipStream_t, size_t, const uint32_t*, const uint32_t*, const uint32_t*,
                                              const uint32_t*, const uint32_t*, const Affine<KZ_CURVE_T>*,
                                              Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, uint32_t*,
-                                             uint32_t);
+                                             uint32_t, size_t, uint32_t*);
 template void Launch<KZ_CURVE_T>::pts_to29(hipStream_t, Affine<KZ_CURVE_T>*, uint32_t);
 template void Launch<KZ_CURVE_T>::reduce(hipStream_t, uint32_t, const uint32_t*, const Xyzz<KZ_CURVE_T>*,
                                          const uint32_t*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*,

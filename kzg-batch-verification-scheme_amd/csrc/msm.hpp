@@ -586,6 +586,13 @@ KZ_DEV Xyzz<Cv> load_xyzz(const Xyzz<Cv>* src) {
 // value in k_accumulate and k_fixup).  The host picks nthreads ~ (entry bound) / ACC_CHUNK(_SMALL),
 // capped at one resident round: the capped grid gives longer, equal chunks (fewer pieces, no
 // partial last round).
+// Work-queue form for calls whose grid reaches the cap (api.hip run_msm_core): ACC_QUEUE_FACTOR
+// chunks per launched thread, none shorter than ACC_QUEUE_MIN_LEN entries.
+#ifndef KZ_ACC_QUEUE_FACTOR
+#define KZ_ACC_QUEUE_FACTOR 2
+#endif
+constexpr int ACC_QUEUE_FACTOR = KZ_ACC_QUEUE_FACTOR;
+constexpr size_t ACC_QUEUE_MIN_LEN = 32;
 KZ_DEV uint32_t acc_chunk_len(uint32_t total, uint32_t nthreads) {
   const uint32_t per = ((total + nthreads - 1) / nthreads + 3) & ~3u;
   return per > 4u ? per : 4u;
@@ -862,13 +869,13 @@ __device__ __noinline__ Xy29<Q> dbl_affine29(const F29<Q> qx, const F29<Q> qy, u
 template <class Cv>
 KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t chunk, uint32_t cur,
                        const uint32_t* __restrict__ sorted_val, const uint32_t* __restrict__ sorted_key,
-                       const uint32_t* __restrict__ pts29, uint32_t* __restrict__ acc29, uint32_t nb) {
+                       const uint32_t* __restrict__ pts29, uint32_t* __restrict__ acc29, uint32_t nb,
+                       uint32_t nthreads) {
   using Q = Fp29Of<Cv>;
   using G = F29<Q>;
   constexpr int N = Q::N, W29 = kW29<Q>;
   __shared__ uint32_t s_zz[N][256], s_zzz[N][256];
   const uint32_t tx = threadIdx.x;
-  const uint32_t nthreads = gridDim.x * blockDim.x;
   auto ld = [tx](uint32_t (&a)[N][256]) {
     asm volatile("" ::: "memory");
     G r;
@@ -1019,8 +1026,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
                                                     Xyzz<Cv>* __restrict__ buckets,
                                                     Xyzz<Cv>* __restrict__ part_first,
                                                     Xyzz<Cv>* __restrict__ part_last,
-                                                    uint32_t* __restrict__ acc29, uint32_t nb) {
+                                                    uint32_t* __restrict__ acc29, uint32_t nb,
+                                                    uint32_t nchunks, uint32_t* __restrict__ next_chunk) {
   const uint32_t total = *total_p;
+  if constexpr (kAcc29<Cv>) {
+    if (next_chunk) {
+      // Work queue (large calls, Launch::accumulate): nchunks chunks, more than the launched
+      // threads; every wavefront takes the next 64 consecutive chunks (one per lane, the same
+      // layout as the static grid) until none is left.  Waves that start late -- behind another
+      // slot's accumulation -- take fewer, so the last accumulation in flight ends on every CU
+      // at about the same time instead of a whole chunk duration apart.  Every wave's loop ends
+      // once the counter passes nchunks (a multiple of 64).
+      const uint32_t len = acc_chunk_len(total, nchunks);
+      const uint32_t lane = threadIdx.x & 63u;
+      for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(next_chunk, 64u);
+        base = __shfl(base, 0);
+        if (base >= nchunks) break;
+        const uint32_t chunk = base + lane;
+        const uint32_t start = chunk * len;
+        if (start < total)
+          acc_loop29<Cv>(start, min(start + len, total), total, chunk, sorted_key[start], sorted_val, sorted_key,
+                         reinterpret_cast<const uint32_t*>(pts), acc29, nb, nchunks);
+      }
+      return;
+    }
+  }
   const uint32_t len = acc_chunk_len(total, gridDim.x * blockDim.x);
   const uint32_t chunk = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t start = chunk * len;
@@ -1029,7 +1061,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
   uint32_t cur = sorted_key[start];
   if constexpr (kAcc29<Cv>) {
     acc_loop29<Cv>(start, end, total, chunk, cur, sorted_val, sorted_key,
-                   reinterpret_cast<const uint32_t*>(pts), acc29, nb);
+                   reinterpret_cast<const uint32_t*>(pts), acc29, nb, gridDim.x * blockDim.x);
   } else {  // A/B reference (KZ_NO_ACC29*): 32-bit limbs
   // ZZ and ZZZ of the running bucket sum live in LDS (word-major per thread: conflict-free
   // 32-bit accesses), X and Y in registers.  ZZ/ZZZ are read only at the start (U2, S2) and the

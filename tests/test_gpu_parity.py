@@ -276,6 +276,43 @@ def test_split_sort_entries(curve, golden):
 
 
 @pytest.mark.parametrize("curve", CURVES)
+def test_accumulation_work_queue(curve, golden):
+    """k_accumulate's work-queue form (calls whose grid reaches the cap): a context whose cap is
+    256 threads (KZGMI_ACC_THREADS) with 8 chunks per thread (KZGMI_ACC_QUEUE) makes every wave
+    take several 64-chunk groups from the counter.  Random and skewed MSMs (one bucket cut into
+    many chunk pieces: the two-level join) against the oracle, and the largest golden batch
+    (below the queue's 32-entry minimum chunk: the static grid) through the same context."""
+    import kzgmi
+    saved = {k: os.environ.get(k) for k in ("KZGMI_ACC_THREADS", "KZGMI_ACC_QUEUE")}
+    os.environ.update(KZGMI_ACC_THREADS="256", KZGMI_ACC_QUEUE="8")
+    try:
+        c = kzgmi.Context(0, 1)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    try:
+        C = pc.CURVES[curve]
+        rng = random.Random(59)
+        n = 5000
+        ks = [rng.randrange(C.r) for _ in range(n)]
+        pts = O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(k) for k in ks), n)
+        for sc in [b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(n)),
+                   b"".join(pk.fr_to_bytes(0x1234567) for _ in range(n)),
+                   b"".join(pk.fr_to_bytes(rng.choice([1, 2, 3, 65535])) for _ in range(n))]:
+            assert c.msm_g1(curve, pts, sc) == O.msm_g1(curve, pts, sc, n)
+        g = golden("%s_batch_n%d.json" % (curve, SIZES[curve][-1]))
+        srs = c.load_srs(curve, h(g["g2"]), h(g["tau_g2"]))
+        ok = c.batch_verify(srs, h(g["commitments"]), h(g["zs"]), h(g["ys"]), h(g["proofs"]), seed=h(g["seed"]))
+        A, B = c.last_combination(curve)
+        assert (A.hex(), B.hex(), ok) == (g["valid"]["A"], g["valid"]["B"], g["valid"]["ok"])
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("curve", CURVES)
 def test_msm_cancelling_buckets(ctx, curve):
     """Buckets whose running sum returns to infinity mid-chunk (P + (-P)), then keeps adding
     (the accumulation's infinity flag, csrc/g1.hpp xyzz_acc_affine_lazy), doubling (P + P),
