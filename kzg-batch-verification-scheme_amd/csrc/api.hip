@@ -120,6 +120,7 @@ struct kzgmi_ctx {
   int ncu = 0;                // compute units: the accumulation grid cap (kAccWaves, msm.hpp)
   size_t acc_threads_env = 0;  // KZGMI_ACC_THREADS override of that cap (0 = none)
   int acc_queue = ACC_QUEUE_FACTOR;  // KZGMI_ACC_QUEUE: chunks per capped thread (<= 1: static grid)
+  size_t acc_queue_min = ACC_QUEUE_MIN_LEN;  // KZGMI_ACC_QUEUE_MIN: shortest queue chunk (entries)
   bool sort_split = false;     // KZGMI_SORT_SPLIT: split coarse-pass entries at every size (tests)
   int wbits_env = 0;           // KZGMI_WBITS: 13 or 16 forces the window width (tests, A/B)
   double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
@@ -262,7 +263,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   size_t acc_threads = 0;
   if (kAcc29<Cv> && c->acc_queue > 1 && cap && nchunks == cap && cap % 256 == 0) {
     acc_threads = cap;
-    nchunks = std::min(cap * (size_t)c->acc_queue, std::max(cap, emax / ACC_QUEUE_MIN_LEN));
+    nchunks = std::min(cap * (size_t)c->acc_queue, std::max(cap, emax / c->acc_queue_min));
     if (nchunks <= cap) acc_threads = 0;
   }
   nchunks = (nchunks + 255) / 256 * 256;  // = the launched thread count (part arrays indexed by thread)
@@ -624,6 +625,7 @@ int kzgmi_ctx_create(kzgmi_ctx** out, int device_id, int pipeline_slots) {
     c->ncu = ncu;
   if (const char* e = getenv("KZGMI_ACC_THREADS")) c->acc_threads_env = (size_t)strtoull(e, nullptr, 10);
   if (const char* e = getenv("KZGMI_ACC_QUEUE")) c->acc_queue = atoi(e);
+  if (const char* e = getenv("KZGMI_ACC_QUEUE_MIN")) c->acc_queue_min = std::max<size_t>(4, strtoull(e, nullptr, 10));
   if (const char* e = getenv("KZGMI_SORT_SPLIT")) c->sort_split = atoi(e) != 0;
   if (const char* e = getenv("KZGMI_WBITS")) c->wbits_env = atoi(e);
   c->slots.resize(pipeline_slots);

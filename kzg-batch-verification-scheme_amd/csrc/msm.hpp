@@ -592,7 +592,7 @@ KZ_DEV Xyzz<Cv> load_xyzz(const Xyzz<Cv>* src) {
 #define KZ_ACC_QUEUE_FACTOR 2
 #endif
 constexpr int ACC_QUEUE_FACTOR = KZ_ACC_QUEUE_FACTOR;
-constexpr size_t ACC_QUEUE_MIN_LEN = 32;
+constexpr size_t ACC_QUEUE_MIN_LEN = 64;
 KZ_DEV uint32_t acc_chunk_len(uint32_t total, uint32_t nthreads) {
   const uint32_t per = ((total + nthreads - 1) / nthreads + 3) & ~3u;
   return per > 4u ? per : 4u;
