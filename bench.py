@@ -75,14 +75,41 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def gen_inputs(ctx, curve, n, seed):
+def gen_inputs(ctx, curve, n, seed, tau=None):
     g1b = 2 * kzgmi.FP_BYTES[curve]
     C = torch.empty(n * g1b, dtype=torch.uint8, device="cuda")
     P = torch.empty(n * g1b, dtype=torch.uint8, device="cuda")
     z = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
     y = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
-    ctx.gen_tuples(curve, TAU, seed, n, C, z, y, P)
+    ctx.gen_tuples(curve, TAU if tau is None else tau, seed, n, C, z, y, P)
     return C, z, y, P
+
+
+def pipelined_rate(ctx, slots, steps, submit, sync=None):
+    """Batches per second of `steps` calls submit(slot) issued round-robin over `slots` slots (each
+    slot's previous verdict collected -- and asserted -- before it is reused), after one warm-up
+    pass over every slot; synchronize + host clock on both sides of the timed loop."""
+    import torch
+    pend = [False] * slots
+
+    def go(count):
+        for k in range(count):
+            s = k % slots
+            if pend[s]:
+                assert ctx.wait(s), "batch rejected"
+            submit(s)
+            pend[s] = True
+        for s in range(slots):
+            if pend[s]:
+                assert ctx.wait(s), "batch rejected"
+                pend[s] = False
+
+    go(min(slots, steps))
+    (sync or torch.cuda.synchronize)()
+    a = time.perf_counter()
+    go(steps)
+    (sync or torch.cuda.synchronize)()
+    return steps / (time.perf_counter() - a)
 
 
 def _read(path):
@@ -222,7 +249,7 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20, help="tuples per GPU")
     ap.add_argument("--curve", default="bls12_381", choices=["bls12_381", "bn254"])
     ap.add_argument("--slots", type=int, default=0,
-                    help="batches in flight (default 16 single-GPU; sharded 8 + 2 combine lanes)")
+                    help="batches in flight per GPU (default 16; sharded runs chain each combine on its slot)")
     ap.add_argument("--msm-steps", type=int, default=96,
                     help="configs[1]: pipelined 2^20 MSMs timed (the drain of the last in-flight MSMs is "
                          "inside the region: 24 steps read 356-358 M pts/s, 96 steps 372-374, tools/msm_steps_check.sh; 0 = skip)")
@@ -244,6 +271,15 @@ def main():
                     help="timed regions in a row (value = the first; their median in secondary)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU pipeline (RCCL all-gather per batch) even at world size 1")
+    ap.add_argument("--h2d-steps", type=int, default=48,
+                    help="secondary.h2d_inclusive: pipelined batches from host buffers (pinned; the pageable "
+                         "form runs half as many; 0 = skip)")
+    ap.add_argument("--bn254-steps", type=int, default=48,
+                    help="secondary.bn254_cfg4: pipelined BN254 batches at configs[4]'s per-GPU shard (2^19) "
+                         "and a third as many at 2^22 (0 = skip)")
+    ap.add_argument("--shard17-steps", type=int, default=240,
+                    help="secondary.sharded_2e17_world1: 2^17-tuple batches (configs[2]'s 8-way per-rank share) "
+                         "through ShardedPipeline + RCCL at world 1, and unsharded (0 = skip)")
     ap.add_argument("--strong-steps", type=int, default=0,
                     help="sharded runs: batches of the strong-scaled leg (one --n batch split over the ranks; "
                          "default = --steps)")
@@ -274,8 +310,8 @@ def main():
     # measured (profiles/r01/slots_sweep.txt, sharded_sweep.txt): single 12 slots; sharded at
     # world 1 over RCCL, 6/8/10 slots + 2 combine lanes: 135.0/136.3/134.3 batch-verifies/s,
     # MSM 193/217/220 M pts/s (12+2 streams exceed the hardware queues: 70/s)
-    slots = args.slots if args.slots else (8 if sharded else 16)
-    lanes = 2 if sharded else 0
+    slots = args.slots if args.slots else 16
+    lanes = 0  # the eager ShardedPipeline schedule chains each combine on its partial's slot
     ctx = kzgmi.Context(local, slots + lanes)  # + the combine lanes
     g2 = kzgmi.G2_GENERATOR[curve]
     tg2 = ctx.g2_mul(curve, g2, TAU)
@@ -291,6 +327,8 @@ def main():
     torch.cuda.synchronize()
     log("[rank %d] generated %d tuples in %.2f s" % (rank, n, time.perf_counter() - t0))
     pipe = ShardedPipeline(ctx, srs, slots, lanes) if sharded else None
+    # host copies of the batch (the H2D-inclusive leg and the CPU baseline)
+    host_np = None
 
     def step_sharded():
         # every rank holds n tuples of a global batch of world*n; one RCCL all-gather per batch,
@@ -578,6 +616,156 @@ def main():
                   "method": "16 resident rows of 2^(16w)-shifted SRS points, one bucket set, "
                             "pipelined over the slots"}
         del ck
+
+    # ---- secondary: the literal drop-in path -- batch_verify from HOST buffers (SURVEY.md 8d
+    # "secondary: includes the H2D copy"; kzgmi_batch_verify_ex_async), pipelined over the slots:
+    # the H2D DMA of one batch runs beside the kernels of the others.  Pinned host memory
+    # (kzgmi_host_alloc) is DMA'd directly; pageable numpy arrays go through the slots' pinned
+    # staging rings (host copy by the library's copy pool).
+    h2d = None
+    if world == 1 and not sharded and args.h2d_steps > 0:
+        g1b = 2 * kzgmi.FP_BYTES[curve]
+        host_np = [t.cpu().numpy() for t in (Cm, z, y, P)]
+        batch_bytes = sum(a.nbytes for a in host_np)
+        pinned = kzgmi.HostBuffer(batch_bytes)
+        views, off = [], 0
+        for a_ in host_np:
+            v = pinned.view(off, a_.nbytes)
+            v[:] = a_
+            views.append(v)
+            off += a_.nbytes
+        # PCIe probe: one batch's bytes pinned -> HBM in one copy (torch, its own stream), median of 5
+        hp = torch.empty(batch_bytes, dtype=torch.uint8, pin_memory=True)
+        dp = torch.empty(batch_bytes, dtype=torch.uint8, device="cuda")
+        cts = []
+        for _ in range(6):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            dp.copy_(hp, non_blocking=True)
+            e1.record()
+            e1.synchronize()
+            cts.append(e0.elapsed_time(e1))
+        copy_ms = statistics.median(cts[1:])
+        del hp, dp
+        rate_pinned = pipelined_rate(ctx, slots, args.h2d_steps,
+                                     lambda s_: ctx.batch_verify_host_async(srs, s_, *views, seed=vseed))
+        rate_pageable = pipelined_rate(ctx, slots, max(1, args.h2d_steps // 2),
+                                       lambda s_: ctx.batch_verify_host_async(srs, s_, *host_np, seed=vseed))
+        # one synchronous host-buffer batch per kind, phases on the slot's stream (h2d = the copy)
+        ctx.set_profiling(True)
+        assert ctx.batch_verify(srs, *views, seed=vseed)
+        ph_pin = ctx.phase_ms()
+        ctx.set_profiling(False)
+        ctx.set_profiling(True)
+        a = time.perf_counter()
+        assert ctx.batch_verify(srs, *host_np, seed=vseed)
+        lat_pageable = 1e3 * (time.perf_counter() - a)
+        ph_page = ctx.phase_ms()
+        ctx.set_profiling(False)
+        kernel_step_ms = 1e3 * elapsed / args.steps
+        bound_ms = max(copy_ms, kernel_step_ms)
+        h2d = {
+            "batch_verifies_per_s_pinned": rate_pinned,
+            "batch_verifies_per_s_pageable": rate_pageable,
+            "steps_pinned": args.h2d_steps, "steps_pageable": max(1, args.h2d_steps // 2),
+            "bytes_per_batch": batch_bytes,
+            "pcie_h2d_GBps": batch_bytes / (copy_ms * 1e-3) / 1e9,
+            "pcie_probe": "one %d-B pinned -> HBM copy (torch non_blocking copy, HIP events), median of 5" % batch_bytes,
+            "copy_ms_per_batch_probe": copy_ms,
+            "h2d_ms_single_batch_pinned": ph_pin.get("h2d"),
+            "h2d_ms_single_batch_pageable": ph_page.get("h2d"),
+            "single_batch_latency_ms_pageable": lat_pageable,
+            "kernel_ms_per_step_hbm_resident": kernel_step_ms,
+            "bound_ms_per_batch": bound_ms,
+            "bound_batch_verifies_per_s": 1e3 / bound_ms,
+            "frac_of_bound_pinned": rate_pinned * bound_ms / 1e3,
+            "bound_note": "pipelined host-buffer batches can run no faster than max(PCIe copy of one batch, the "
+                          "HBM-resident pipelined step): the copy engine and the CUs overlap across slots",
+            "method": "kzgmi_batch_verify_ex_async over %d slots (pinned: kzgmi_host_alloc block, DMA on the slot's "
+                      "stream; pageable: numpy arrays staged through each slot's pinned ring by the library's copy "
+                      "pool, %s threads), every verdict asserted" % (slots, os.environ.get("KZGMI_COPY_THREADS", "8")),
+        }
+        pinned.free()
+
+    # ---- secondary: configs[2] split 8 ways -- 2^17-tuple batches at world 1 through the real
+    # multi-GPU path (ShardedPipeline: partial + RCCL all-gather + combine per batch) and
+    # unsharded; their ratio to `value` projects the 8-GPU strong speed-up of one 2^20 batch
+    shard17 = None
+    if world == 1 and not sharded and args.shard17_steps > 0 and n >= (1 << 17):
+        n17 = 1 << 17
+        g1b = 2 * kzgmi.FP_BYTES[curve]
+        v17 = (Cm[: n17 * g1b], z[: n17 * 32], y[: n17 * 32], P[: n17 * g1b])
+        rate_unsharded = pipelined_rate(ctx, slots, args.shard17_steps,
+                                        lambda s_: ctx.batch_verify_async(srs, s_, *v17, n17, seed=vseed))
+        own_pg = not dist.is_initialized()
+        if own_pg:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29541")
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+        res17 = {}
+        for mode, (sl17, ln17) in (("eager", (16, 0)), ("eager8", (8, 0)), ("deferred", (8, 2))):
+            pipe17 = ShardedPipeline(ctx, srs, sl17, ln17, eager=mode != "deferred")
+
+            def sub17():
+                for ok in pipe17.submit(*v17, n17, 0, vseed):
+                    assert ok, "batch rejected"
+            for _ in range(sl17):
+                sub17()
+            assert all(pipe17.drain())
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            for _ in range(args.shard17_steps):
+                sub17()
+            assert all(pipe17.drain())
+            torch.cuda.synchronize()
+            res17[mode] = args.shard17_steps / (time.perf_counter() - a)
+            del pipe17
+        if own_pg:
+            dist.destroy_process_group()
+        shard17 = {
+            "n_per_rank": n17, "steps": args.shard17_steps,
+            "batch_verifies_per_s_sharded_rccl_world1": res17["eager"],
+            "batch_verifies_per_s_sharded_eager_8_slots": res17["eager8"],
+            "batch_verifies_per_s_sharded_deferred": res17["deferred"],
+            "batch_verifies_per_s_unsharded": rate_unsharded,
+            "projected_8gpu_strong_speedup": res17["eager"] / value,
+            "projection_note": "one 2^20 batch split 8 ways runs one 2^17 shard per GPU plus an all-gather of 2 "
+                               "partial records per rank; per-rank rate measured here through the same RCCL path at "
+                               "world 1, over this run's 2^20 value",
+            "method": "kzgmi.distributed.ShardedPipeline, eager schedule on all %d slots (the all-gather and the "
+                      "combine + pairing of a batch enqueued right behind its partial, ordered on the GPU by "
+                      "kzgmi_slot_signal, the combine chained on the partial's slot); also eager on 8 slots and the "
+                      "deferred schedule (host waits each partial; 8 slots + 2 combine lanes); unsharded: "
+                      "kzgmi_batch_verify_device_async over %d slots" % (slots, slots),
+        }
+
+    # ---- secondary: configs[4] (BASELINE.json:11) on one GPU: BN254 batches at the 8-GPU run's
+    # per-GPU shard (2^19 tuples) and whole (2^22), pipelined over the slots, GLV (cofactor 1)
+    bn = None
+    if world == 1 and not sharded and args.bn254_steps > 0 and curve == "bls12_381":
+        bn = {}
+        g2b = kzgmi.G2_GENERATOR["bn254"]
+        tg2b = ctx.g2_mul("bn254", g2b, TAU % (1 << 250))
+        srs_b = ctx.load_srs("bn254", g2b, tg2b)
+        nb = 1 << 22
+        ctx.reserve("bn254", nb)
+        Cb, zb, yb, Pb = gen_inputs(ctx, "bn254", nb, hashlib.sha256(b"kzgmi-bench-bn254").digest(), TAU % (1 << 250))
+        for key, nn_, st_ in (("n2e19_per_gpu_shard", 1 << 19, args.bn254_steps),
+                              ("n2e22_whole", nb, max(1, args.bn254_steps // 3))):
+            vb = (Cb[: nn_ * 64], zb[: nn_ * 32], yb[: nn_ * 32], Pb[: nn_ * 64])
+            rate_b = pipelined_rate(ctx, slots, st_, lambda s_: ctx.batch_verify_async(srs_b, s_, *vb, nn_, seed=vseed))
+            ctx.set_profiling(True)
+            a = time.perf_counter()
+            assert ctx.batch_verify(srs_b, *vb, seed=vseed, n=nn_)
+            lat_b = 1e3 * (time.perf_counter() - a)
+            phb = ctx.phase_ms()
+            ctx.set_profiling(False)
+            bn[key] = {"n": nn_, "steps": st_, "batch_verifies_per_s": rate_b, "tuples_per_s": rate_b * nn_,
+                       "single_batch_latency_ms": lat_b, "phase_ms_single_batch": phb}
+        bn["method"] = ("BN254 toy-tau tuples generated on the GPU, kzgmi_batch_verify_device_async over %d slots "
+                        "(GLV split: BN254's G1 has cofactor 1)" % slots)
+        bn["projected_8gpu_whole_batch_per_s"] = bn["n2e19_per_gpu_shard"]["batch_verifies_per_s"]
+        del Cb, zb, yb, Pb, srs_b
 
     # ---- secondary: G1 MSM pts/s at n points per GPU (commitments as points, z as scalars),
     # pipelined over the same slots as the batch verifications (configs[1] throughput); once as
@@ -876,6 +1064,9 @@ def main():
             "fiat_shamir": fsm,
             "prover_commit": commit,
             "cfg4_msm_2e24": cfg4,
+            "h2d_inclusive": h2d,
+            "sharded_2e17_world1": shard17,
+            "bn254_cfg4": bn,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu and "value" in cpu else None,
             "gpu_vs_cpu_note": "against the unoptimised oracle on %s CPUs (see cpu_baseline.sample), not a tuned "
                                "CPU verifier" % ((cpu or {}).get("cores")),

@@ -47,10 +47,16 @@ int main(int argc, char** argv) {
   unsigned char* pf = slurp(argv[8], n * g1b);
   unsigned char* seed = slurp(argv[9], 32);
 
+  /* a library built for another ABI revision must not be bound (include/kzgmi.h) */
+  if (kzgmi_abi_version() != KZGMI_ABI_VERSION) {
+    fprintf(stderr, "libkzgmi ABI %d, this program was built for %d\n", kzgmi_abi_version(), KZGMI_ABI_VERSION);
+    return 2;
+  }
   kzgmi_ctx* ctx = NULL;
   kzgmi_srs* srs = NULL;
   int ok = -1;
-  int rc = kzgmi_ctx_create(&ctx, 0, 1);
+  const int devices[1] = {0};
+  int rc = kzgmi_ctx_create(&ctx, devices, 1, 1);
   if (!rc) rc = kzgmi_srs_load(ctx, curve, NULL, g2, tg2, &srs);
   if (!rc) rc = kzgmi_batch_verify(ctx, srs, cm, zs, ys, pf, n, seed, &ok);
   unsigned char a[96], b[96];

@@ -48,9 +48,13 @@ typedef enum { KZGMI_BLS12_381 = 0, KZGMI_BN254 = 1 } kzgmi_curve;
 
 /* ABI revision of this header.  2: kzgmi_srs_load gained the g1 argument (3rd position),
  * kzgmi_ctx_reserve / kzgmi_alloc_count / kzgmi_abi_version were added.  3: kzgmi_pairing
- * returns the standard e(P, Q) on BLS12-381 (was its cube).  A caller built
- * against another revision must not bind the library: compare with kzgmi_abi_version(). */
-#define KZGMI_ABI_VERSION 3
+ * returns the standard e(P, Q) on BLS12-381 (was its cube).  4: kzgmi_ctx_create takes the
+ * SURVEY.md 8b device list (the single-device form is kzgmi_ctx_create_device; the ABI-3
+ * kzgmi_ctx_create_multi is gone), and the pipelined host-buffer entry
+ * kzgmi_batch_verify_ex_async, the pinned-host helpers kzgmi_host_* and kzgmi_slot_signal were
+ * added.  A caller built against another revision must not bind the library: compare with
+ * kzgmi_abi_version(). */
+#define KZGMI_ABI_VERSION 4
 
 #define KZGMI_OK 0
 #define KZGMI_ERR_ARG (-1)
@@ -90,31 +94,34 @@ int kzgmi_abi_version(void);
 /* Thread-local description of the last error. */
 const char* kzgmi_last_error(void);
 
-/* SURVEY.md 8b kzgmi_ctx_create, single device: bind device `device_id` (>= 0).  `pipeline_slots` >= 1 is
- * the number of independent workspaces/streams for the async batch API (1 is enough for
- * the synchronous calls), at most 64; each holds ~1 GiB at n = 2^20. */
-int kzgmi_ctx_create(kzgmi_ctx** out, int device_id, int pipeline_slots);
+/* SURVEY.md 8b kzgmi_ctx_create(out, device_ids, n_devices), plus the pipeline depth: one
+ * context over a device list (one process driving several GPUs; a device id may repeat;
+ * n_devices = 1 is the common single-GPU context).  device_ids[0] is the primary device: every
+ * single-device entry point below runs there.  `pipeline_slots` >= 1 (at most 64) is the number
+ * of independent workspaces/streams for the async entry points on the primary (1 is enough for
+ * the synchronous calls); each holds ~1.3 GiB at n = 2^20.  With n_devices > 1 the host-buffer
+ * entry points kzgmi_batch_verify / kzgmi_batch_verify_ex / kzgmi_msm_g1 split their input by
+ * point range over all devices (balanced, in units of 4096), run the shards concurrently and
+ * combine the partial sums on the primary; kzgmi_batch_verify_multi_device /
+ * kzgmi_msm_g1_multi_device take shards already resident on each device.  The exchange is 2
+ * (batch) or 1 (MSM) partial records per device, copied to the primary with hipMemcpyPeerAsync
+ * (xGMI) on the primary's slot-0 stream after every shard completed; processes that own one GPU
+ * each instead all-gather kzgmi_batch_partial_device records over RCCL.  Peer
+ * devices get one workspace each (their shard). */
+int kzgmi_ctx_create(kzgmi_ctx** out, const int* device_ids, int n_devices, int pipeline_slots);
+/* The n_devices = 1 case of kzgmi_ctx_create, by device id (>= 0). */
+int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots);
 void kzgmi_ctx_destroy(kzgmi_ctx* ctx);
-
-/* SURVEY.md 8b kzgmi_ctx_create(out, device_ids, n_devices): one context over a device list
- * (one process driving several GPUs; a device id may repeat).  device_ids[0] is the primary
- * device: every single-device entry point below runs there.  The host-buffer entry points
- * kzgmi_batch_verify / kzgmi_batch_verify_ex / kzgmi_msm_g1 split their input by point range
- * over all devices (balanced, in units of 4096), run the shards concurrently and combine the
- * partial sums on the primary; kzgmi_batch_verify_multi_device / kzgmi_msm_g1_multi_device take
- * shards already resident on each device.  The exchange is 2 (batch) or 1 (MSM) partial
- * records per device, copied to the primary with hipMemcpyPeerAsync (xGMI) on the primary's
- * slot-0 stream after every shard completed; processes that own one GPU each instead
- * all-gather kzgmi_batch_partial_device records over RCCL.  Peer devices get
- * one workspace each (their shard); pipeline_slots applies to the primary. */
-int kzgmi_ctx_create_multi(kzgmi_ctx** out, const int* device_ids, int n_devices, int pipeline_slots);
 int kzgmi_ctx_num_devices(const kzgmi_ctx* ctx);
 
 /* Size every pipeline slot's device workspace (and, on a multi-device context, each device's
  * shard workspace) for batches of up to n tuples of `curve` verified with `flags`
  * (KZGMI_FLAG_*), and create the profiling events, so that later batch calls of at most that
  * size and mode allocate nothing.  Workspaces otherwise grow on first use; a caller timing a
- * steady state calls this first.  No job may be in flight. */
+ * steady state calls this first.  No job may be in flight.  On a multi-device context each
+ * peer is sized for its share of the library's own balanced split (what the host-buffer entry
+ * points use): shards passed to kzgmi_batch_verify_multi_device that are larger than
+ * ceil(n / n_devices) rounded up to 4096 still grow the peer's workspace on first use. */
 int kzgmi_ctx_reserve(kzgmi_ctx* ctx, kzgmi_curve curve, size_t n, uint32_t flags);
 /* Process-wide number of device workspace allocations the library has made so far (a timed
  * region that leaves it unchanged allocated nothing). */
@@ -123,6 +130,23 @@ uint64_t kzgmi_alloc_count(void);
 /* Order slot `slot`'s stream after all work enqueued so far on `hip_stream` (a hipStream_t of
  * the ctx's primary device, passed as void*; NULL = the null stream), without a host sync. */
 int kzgmi_stream_wait(kzgmi_ctx* ctx, int slot, void* hip_stream);
+/* The other direction: order all work enqueued later on `hip_stream` (a hipStream_t of the
+ * primary device; NULL = the null stream) after everything enqueued so far on slot `slot`,
+ * without a host sync -- e.g. an RCCL all-gather of a kzgmi_batch_partial_device_async partial
+ * issued on the caller's stream.  The slot's job still completes (and reports its errors) with
+ * kzgmi_slot_wait. */
+int kzgmi_slot_signal(kzgmi_ctx* ctx, int slot, void* hip_stream);
+
+/* Page-locked host memory for the host-buffer entry points: input arrays that lie inside a
+ * kzgmi_host_alloc block or a kzgmi_host_register'ed range are copied to HBM by DMA on the
+ * slot's stream, asynchronously (PCIe at full rate, overlapped with other slots' kernels).
+ * Other (pageable) host memory is first copied by the calling thread(s) into the slot's own
+ * pinned staging ring.  kzgmi_host_register pins an existing allocation (hipHostRegister);
+ * unregister/free only when no job reading it is in flight. */
+int kzgmi_host_alloc(size_t bytes, void** out);
+void kzgmi_host_free(void* p);
+int kzgmi_host_register(void* p, size_t bytes);
+int kzgmi_host_unregister(void* p);
 
 /* SURVEY.md 8b kzgmi_srs_load (BASELINE.json:5 "srs" = {G1, [1]_2, [tau]_2}): host encodings
  * of the SRS's G1 element g1 (the base of the -t G1 term; validated, must be a G1 member
@@ -133,7 +157,8 @@ int kzgmi_srs_load(kzgmi_ctx* ctx, kzgmi_curve curve, const uint8_t* g1, const u
 void kzgmi_srs_free(kzgmi_srs* srs);
 
 /* BASELINE.json:5 batch_verify(commitments, zs, ys, proofs, srs) -- host buffers (copied to
- * HBM, i.e. the PCIe-inclusive path).  *ok_out = 1 accept, 0 reject. */
+ * HBM, i.e. the PCIe-inclusive path; see kzgmi_batch_verify_ex_async for how).  *ok_out = 1
+ * accept, 0 reject. */
 int kzgmi_batch_verify(kzgmi_ctx* ctx, const kzgmi_srs* srs, const uint8_t* commitments,
                        const uint8_t* zs, const uint8_t* ys, const uint8_t* proofs, size_t n,
                        const uint8_t* seed32, int* ok_out);
@@ -162,8 +187,21 @@ int kzgmi_batch_verify_device_ex_async(kzgmi_ctx* ctx, const kzgmi_srs* srs, int
                                        const void* d_commitments, const void* d_zs,
                                        const void* d_ys, const void* d_proofs, size_t n,
                                        const uint8_t* seed32, uint32_t flags);
+/* BASELINE.json:5 batch_verify from HOST buffers, pipelined: the H2D copy of the four arrays is
+ * enqueued on slot `slot`'s stream ahead of the batch's kernels, so the copy of one batch runs
+ * beside the kernels of the batches on the other slots; kzgmi_slot_wait() returns the verdict.
+ * Arrays inside pinned memory (kzgmi_host_alloc / kzgmi_host_register) are DMA'd directly and
+ * the call returns at once -- they must stay allocated and unmodified until the wait returns.
+ * Pageable arrays are copied through the slot's pinned staging ring before the call returns
+ * (they may be reused at once; the call then costs the host-side copy).  Single-device
+ * contexts only (a multi-device context shards host buffers in kzgmi_batch_verify_ex).
+ * kzgmi_batch_verify / kzgmi_batch_verify_ex are this on slot 0 followed by the wait. */
+int kzgmi_batch_verify_ex_async(kzgmi_ctx* ctx, const kzgmi_srs* srs, int slot,
+                                const uint8_t* commitments, const uint8_t* zs, const uint8_t* ys,
+                                const uint8_t* proofs, size_t n, const uint8_t* seed32,
+                                uint32_t flags);
 
-/* Multi-device context (kzgmi_ctx_create_multi): device d holds n_per_device[d] tuples
+/* Multi-device context (kzgmi_ctx_create with n_devices > 1): device d holds n_per_device[d] tuples
  * (global indices follow device order) at d_*[d], device pointers on device_ids[d].  flags as
  * kzgmi_batch_verify_ex; with KZGMI_FLAG_FIAT_SHAMIR every non-empty shard but the last must
  * hold a multiple of 4096 tuples.  Synchronous. */
@@ -274,6 +312,8 @@ int kzgmi_commit_device_async(kzgmi_ctx* ctx, const kzgmi_ck* ck, int slot, cons
  * 3^-1 mod r first, so the result is the standard e(P, Q) -- for P outside G1 it is not.) */
 int kzgmi_pairing(kzgmi_ctx* ctx, kzgmi_curve curve, const uint8_t* g1, const uint8_t* g2,
                   uint8_t* out);
+/* (The 3^-1 scaling runs the library's MSM on one point with the GLV split forced off, so the
+ * result does not depend on kzgmi_set_trusted_g1 / kzgmi_set_glv.) */
 
 /* ---- synthetic-input generators (device side; used by bench.py and GPU tests) ---------
  * d_points_out[i] = k_i * G1 for device scalars k_i (32 B BE each). */

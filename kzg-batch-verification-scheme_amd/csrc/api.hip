@@ -17,6 +17,10 @@
 #include <string>
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <map>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 using namespace kzgmi;
@@ -77,9 +81,14 @@ struct Roctx {
   Roctx& operator=(const Roctx&) = delete;
 };
 
-const char* const kPhaseNames = "convert,scalars,sort,accumulate,reduce,combine,pairing";
-constexpr int kNumPhases = 7;
-enum Phase { PH_CONVERT = 0, PH_SCALARS, PH_SORT, PH_ACCUM, PH_REDUCE, PH_COMBINE, PH_PAIRING };
+// the batch phases in stream order, then "h2d": the host-to-HBM copy of a host-buffer call
+// (kzgmi_batch_verify_ex_async), timed by its own pair of events
+const char* const kPhaseNames = "convert,scalars,sort,accumulate,reduce,combine,pairing,h2d";
+constexpr int kNumPhases = 8;
+constexpr int kNumBatchPhases = 7;
+enum Phase { PH_CONVERT = 0, PH_SCALARS, PH_SORT, PH_ACCUM, PH_REDUCE, PH_COMBINE, PH_PAIRING, PH_H2D };
+constexpr int EV_H2D0 = kNumBatchPhases + 1, EV_H2D1 = kNumBatchPhases + 2;  // Slot::ev indices
+constexpr size_t kRingBytes = size_t(16) << 20;  // pinned staging ring of pageable host inputs (x 2 per slot)
 
 struct Slot {
   hipStream_t stream = nullptr;
@@ -92,11 +101,17 @@ struct Slot {
   DevBuf digits;                                 // signed window digit codes of every term (msm.hpp)
   int* host_flags = nullptr;  // pinned: [ok, err]
   uint8_t* host_out = nullptr;  // pinned: encoded MSM result of an async MSM job
-  hipEvent_t ev[kNumPhases + 1] = {};
-  hipEvent_t order_ev = nullptr;  // kzgmi_stream_wait: the caller's stream -> this slot's stream
-  bool ev_used[kNumPhases + 1] = {};
+  uint8_t* ring[2] = {};        // pinned staging of pageable host inputs (kRingBytes each, lazily)
+  hipEvent_t ring_ev[2] = {};   // the DMA that last read ring[b]
+  int ring_next = 0;
+  hipEvent_t h2d_ev = nullptr;  // this slot's inputs copied (on the context's H2D stream)
+  hipEvent_t ev[kNumBatchPhases + 3] = {};  // phase marks 0..7, then the H2D pair
+  hipEvent_t order_ev = nullptr;   // kzgmi_stream_wait: the caller's stream -> this slot's stream
+  hipEvent_t signal_ev = nullptr;  // kzgmi_slot_signal: this slot's stream -> the caller's stream
+  bool ev_used[kNumBatchPhases + 3] = {};
   bool pending = false;
   bool partial_job = false;  // pending job produces a partial record, not a verdict
+  int partial_of = 0;        // ... of a batch (1) or an MSM (2): a combine of that kind may chain behind it
   bool msm_job = false;      // pending job is an MSM whose encoded result lands in host_out
   int curve = 0;
 };
@@ -124,13 +139,17 @@ struct kzgmi_ctx {
   bool sort_split = false;     // KZGMI_SORT_SPLIT: split coarse-pass entries at every size (tests)
   int wbits_env = 0;           // KZGMI_WBITS: 13 or 16 forces the window width (tests, A/B)
   double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
+  // host-buffer inputs of every slot are copied on ONE stream, in submission order: each
+  // batch's copy then gets the whole link and completes first-in first-out (16 concurrent
+  // 256-MiB copies on the slots' own streams shared the link and all finished late)
+  hipStream_t h2d_stream = nullptr;
   int phase_calls = 0;
   DevBuf table[2], table_base[2];
   bool table_ready[2] = {false, false};
   DevBuf lines_tmp, tmp;
   DevBuf gath;                       // multi-device: partial records gathered from every device
   DevBuf mdig, mdig_all;             // multi-device Fiat-Shamir: this device's / every device's subtree roots
-  std::vector<kzgmi_ctx*> peers;     // multi-device: contexts of device_ids[1..] (kzgmi_ctx_create_multi)
+  std::vector<kzgmi_ctx*> peers;     // multi-device: contexts of device_ids[1..] (kzgmi_ctx_create, n_devices > 1)
   std::vector<kzgmi_srs*> srs_list;  // live SRS objects: detached (device memory freed) on destroy
   std::vector<kzgmi_ck*> ck_list;    // live commit keys: same
 };
@@ -173,7 +192,7 @@ void mark(kzgmi_ctx* c, Slot& s, int idx) {
 void collect_phases(kzgmi_ctx* c, Slot& s) {
   if (!c->profiling) return;
   // phase k spans from the latest earlier recorded mark to mark k+1
-  for (int k = 0; k < kNumPhases; ++k) {
+  for (int k = 0; k < kNumBatchPhases; ++k) {
     if (!s.ev_used[k + 1]) continue;
     int j = k;
     while (j >= 0 && !s.ev_used[j]) --j;
@@ -181,8 +200,12 @@ void collect_phases(kzgmi_ctx* c, Slot& s) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, s.ev[j], s.ev[k + 1]) == hipSuccess) c->phase_ms[k] += ms;
   }
+  if (s.ev_used[EV_H2D0] && s.ev_used[EV_H2D1]) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, s.ev[EV_H2D0], s.ev[EV_H2D1]) == hipSuccess) c->phase_ms[PH_H2D] += ms;
+  }
   c->phase_calls += 1;
-  for (int k = 0; k <= kNumPhases; ++k) s.ev_used[k] = false;
+  for (bool& u : s.ev_used) u = false;
 }
 
 Seed make_seed(const uint8_t* seed32, uint8_t (&buf)[32]) {
@@ -542,6 +565,7 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
   s.pending = true;
   s.partial_job = d_partial_out != nullptr;
+  s.partial_of = s.partial_job ? 1 : 0;
   s.msm_job = false;
   s.curve = Cv::ID;
   return 0;
@@ -600,6 +624,135 @@ int ensure_table(kzgmi_ctx* c, hipStream_t st) {
   return 0;
 }
 
+// ---------------------------------------------------------------- host buffers (PCIe path)
+// Pinned host ranges the library may DMA from directly: kzgmi_host_alloc blocks and
+// kzgmi_host_register'ed ranges, keyed by start address.
+struct HostRange {
+  uintptr_t hi;
+  bool owned;  // kzgmi_host_alloc (hipHostFree) vs kzgmi_host_register (hipHostUnregister)
+};
+std::mutex g_host_mu;
+std::map<uintptr_t, HostRange> g_host;
+
+bool host_pinned(const void* p, size_t bytes) {
+  const uintptr_t a = (uintptr_t)p;
+  std::lock_guard<std::mutex> lk(g_host_mu);
+  auto it = g_host.upper_bound(a);
+  if (it == g_host.begin()) return false;
+  --it;
+  return a >= it->first && a + bytes <= it->second.hi;
+}
+
+// Parallel memcpy for pageable -> pinned staging: one memcpy thread reaches ~10-20 GB/s, below
+// PCIe Gen5's ~50 GB/s, so the copy is split over KZGMI_COPY_THREADS workers (default 8) plus
+// the caller.  One job at a time (contexts on several host threads take turns).
+class CopyPool {
+ public:
+  void copy(void* dst, const void* src, size_t len) {
+    if (len < (size_t(2) << 20) || threads() <= 1) {
+      memcpy(dst, src, len);
+      return;
+    }
+    std::lock_guard<std::mutex> job(job_mu_);
+    start();
+    const int parts = (int)workers_.size() + 1;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      dst_ = (uint8_t*)dst;
+      src_ = (const uint8_t*)src;
+      len_ = len;
+      parts_ = parts;
+      left_ = parts - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    part(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return left_ == 0; });
+  }
+
+ private:
+  int threads() {
+    if (nthreads_ < 0) {
+      const char* e = getenv("KZGMI_COPY_THREADS");
+      nthreads_ = e ? std::max(1, atoi(e)) : 8;
+    }
+    return nthreads_;
+  }
+  void start() {
+    if (!workers_.empty()) return;
+    for (int i = 1; i < nthreads_; ++i) {
+      workers_.emplace_back([this, i] { loop(i); });
+      workers_.back().detach();  // the pool lives as long as the process (never destroyed)
+    }
+  }
+  void part(int i) {
+    const size_t per = (len_ / parts_ + 63) & ~size_t(63);
+    const size_t lo = std::min(len_, per * i), hi = std::min(len_, per * (i + 1));
+    if (hi > lo) memcpy(dst_ + lo, src_ + lo, hi - lo);
+  }
+  void loop(int i) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+      }
+      part(i);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--left_ == 0) done_.notify_one();
+    }
+  }
+  int nthreads_ = -1;
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> workers_;
+  uint8_t* dst_ = nullptr;
+  const uint8_t* src_ = nullptr;
+  size_t len_ = 0;
+  int parts_ = 1, left_ = 0;
+  uint64_t gen_ = 0;
+};
+CopyPool* copy_pool() {
+  static CopyPool* p = new CopyPool();  // never destroyed: its workers are detached
+  return p;
+}
+
+// enqueue host -> device on the copy stream cs: pinned ranges by DMA directly (asynchronous);
+// pageable ones through the slot's two pinned ring buffers, the host copy of chunk k+1
+// overlapping the DMA of chunk k (the call returns when the last chunk is staged)
+int h2d(Slot& s, hipStream_t cs, void* dst, const void* src, size_t bytes) {
+  if (!bytes) return 0;
+  if (host_pinned(src, bytes)) {
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, cs));
+    return 0;
+  }
+  for (int b = 0; b < 2; ++b) {
+    if (!s.ring[b]) {
+      if (hipHostMalloc((void**)&s.ring[b], kRingBytes, hipHostMallocDefault) != hipSuccess) {
+        s.ring[b] = nullptr;
+        return fail(KZGMI_ERR_OOM, "pinned staging allocation failed");
+      }
+      g_allocs.fetch_add(1, std::memory_order_relaxed);
+    }
+    if (!s.ring_ev[b]) {
+      HIPCHK(hipEventCreateWithFlags(&s.ring_ev[b], hipEventDisableTiming));
+      HIPCHK(hipEventRecord(s.ring_ev[b], cs));  // so the first wait on it has a record
+    }
+  }
+  for (size_t off = 0; off < bytes; off += kRingBytes) {
+    const size_t len = std::min(kRingBytes, bytes - off);
+    const int b = s.ring_next;
+    s.ring_next ^= 1;
+    HIPCHK(hipEventSynchronize(s.ring_ev[b]));  // its previous DMA has read it
+    copy_pool()->copy(s.ring[b], (const uint8_t*)src + off, len);
+    HIPCHK(hipMemcpyAsync((uint8_t*)dst + off, s.ring[b], len, hipMemcpyHostToDevice, cs));
+    HIPCHK(hipEventRecord(s.ring_ev[b], cs));
+  }
+  return 0;
+}
+
 }  // namespace
 
 // ================================================================================ C ABI
@@ -611,7 +764,7 @@ uint64_t kzgmi_alloc_count(void) { return g_allocs.load(std::memory_order_relaxe
 const char* kzgmi_last_error(void) { return g_err.c_str(); }
 const char* kzgmi_phase_names(void) { return kPhaseNames; }
 
-int kzgmi_ctx_create(kzgmi_ctx** out, int device_id, int pipeline_slots) {
+int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) {
   if (!out || device_id < 0 || pipeline_slots < 1 || pipeline_slots > 64) return fail(KZGMI_ERR_ARG, "bad ctx args");
   *out = nullptr;
   int ndev = 0;
@@ -654,11 +807,21 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
     for (auto& e : s.ev)
       if (e) (void)hipEventDestroy(e);
     if (s.order_ev) (void)hipEventDestroy(s.order_ev);
+    if (s.signal_ev) (void)hipEventDestroy(s.signal_ev);
+    if (s.h2d_ev) (void)hipEventDestroy(s.h2d_ev);
+    for (int b = 0; b < 2; ++b) {
+      if (s.ring_ev[b]) (void)hipEventDestroy(s.ring_ev[b]);
+      if (s.ring[b]) (void)hipHostFree(s.ring[b]);
+    }
     if (s.host_flags) (void)hipHostFree(s.host_flags);
     if (s.host_out) (void)hipHostFree(s.host_out);
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
   for (int k = 0; k < 2; ++k) { c->table[k].release(); c->table_base[k].release(); }
+  if (c->h2d_stream) {
+    (void)hipStreamSynchronize(c->h2d_stream);
+    (void)hipStreamDestroy(c->h2d_stream);
+  }
   c->lines_tmp.release();
   c->tmp.release();
   for (kzgmi_ck* ck : c->ck_list) {  // detach: later kzgmi_ck_free() only deletes the struct
@@ -826,6 +989,7 @@ int kzgmi_batch_verify_device_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int s
     s.host_flags[1] = 0;
     s.pending = true;
     s.partial_job = false;
+    s.partial_of = 0;
     s.msm_job = false;
     return 0;
   }
@@ -863,23 +1027,98 @@ int kzgmi_batch_verify_ex(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* com
   if (n && (!commitments || !zs || !ys || !proofs)) return fail(KZGMI_ERR_ARG, "null input");
   CHK(slot0_idle(c));
   if (!c->peers.empty()) return batch_multi_host(c, srs, commitments, zs, ys, proofs, n, seed32, flags, ok_out);
-  Slot& s = c->slots[0];
-  uint8_t *dC = nullptr, *dpi = nullptr, *dz = nullptr, *dy = nullptr;
-  if (n) {
-    const size_t gb = (flags & KZGMI_FLAG_COMPRESSED) ? g1_bytes(srs->curve) / 2 : g1_bytes(srs->curve);
-    CHK(s.stage.ensure(n * (2 * gb + 64)));
-    uint8_t* base = s.stage.template as<uint8_t>();
-    dC = base;
-    dpi = base + n * gb;
-    dz = base + 2 * n * gb;
-    dy = dz + 32 * n;
-    HIPCHK(hipMemcpyAsync(dC, commitments, n * gb, hipMemcpyHostToDevice, s.stream));
-    HIPCHK(hipMemcpyAsync(dpi, proofs, n * gb, hipMemcpyHostToDevice, s.stream));
-    HIPCHK(hipMemcpyAsync(dz, zs, n * 32, hipMemcpyHostToDevice, s.stream));
-    HIPCHK(hipMemcpyAsync(dy, ys, n * 32, hipMemcpyHostToDevice, s.stream));
-  }
-  CHK(kzgmi_batch_verify_device_ex_async(c, srs, 0, dC, dz, dy, dpi, n, seed32, flags));
+  CHK(kzgmi_batch_verify_ex_async(c, srs, 0, commitments, zs, ys, proofs, n, seed32, flags));
   return kzgmi_slot_wait(c, 0, ok_out);
+}
+
+int kzgmi_batch_verify_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const uint8_t* commitments,
+                                const uint8_t* zs, const uint8_t* ys, const uint8_t* proofs, size_t n,
+                                const uint8_t* seed32, uint32_t flags) {
+  CHK(check_ctx(c, slot));
+  if (!srs) return fail(KZGMI_ERR_ARG, "null argument");
+  if (srs->ctx != c) return fail(KZGMI_ERR_ARG, "srs does not belong to this context");
+  if (!c->peers.empty())
+    return fail(KZGMI_ERR_ARG, "kzgmi_batch_verify_ex_async: single-device contexts only (use kzgmi_batch_verify_ex)");
+  if (n && (!commitments || !zs || !ys || !proofs)) return fail(KZGMI_ERR_ARG, "null input");
+  if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "batch too large (max 2^26 tuples per call)");
+  if (flags & ~kAllFlags) return fail(KZGMI_ERR_ARG, "unknown flags");
+  Slot& s = c->slots[slot];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_slot_wait first");
+  if (n == 0) return kzgmi_batch_verify_device_ex_async(c, srs, slot, nullptr, nullptr, nullptr, nullptr, 0, seed32, flags);
+  Roctx rx("kzgmi_batch_verify_ex_async");
+  const size_t gb = (flags & KZGMI_FLAG_COMPRESSED) ? g1_bytes(srs->curve) / 2 : g1_bytes(srs->curve);
+  CHK(s.stage.ensure(n * (2 * gb + 64)));
+  uint8_t* dC = s.stage.template as<uint8_t>();
+  uint8_t* dpi = dC + n * gb;
+  uint8_t* dz = dC + 2 * n * gb;
+  uint8_t* dy = dz + 32 * n;
+  if (!c->h2d_stream) HIPCHK(hipStreamCreateWithFlags(&c->h2d_stream, hipStreamNonBlocking));
+  hipStream_t cs = c->h2d_stream;
+  if (!s.h2d_ev) HIPCHK(hipEventCreateWithFlags(&s.h2d_ev, hipEventDisableTiming));
+  // the copy overwrites s.stage: after everything already on the slot's stream
+  HIPCHK(hipEventRecord(s.h2d_ev, s.stream));
+  HIPCHK(hipStreamWaitEvent(cs, s.h2d_ev, 0));
+  if (c->profiling) {
+    if (!s.ev[EV_H2D0]) HIPCHK(hipEventCreate(&s.ev[EV_H2D0]));
+    if (!s.ev[EV_H2D1]) HIPCHK(hipEventCreate(&s.ev[EV_H2D1]));
+    HIPCHK(hipEventRecord(s.ev[EV_H2D0], cs));
+  }
+  CHK(h2d(s, cs, dC, commitments, n * gb));
+  CHK(h2d(s, cs, dpi, proofs, n * gb));
+  CHK(h2d(s, cs, dz, zs, n * 32));
+  CHK(h2d(s, cs, dy, ys, n * 32));
+  if (c->profiling) HIPCHK(hipEventRecord(s.ev[EV_H2D1], cs));
+  HIPCHK(hipEventRecord(s.h2d_ev, cs));  // the batch's kernels wait for its copy only
+  HIPCHK(hipStreamWaitEvent(s.stream, s.h2d_ev, 0));
+  const int r = kzgmi_batch_verify_device_ex_async(c, srs, slot, dC, dz, dy, dpi, n, seed32, flags);
+  if (c->profiling) s.ev_used[EV_H2D0] = s.ev_used[EV_H2D1] = (r == 0);
+  return r;
+}
+
+// ------------------------------------------------------------------------------ pinned host memory
+int kzgmi_host_alloc(size_t bytes, void** out) {
+  if (!out || bytes == 0) return fail(KZGMI_ERR_ARG, "bad argument");
+  *out = nullptr;
+  void* p = nullptr;
+  HIPCHK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+  std::lock_guard<std::mutex> lk(g_host_mu);
+  g_host[(uintptr_t)p] = HostRange{(uintptr_t)p + bytes, true};
+  *out = p;
+  return 0;
+}
+
+void kzgmi_host_free(void* p) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    auto it = g_host.find((uintptr_t)p);
+    if (it == g_host.end() || !it->second.owned) return;  // not ours: leave it alone
+    g_host.erase(it);
+  }
+  (void)hipHostFree(p);
+}
+
+int kzgmi_host_register(void* p, size_t bytes) {
+  if (!p || bytes == 0) return fail(KZGMI_ERR_ARG, "bad argument");
+  {
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    if (g_host.count((uintptr_t)p)) return fail(KZGMI_ERR_ARG, "range already registered");
+  }
+  HIPCHK(hipHostRegister(p, bytes, hipHostRegisterDefault));
+  std::lock_guard<std::mutex> lk(g_host_mu);
+  g_host[(uintptr_t)p] = HostRange{(uintptr_t)p + bytes, false};
+  return 0;
+}
+
+int kzgmi_host_unregister(void* p) {
+  {
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    auto it = g_host.find((uintptr_t)p);
+    if (it == g_host.end() || it->second.owned) return fail(KZGMI_ERR_ARG, "range was not registered");
+    g_host.erase(it);
+  }
+  HIPCHK(hipHostUnregister(p));
+  return 0;
 }
 
 int kzgmi_last_combination(kzgmi_ctx* c, uint8_t* a_out, uint8_t* b_out) {
@@ -907,8 +1146,8 @@ int kzgmi_last_combination(kzgmi_ctx* c, uint8_t* a_out, uint8_t* b_out) {
 }  // extern "C"
 namespace {
 template <class Cv>
-int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t n) {
-  const bool glv = c->glv_msm && (Cv::ID == 1 || c->msm_trusted_g1);
+int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t n, bool allow_glv = true) {
+  const bool glv = allow_glv && c->glv_msm && (Cv::ID == 1 || c->msm_trusted_g1);
   CHK(s.pts.ensure((glv ? 2 : 1) * n * sizeof(Affine<Cv>)));
   CHK(s.inf.ensure((glv ? 2 : 1) * n));
   CHK(s.scal_s.ensure(n * 32));
@@ -1067,6 +1306,7 @@ int kzgmi_commit_device_async(kzgmi_ctx* c, const kzgmi_ck* ck, int slot, const 
     HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
     s.pending = true;
     s.partial_job = false;
+    s.partial_of = 0;
     s.msm_job = true;
     s.curve = Cv::ID;
     return 0;
@@ -1141,6 +1381,7 @@ int kzgmi_msm_g1_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, const v
     }
     s.pending = true;
     s.partial_job = false;
+    s.partial_of = 0;
     s.msm_job = true;
     s.curve = Cv::ID;
     return 0;
@@ -1203,13 +1444,17 @@ int kzgmi_batch_partial_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slo
   return dispatch(srs->curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     if (n == 0) {  // empty shard: both partials are the point at infinity (zz = 0)
+      CHK(s.flags.ensure(16));
       HIPCHK(hipMemsetAsync(d_partial_out, 0, 2 * sizeof(Xyzz<Cv>), s.stream));
+      HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));  // a chained combine keeps the error word
       HIPCHK(hipStreamSynchronize(s.stream));
       s.host_flags[0] = 1;
       s.host_flags[1] = 0;
       s.pending = true;
       s.partial_job = true;
+      s.partial_of = 1;
       s.msm_job = false;
+      s.curve = Cv::ID;
       return 0;
     }
     return enqueue_batch<Cv>(c, s, srs, dC, dz, dy, dpi, n, seed, index_offset, d_partial_out, flags);
@@ -1228,15 +1473,21 @@ int kzgmi_batch_combine_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slo
   CHK(check_ctx(c, slot));
   if (!srs || srs->ctx != c || !d_partials || n_parts < 1) return fail(KZGMI_ERR_ARG, "bad argument");
   Slot& s = c->slots[slot];
-  if (s.pending) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_slot_wait first");
+  // chained: behind this slot's own pending batch partial (one kzgmi_slot_wait completes both;
+  // the partial's error word is kept, the pairing writes the verdict word)
+  const bool chain = s.pending && s.partial_of == 1;
+  if (s.pending && !chain) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_slot_wait first");
+  if (chain && s.curve != srs->curve) return fail(KZGMI_ERR_ARG, "chained combine: curve differs from the partial's");
   return dispatch(srs->curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     using XY = Xyzz<Cv>;
     CHK(s.res.ensure(2 * sizeof(XY)));
     CHK(s.flags.ensure(16));
     hipStream_t st = s.stream;
-    HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
-    mark(c, s, PH_COMBINE);
+    if (!chain) {
+      HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
+      mark(c, s, PH_COMBINE);
+    }
     Launch<Cv>::sum_partials(st, (const XY*)d_partials, (uint32_t)n_parts, 2, 2, s.res.template as<XY>());
     Launch<Cv>::pairing_check(st, s.res.template as<XY>(), srs->lines.template as<Line<Cv>>(),
                               srs->q_inf.template as<uint8_t>(), s.flags.template as<int>());
@@ -1245,6 +1496,7 @@ int kzgmi_batch_combine_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slo
     HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
     s.pending = true;
     s.partial_job = false;
+    s.partial_of = 0;
     s.msm_job = false;
     s.curve = Cv::ID;
     return 0;
@@ -1406,8 +1658,10 @@ int kzgmi_msm_partial_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, co
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     if (n == 0) {
+      CHK(s.flags.ensure(16));
       HIPCHK(hipStreamSynchronize(s.stream));
       HIPCHK(hipMemsetAsync(d_partial_out, 0, sizeof(Xyzz<Cv>), s.stream));  // ZZ = 0: infinity
+      HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));  // a chained combine keeps the error word
       s.host_flags[0] = 1;
       s.host_flags[1] = 0;
     } else {
@@ -1417,6 +1671,7 @@ int kzgmi_msm_partial_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, co
     }
     s.pending = true;
     s.partial_job = true;
+    s.partial_of = 2;
     s.msm_job = false;
     s.curve = Cv::ID;
     return 0;
@@ -1427,7 +1682,9 @@ int kzgmi_msm_combine_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, co
   CHK(check_ctx(c, slot));
   if (!d_partials || n_parts < 1) return fail(KZGMI_ERR_ARG, "bad argument");
   Slot& s = c->slots[slot];
-  if (s.pending) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_msm_wait first");
+  const bool chain = s.pending && s.partial_of == 2;  // behind this slot's own MSM partial
+  if (s.pending && !chain) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_msm_wait first");
+  if (chain && s.curve != (int)curve) return fail(KZGMI_ERR_ARG, "chained combine: curve differs from the partial's");
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     using XY = Xyzz<Cv>;
@@ -1435,7 +1692,7 @@ int kzgmi_msm_combine_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, co
     CHK(s.res.ensure(2 * sizeof(XY)));
     CHK(s.outb.ensure(gb));
     CHK(s.flags.ensure(16));
-    HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));
+    if (!chain) HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));
     Launch<Cv>::sum_partials(s.stream, (const XY*)d_partials, (uint32_t)n_parts, 1, 1, s.res.template as<XY>());
     Launch<Cv>::encode_points(s.stream, s.res.template as<XY>(), 1, s.outb.template as<uint8_t>());
     HIPCHK(hipGetLastError());
@@ -1443,6 +1700,7 @@ int kzgmi_msm_combine_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, co
     HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, s.stream));
     s.pending = true;
     s.partial_job = false;
+    s.partial_of = 0;
     s.msm_job = true;
     s.curve = Cv::ID;
     return 0;
@@ -1476,13 +1734,25 @@ int kzgmi_pairing(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uint
   CHK(slot0_idle(c));
   // BLS12-381: the pairing program's hard part is the x-chain of 3 (p^4 - p^2 + 1) / r, so it
   // yields e(P, Q)^3 (as the oracle and pyspec do); e(P, Q) = e([3^-1 mod r] P, Q)^3 for P in G1,
-  // so P is first scaled by 3^-1 mod r with the library's own (exact, non-GLV) MSM
+  // so P is first scaled by 3^-1 mod r with the library's MSM on one point, GLV forced off (the
+  // GLV split is exact only on G1, and kzgmi_set_trusted_g1 must not change this diagnostic)
   uint8_t g1s[96];
   if (curve == KZGMI_BLS12_381) {
     static const uint8_t kInv3[32] = {0x4d, 0x49, 0x1a, 0x37, 0x71, 0x13, 0xa8, 0xda, 0xcc, 0xd1, 0x3a,
                                       0xb0, 0x06, 0x6b, 0xe5, 0x58, 0xe2, 0x7e, 0x6d, 0x57, 0x55, 0x54,
                                       0x3d, 0x54, 0xaa, 0xaa, 0xaa, 0xaa, 0x00, 0x00, 0x00, 0x01};
-    CHK(kzgmi_msm_g1(c, curve, g1, kInv3, 1, g1s));
+    using Cv = Bls12_381;
+    Slot& s = c->slots[0];
+    CHK(s.stage.ensure(96 + 32));
+    CHK(s.outb.ensure(96));
+    uint8_t* dp = s.stage.template as<uint8_t>();
+    HIPCHK(hipMemcpyAsync(dp, g1, 96, hipMemcpyHostToDevice, s.stream));
+    HIPCHK(hipMemcpyAsync(dp + 96, kInv3, 32, hipMemcpyHostToDevice, s.stream));
+    CHK(enqueue_msm<Cv>(c, s, dp, dp + 96, 1, /*allow_glv=*/false));
+    Launch<Cv>::encode_points(s.stream, s.res.template as<Xyzz<Cv>>(), 1, s.outb.template as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    CHK(read_flags_sync(c, s));
+    HIPCHK(hipMemcpy(g1s, s.outb.p, 96, hipMemcpyDeviceToHost));
     g1 = g1s;
   }
   return dispatch(curve, [&](auto cv) -> int {
@@ -1676,6 +1946,15 @@ int kzgmi_stream_wait(kzgmi_ctx* c, int slot, void* stream) {
   return 0;
 }
 
+int kzgmi_slot_signal(kzgmi_ctx* c, int slot, void* stream) {
+  CHK(check_ctx(c, slot));
+  Slot& s = c->slots[slot];
+  if (!s.signal_ev) HIPCHK(hipEventCreateWithFlags(&s.signal_ev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(s.signal_ev, s.stream));
+  HIPCHK(hipStreamWaitEvent((hipStream_t)stream, s.signal_ev, 0));
+  return 0;
+}
+
 int kzgmi_partial_encode_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_records, size_t count, uint8_t* out) {
   CHK(check_ctx(c));
   if (!d_records || !out || count == 0 || count > 4096) return fail(KZGMI_ERR_ARG, "bad argument");
@@ -1694,14 +1973,14 @@ int kzgmi_partial_encode_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_r
 }
 
 // ------------------------------------------------------------------------------ multi-device context
-int kzgmi_ctx_create_multi(kzgmi_ctx** out, const int* device_ids, int n_devices, int pipeline_slots) {
-  if (!out || !device_ids || n_devices < 1 || n_devices > 64) return fail(KZGMI_ERR_ARG, "bad multi-device ctx args");
+int kzgmi_ctx_create(kzgmi_ctx** out, const int* device_ids, int n_devices, int pipeline_slots) {
+  if (!out || !device_ids || n_devices < 1 || n_devices > 64) return fail(KZGMI_ERR_ARG, "bad ctx args");
   *out = nullptr;
   kzgmi_ctx* c = nullptr;
-  CHK(kzgmi_ctx_create(&c, device_ids[0], pipeline_slots));
+  CHK(kzgmi_ctx_create_device(&c, device_ids[0], pipeline_slots));
   for (int k = 1; k < n_devices; ++k) {
     kzgmi_ctx* p = nullptr;
-    if (int r = kzgmi_ctx_create(&p, device_ids[k], 1)) {  // peers only ever run on their slot 0
+    if (int r = kzgmi_ctx_create_device(&p, device_ids[k], 1)) {  // peers only ever run on their slot 0
       kzgmi_ctx_destroy(c);
       return r;
     }

@@ -22,10 +22,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # KZGMI_LIB selects an alternative build (timing experiments); default: the in-tree library
 LIB_PATH = os.environ.get("KZGMI_LIB") or os.path.join(_HERE, "libkzgmi.so")
 
-ABI_VERSION = 3  # include/kzgmi.h KZGMI_ABI_VERSION
+ABI_VERSION = 4  # include/kzgmi.h KZGMI_ABI_VERSION
 CURVES = {"bls12_381": 0, "bn254": 1}
 FP_BYTES = {"bls12_381": 48, "bn254": 32}
-PHASES = ["convert", "scalars", "sort", "accumulate", "reduce", "combine", "pairing"]
+PHASES = ["convert", "scalars", "sort", "accumulate", "reduce", "combine", "pairing", "h2d"]
 
 ERR_NAMES = {-1: "ARG", -2: "ENCODING", -3: "NOT_ON_CURVE", -4: "SCALAR", -5: "DEVICE", -6: "OOM",
              -7: "NOT_IN_SUBGROUP"}
@@ -61,24 +61,30 @@ def lib():
         "kzgmi_version": ([], c.c_char_p),
         "kzgmi_last_error": ([], c.c_char_p),
         "kzgmi_phase_names": ([], c.c_char_p),
-        "kzgmi_ctx_create": ([c.POINTER(vp), c.c_int, c.c_int], c.c_int),
+        "kzgmi_ctx_create": ([c.POINTER(vp), c.POINTER(c.c_int), c.c_int, c.c_int], c.c_int),
+        "kzgmi_ctx_create_device": ([c.POINTER(vp), c.c_int, c.c_int], c.c_int),
         "kzgmi_ctx_destroy": ([vp], None),
         "kzgmi_srs_load": ([vp, c.c_int, u8p, u8p, u8p, c.POINTER(vp)], c.c_int),
-        "kzgmi_ctx_create_multi": ([c.POINTER(vp), c.POINTER(c.c_int), c.c_int, c.c_int], c.c_int),
         "kzgmi_ctx_num_devices": ([vp], c.c_int),
         "kzgmi_abi_version": ([], c.c_int),
         "kzgmi_ctx_reserve": ([vp, c.c_int, sz, c.c_uint32], c.c_int),
         "kzgmi_alloc_count": ([], c.c_uint64),
         "kzgmi_stream_wait": ([vp, c.c_int, vp], c.c_int),
+        "kzgmi_slot_signal": ([vp, c.c_int, vp], c.c_int),
+        "kzgmi_host_alloc": ([sz, c.POINTER(vp)], c.c_int),
+        "kzgmi_host_free": ([vp], None),
+        "kzgmi_host_register": ([vp, sz], c.c_int),
+        "kzgmi_host_unregister": ([vp], c.c_int),
         "kzgmi_partial_encode_device": ([vp, c.c_int, vp, sz, u8p], c.c_int),
         "kzgmi_batch_verify_multi_device": ([vp, vp, c.POINTER(vp), c.POINTER(vp), c.POINTER(vp), c.POINTER(vp),
                                              c.POINTER(sz), u8p, c.c_uint32, ip], c.c_int),
         "kzgmi_msm_g1_multi_device": ([vp, c.c_int, c.POINTER(vp), c.POINTER(vp), c.POINTER(sz), u8p], c.c_int),
         "kzgmi_srs_free": ([vp], None),
-        "kzgmi_batch_verify": ([vp, vp, u8p, u8p, u8p, u8p, sz, u8p, ip], c.c_int),
+        "kzgmi_batch_verify": ([vp, vp, vp, vp, vp, vp, sz, u8p, ip], c.c_int),
         "kzgmi_batch_verify_device": ([vp, vp, vp, vp, vp, vp, sz, u8p, ip], c.c_int),
         "kzgmi_batch_verify_device_async": ([vp, vp, c.c_int, vp, vp, vp, vp, sz, u8p], c.c_int),
-        "kzgmi_batch_verify_ex": ([vp, vp, u8p, u8p, u8p, u8p, sz, u8p, c.c_uint32, ip], c.c_int),
+        "kzgmi_batch_verify_ex": ([vp, vp, vp, vp, vp, vp, sz, u8p, c.c_uint32, ip], c.c_int),
+        "kzgmi_batch_verify_ex_async": ([vp, vp, c.c_int, vp, vp, vp, vp, sz, u8p, c.c_uint32], c.c_int),
         "kzgmi_batch_verify_device_ex_async": ([vp, vp, c.c_int, vp, vp, vp, vp, sz, u8p, c.c_uint32], c.c_int),
         "kzgmi_g1_validate_device": ([vp, c.c_int, vp, sz, c.c_uint32], c.c_int),
         "kzgmi_g1_compress_device": ([vp, c.c_int, vp, sz, vp], c.c_int),
@@ -91,7 +97,7 @@ def lib():
         "kzgmi_fs_challenge_from_digests_device": ([vp, c.c_int, vp, sz, c.c_uint64, u8p], c.c_int),
         "kzgmi_slot_wait": ([vp, c.c_int, ip], c.c_int),
         "kzgmi_last_combination": ([vp, u8p, u8p], c.c_int),
-        "kzgmi_msm_g1": ([vp, c.c_int, u8p, u8p, sz, u8p], c.c_int),
+        "kzgmi_msm_g1": ([vp, c.c_int, vp, vp, sz, u8p], c.c_int),
         "kzgmi_msm_g1_device": ([vp, c.c_int, vp, vp, sz, u8p], c.c_int),
         "kzgmi_msm_g1_device_async": ([vp, c.c_int, c.c_int, vp, vp, sz], c.c_int),
         "kzgmi_msm_wait": ([vp, c.c_int, u8p], c.c_int),
@@ -129,7 +135,7 @@ def lib():
 
 def exported_symbols():
     return [
-        "kzgmi_version", "kzgmi_last_error", "kzgmi_phase_names", "kzgmi_ctx_create",
+        "kzgmi_version", "kzgmi_last_error", "kzgmi_phase_names", "kzgmi_ctx_create", "kzgmi_ctx_create_device",
         "kzgmi_ctx_destroy", "kzgmi_srs_load", "kzgmi_srs_free", "kzgmi_batch_verify",
         "kzgmi_batch_verify_device", "kzgmi_batch_verify_device_async", "kzgmi_slot_wait",
         "kzgmi_batch_verify_ex", "kzgmi_batch_verify_device_ex_async", "kzgmi_g1_validate_device",
@@ -142,9 +148,10 @@ def exported_symbols():
         "kzgmi_batch_combine_device_async", "kzgmi_msm_partial_device",
         "kzgmi_msm_combine_device", "kzgmi_pairing", "kzgmi_gen_g1", "kzgmi_gen_tuples",
         "kzgmi_g2_mul", "kzgmi_probe_fpmul", "kzgmi_set_profiling", "kzgmi_get_phase_ms",
-        "kzgmi_ctx_create_multi", "kzgmi_ctx_num_devices", "kzgmi_stream_wait", "kzgmi_partial_encode_device",
+        "kzgmi_ctx_num_devices", "kzgmi_stream_wait", "kzgmi_slot_signal", "kzgmi_partial_encode_device",
         "kzgmi_batch_verify_multi_device", "kzgmi_msm_g1_multi_device",
-        "kzgmi_abi_version", "kzgmi_ctx_reserve", "kzgmi_alloc_count",
+        "kzgmi_abi_version", "kzgmi_ctx_reserve", "kzgmi_alloc_count", "kzgmi_batch_verify_ex_async",
+        "kzgmi_host_alloc", "kzgmi_host_free", "kzgmi_host_register", "kzgmi_host_unregister",
     ]
 
 
@@ -208,6 +215,70 @@ def _host_bytes(x) -> bytes:
     raise TypeError("unsupported buffer type %r" % type(x))
 
 
+def _host_ptr(x):
+    """(address, nbytes, keepalive) of a host buffer, without copying it: bytes, bytearray,
+    memoryview, numpy arrays (C-contiguous) and CPU torch tensors.  The keepalive object must
+    outlive every use of the address."""
+    if isinstance(x, bytes):
+        cp = ctypes.c_char_p(x)  # points into the bytes object itself
+        return ctypes.cast(cp, ctypes.c_void_p).value or 0, len(x), (x, cp)
+    if isinstance(x, HostBuffer):
+        return x.ptr, x.nbytes, x
+    import numpy as np
+    if hasattr(x, "data_ptr") and hasattr(x, "is_cuda"):  # torch CPU tensor
+        t = x.detach()
+        if not t.is_contiguous():
+            t = t.contiguous()
+        return t.data_ptr(), t.numel() * t.element_size(), t
+    if isinstance(x, (bytearray, memoryview)):
+        x = np.frombuffer(x, dtype=np.uint8)
+    if isinstance(x, np.ndarray):
+        if not x.flags["C_CONTIGUOUS"]:
+            x = np.ascontiguousarray(x)
+        return x.ctypes.data, x.nbytes, x
+    raise TypeError("unsupported buffer type %r" % type(x))
+
+
+class HostBuffer:
+    """Page-locked host memory from kzgmi_host_alloc: host-buffer batch_verify calls whose arrays
+    live here are DMA'd to HBM at PCIe rate, asynchronously (no staging copy).  `array` is a
+    writable numpy uint8 view; free() (or garbage collection) releases it -- only when no job
+    reading it is in flight."""
+
+    def __init__(self, nbytes: int):
+        import numpy as np
+        p = ctypes.c_void_p()
+        _check(lib().kzgmi_host_alloc(int(nbytes), ctypes.byref(p)))
+        self.ptr, self.nbytes = p.value, int(nbytes)
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def view(self, offset: int, nbytes: int):
+        """numpy view of [offset, offset + nbytes) (also accepted by the host entry points)."""
+        return self.array[offset:offset + nbytes]
+
+    def free(self):
+        if getattr(self, "ptr", None):
+            self.array = None
+            lib().kzgmi_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def register_host(arr) -> None:
+    """Pin an existing C-contiguous numpy array in place (kzgmi_host_register) so host-buffer
+    calls DMA from it directly; unregister_host(arr) before freeing it."""
+    _check(lib().kzgmi_host_register(arr.ctypes.data, arr.nbytes))
+
+
+def unregister_host(arr) -> None:
+    _check(lib().kzgmi_host_unregister(arr.ctypes.data))
+
+
 def _dptr(x, nbytes: Optional[int] = None) -> int:
     """Device pointer of a contiguous tensor holding at least `nbytes` bytes."""
     if not x.is_contiguous():
@@ -256,7 +327,7 @@ class CommitKey:
 
 class Context:
     """One GPU (device_id) with `slots` independent workspaces/streams; or, with
-    devices=[d0, d1, ...], one context over several GPUs (kzgmi_ctx_create_multi: host-buffer
+    devices=[d0, d1, ...], one context over several GPUs (kzgmi_ctx_create's device list: host-buffer
     batch_verify / msm_g1 are sharded over them; d0 is the primary device).
 
     Device-tensor arguments are read on the library's own streams: every call first orders
@@ -265,13 +336,10 @@ class Context:
 
     def __init__(self, device: int = 0, slots: int = 1, devices=None):
         h = ctypes.c_void_p()
-        if devices is not None:
-            devs = [int(d) for d in devices]
-            arr = (ctypes.c_int * len(devs))(*devs)
-            _check(lib().kzgmi_ctx_create_multi(ctypes.byref(h), arr, len(devs), int(slots)))
-            device = devs[0]
-        else:
-            _check(lib().kzgmi_ctx_create(ctypes.byref(h), int(device), int(slots)))
+        devs = [int(d) for d in devices] if devices is not None else [int(device)]
+        arr = (ctypes.c_int * len(devs))(*devs)
+        _check(lib().kzgmi_ctx_create(ctypes.byref(h), arr, len(devs), int(slots)))
+        device = devs[0]
         self.handle = h
         self.device = device
         self.slots = slots
@@ -289,6 +357,12 @@ class Context:
     def _order(self, slot: int = 0):
         """Order `slot`'s stream after torch's current stream (device inputs written by torch)."""
         _check(lib().kzgmi_stream_wait(self.handle, int(slot), _current_stream(self.device)))
+
+    def signal(self, slot: int, stream=None):
+        """kzgmi_slot_signal: order later work on `stream` (a torch.cuda.Stream; default torch's
+        current stream) after everything enqueued so far on `slot` -- no host sync."""
+        st = stream.cuda_stream if stream is not None else _current_stream(self.device)
+        _check(lib().kzgmi_slot_signal(self.handle, int(slot), st))
 
     def close(self):
         if getattr(self, "handle", None):
@@ -334,14 +408,39 @@ class Context:
                 return self.wait(0)
             _check(lib().kzgmi_batch_verify_device(self.handle, srs.handle, *ptrs, n, sd, ctypes.byref(ok)))
         else:
-            cb, zb, yb, pb = (_host_bytes(v) for v in (commitments, zs, ys, proofs))
-            if n is None:
-                n = len(cb) // g1b
-            if len(cb) < n * g1b or len(pb) < n * g1b or len(zb) < 32 * n or len(yb) < 32 * n:
-                raise ValueError("input buffers shorter than n tuples")
-            _check(lib().kzgmi_batch_verify_ex(self.handle, srs.handle, cb, zb, yb, pb, n, sd, flags,
-                                               ctypes.byref(ok)))
+            ptrs, keep = self._host_inputs(commitments, zs, ys, proofs, n, g1b)
+            n = ptrs[-1]
+            _check(lib().kzgmi_batch_verify_ex(self.handle, srs.handle, *ptrs[:4], n, sd, flags, ctypes.byref(ok)))
+            del keep
         return bool(ok.value)
+
+    @staticmethod
+    def _host_inputs(commitments, zs, ys, proofs, n, g1b):
+        """Addresses of the four host arrays (no copies) in C-ABI order (C, z, y, pi) + n."""
+        (pc, lc, kc), (pz, lz, kz), (py, ly, ky), (pp, lp, kp) = (
+            _host_ptr(v) for v in (commitments, zs, ys, proofs))
+        if n is None:
+            n = lc // g1b
+        if lc < n * g1b or lp < n * g1b or lz < 32 * n or ly < 32 * n:
+            raise ValueError("input buffers shorter than n tuples")
+        return (pc, pz, py, pp, n), (kc, kz, ky, kp)
+
+    def batch_verify_host_async(self, srs: Srs, slot: int, commitments, zs, ys, proofs, n: Optional[int] = None,
+                                seed: Optional[bytes] = None, compressed: bool = False,
+                                subgroup_check: bool = False, fiat_shamir: bool = False, challenge=None,
+                                trusted_g1: bool = False):
+        """kzgmi_batch_verify_ex_async: host arrays -> HBM on `slot`'s stream ahead of the batch's
+        kernels; wait(slot) returns the verdict.  Arrays in a HostBuffer (or register_host'ed) are
+        DMA'd asynchronously and must stay untouched until the wait; others are staged through
+        the slot's pinned ring before this returns."""
+        g1b = (1 if compressed else 2) * FP_BYTES[srs.curve]
+        ptrs, keep = self._host_inputs(commitments, zs, ys, proofs, n, g1b)
+        self._host_keep = getattr(self, "_host_keep", {})
+        self._host_keep[slot] = keep  # the DMA may read the arrays until wait(slot)
+        _check(lib().kzgmi_batch_verify_ex_async(self.handle, srs.handle, int(slot), *ptrs,
+                                                 _challenge_seed(seed, challenge),
+                                                 _flags(compressed, subgroup_check, fiat_shamir, challenge,
+                                                        trusted_g1)))
 
     def batch_verify_async(self, srs: Srs, slot: int, commitments, zs, ys, proofs, n: int,
                            seed: Optional[bytes] = None, compressed: bool = False, subgroup_check: bool = False,
@@ -480,7 +579,10 @@ class Context:
 
     def wait(self, slot: int) -> bool:
         ok = ctypes.c_int(-1)
-        _check(lib().kzgmi_slot_wait(self.handle, int(slot), ctypes.byref(ok)))
+        try:
+            _check(lib().kzgmi_slot_wait(self.handle, int(slot), ctypes.byref(ok)))
+        finally:
+            getattr(self, "_host_keep", {}).pop(slot, None)
         return bool(ok.value)
 
     def last_combination(self, curve: str):
@@ -501,10 +603,13 @@ class Context:
             self._order(0)
             _check(lib().kzgmi_msm_g1_device(self.handle, CURVES[curve], pp, ps, n, out))
         else:
-            pb, sb = _host_bytes(points), _host_bytes(scalars)
+            (pp, lp, kp), (ps, ls, ks) = _host_ptr(points), _host_ptr(scalars)
             if n is None:
-                n = len(pb) // g1b
-            _check(lib().kzgmi_msm_g1(self.handle, CURVES[curve], pb, sb, n, out))
+                n = lp // g1b
+            if lp < n * g1b or ls < 32 * n:
+                raise ValueError("input buffers shorter than n points")
+            _check(lib().kzgmi_msm_g1(self.handle, CURVES[curve], pp, ps, n, out))
+            del kp, ks
         return out.raw
 
     def msm_g1_async(self, curve: str, slot: int, points, scalars, n: int):

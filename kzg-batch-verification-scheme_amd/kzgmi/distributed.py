@@ -101,19 +101,29 @@ def sharded_batch_verify(backend, srs, commitments, zs, ys, proofs, n_local: int
 
 class ShardedPipeline:
     """Several global batches in flight per rank (the multi-GPU form of the single-GPU slot
-    pipeline).  Batch k's shard partial runs on slot k % slots.  When a slot comes round
-    again its partial (batch k - slots) is all-gathered and the sum-of-partials + pairing
-    check is enqueued on combine lane j % lanes (context slots slots .. slots+lanes-1); a
-    lane's verdict is collected only when the lane is reused, so the host never blocks on a
-    pairing while shard work waits to be issued.  The backend context needs slots + lanes
-    workspaces.  Every rank must submit the same sequence of batches (the all-gathers are
-    collectives); verdicts come back in submission order.
+    pipeline).  Batch k's shard partial runs on slot k % slots.  Every rank must submit the
+    same sequence of batches (the all-gathers are collectives); verdicts come back in
+    submission order.
+
+    Two schedules:
+      - eager (a backend with `signal`, i.e. kzgmi.Context on a GPU; the default there): right
+        after batch k's partial is enqueued on slot s, its all-gather and its sum + pairing are
+        enqueued too, ordered on the GPU -- a side stream waits for the slot (kzgmi_slot_signal),
+        RCCL gathers on it, and the combine is chained on slot s itself behind that stream
+        (kzgmi_batch_combine_device_async on a slot whose pending job is a partial).  The host
+        never waits on a partial before issuing the collective; collecting slot s's verdict when
+        it comes round again is the pipeline's only throttle.  The context needs `slots`
+        workspaces;
+      - deferred (otherwise, e.g. the CPU test double): when slot s comes round, its partial
+        (batch k - slots) is waited for on the host, all-gathered, and combined on lane
+        j % lanes (context slots slots .. slots + lanes - 1), whose verdict is collected when
+        the lane is reused.  The context needs slots + lanes workspaces.
 
     submit() returns the verdicts of batches that completed during the call;
     drain() completes everything still in flight.
     """
 
-    def __init__(self, backend, srs, slots: int = 3, lanes: int = 2, group=None):
+    def __init__(self, backend, srs, slots: int = 3, lanes: int = 2, group=None, eager=None):
         import torch
         import torch.distributed as dist
         self.backend, self.srs, self.group = backend, srs, group
@@ -121,13 +131,18 @@ class ShardedPipeline:
         self.world = dist.get_world_size(group)
         pb = backend.partial_bytes(srs.curve)
         self.dev = backend.tensor_device()
+        on_gpu = getattr(self.dev, "type", str(self.dev)) == "cuda"
+        self.eager = (on_gpu and hasattr(backend, "signal")) if eager is None else eager
+        self.comm = torch.cuda.Stream(device=self.dev) if self.eager else None
         self.local = [torch.empty(2 * pb, dtype=torch.uint8, device=self.dev) for _ in range(slots)]
-        # one gather buffer per lane: a lane's combine reads it until the lane is reused
-        self.gathered = [torch.empty(self.world * 2 * pb, dtype=torch.uint8, device=self.dev) for _ in range(lanes)]
+        # one gather buffer per slot (eager) / lane (deferred): the combine reads it until the
+        # slot / lane is reused
+        nbuf = slots if self.eager else lanes
+        self.gathered = [torch.empty(self.world * 2 * pb, dtype=torch.uint8, device=self.dev) for _ in range(nbuf)]
         self.pending = [False] * slots
         self.lane_pending = [False] * lanes
         self.k = 0      # batches submitted
-        self.j = 0      # combines issued
+        self.j = 0      # combines issued (deferred)
 
     def _collect_lane(self, lane: int, out):
         if self.lane_pending[lane]:
@@ -147,15 +162,30 @@ class ShardedPipeline:
         self.backend.batch_combine_async(self.srs, self.slots + lane, self.gathered[lane], self.world)
         self.lane_pending[lane] = True
 
+    def _enqueue_eager(self, s: int):
+        import torch
+        import torch.distributed as dist
+        with torch.cuda.stream(self.comm):
+            self.backend.signal(s, self.comm)                  # the side stream waits for the partial
+            dist.all_gather_into_tensor(self.gathered[s], self.local[s], group=self.group)
+            # chained on slot s, ordered after torch's current stream (= the side stream)
+            self.backend.batch_combine_async(self.srs, s, self.gathered[s], self.world)
+
     def submit(self, commitments, zs, ys, proofs, n_local: int, offset: int, seed: bytes):
         s = self.k % self.slots
         self.k += 1
         done = []
         if self.pending[s]:
-            self._gather_and_combine(s, done)
+            if self.eager:
+                done.append(self.backend.wait(s))              # partial + gather + pairing of batch k - slots
+                self.pending[s] = False
+            else:
+                self._gather_and_combine(s, done)
         self.backend.batch_partial_async(self.srs, s, commitments, zs, ys, proofs, n_local, offset, seed,
                                          self.local[s])
         self.pending[s] = True
+        if self.eager:
+            self._enqueue_eager(s)
         return done
 
     def drain(self):
@@ -163,9 +193,14 @@ class ShardedPipeline:
         for i in range(self.slots):
             s = (self.k + i) % self.slots                      # oldest first
             if self.pending[s]:
-                self._gather_and_combine(s, out)
-        for i in range(self.lanes):
-            self._collect_lane((self.j + i) % self.lanes, out)
+                if self.eager:
+                    out.append(self.backend.wait(s))
+                    self.pending[s] = False
+                else:
+                    self._gather_and_combine(s, out)
+        if not self.eager:
+            for i in range(self.lanes):
+                self._collect_lane((self.j + i) % self.lanes, out)
         return out
 
 
@@ -185,13 +220,15 @@ def sharded_msm(backend, curve: str, points, scalars, n_local: int, group=None) 
 
 
 class ShardedMsmPipeline:
-    """Several global MSMs in flight per rank (the MSM counterpart of ShardedPipeline): the
-    shard partial of MSM k runs on slot k % slots; when the slot comes round its partial
-    record is all-gathered and summed + encoded on combine lane j % lanes (context slots
-    slots .. slots+lanes-1), collected when the lane is reused.  Results (G1 encodings, the
-    same on every rank) come back in submission order."""
+    """Several global MSMs in flight per rank (the MSM counterpart of ShardedPipeline, with the
+    same two schedules): the shard partial of MSM k runs on slot k % slots; eager: its
+    all-gather and the chained sum + encode on the same slot are enqueued right behind it,
+    ordered on the GPU; deferred: when the slot comes round its partial record is waited for,
+    all-gathered and summed + encoded on combine lane j % lanes (context slots slots ..
+    slots+lanes-1), collected when the lane is reused.  Results (G1 encodings, the same on
+    every rank) come back in submission order."""
 
-    def __init__(self, backend, curve: str, slots: int = 3, lanes: int = 2, group=None):
+    def __init__(self, backend, curve: str, slots: int = 3, lanes: int = 2, group=None, eager=None):
         import torch
         import torch.distributed as dist
         self.backend, self.curve, self.group = backend, curve, group
@@ -199,8 +236,12 @@ class ShardedMsmPipeline:
         self.world = dist.get_world_size(group)
         pb = backend.partial_bytes(curve)
         self.dev = backend.tensor_device()
+        on_gpu = getattr(self.dev, "type", str(self.dev)) == "cuda"
+        self.eager = (on_gpu and hasattr(backend, "signal")) if eager is None else eager
+        self.comm = torch.cuda.Stream(device=self.dev) if self.eager else None
         self.local = [torch.empty(pb, dtype=torch.uint8, device=self.dev) for _ in range(slots)]
-        self.gathered = [torch.empty(self.world * pb, dtype=torch.uint8, device=self.dev) for _ in range(lanes)]
+        nbuf = slots if self.eager else lanes
+        self.gathered = [torch.empty(self.world * pb, dtype=torch.uint8, device=self.dev) for _ in range(nbuf)]
         self.pending = [False] * slots
         self.lane_pending = [False] * lanes
         self.k = 0
@@ -222,14 +263,28 @@ class ShardedMsmPipeline:
         self.backend.msm_combine_async(self.curve, self.slots + lane, self.gathered[lane], self.world)
         self.lane_pending[lane] = True
 
+    def _enqueue_eager(self, s: int):
+        import torch
+        import torch.distributed as dist
+        with torch.cuda.stream(self.comm):
+            self.backend.signal(s, self.comm)
+            dist.all_gather_into_tensor(self.gathered[s], self.local[s], group=self.group)
+            self.backend.msm_combine_async(self.curve, s, self.gathered[s], self.world)
+
     def submit(self, points, scalars, n_local: int):
         s = self.k % self.slots
         self.k += 1
         done = []
         if self.pending[s]:
-            self._gather_and_combine(s, done)
+            if self.eager:
+                done.append(self.backend.msm_wait(s))
+                self.pending[s] = False
+            else:
+                self._gather_and_combine(s, done)
         self.backend.msm_partial_async(self.curve, s, points, scalars, n_local, self.local[s])
         self.pending[s] = True
+        if self.eager:
+            self._enqueue_eager(s)
         return done
 
     def drain(self):
@@ -237,7 +292,12 @@ class ShardedMsmPipeline:
         for i in range(self.slots):
             s = (self.k + i) % self.slots
             if self.pending[s]:
-                self._gather_and_combine(s, out)
-        for i in range(self.lanes):
-            self._collect_lane((self.j + i) % self.lanes, out)
+                if self.eager:
+                    out.append(self.backend.msm_wait(s))
+                    self.pending[s] = False
+                else:
+                    self._gather_and_combine(s, out)
+        if not self.eager:
+            for i in range(self.lanes):
+                self._collect_lane((self.j + i) % self.lanes, out)
         return out

@@ -28,7 +28,7 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     curve, n_total, tau = "bls12_381", 3001, 0x5EED
     g1b = 96
-    ctx = kzgmi.Context(0, 3)  # 2 shard slots + 1 combine lane
+    ctx = kzgmi.Context(0, 3)  # 2 shard slots + 1 combine lane (deferred schedule)
     Cm = torch.empty(n_total * g1b, dtype=torch.uint8, device="cuda")
     P = torch.empty(n_total * g1b, dtype=torch.uint8, device="cuda")
     z = torch.empty(n_total * 32, dtype=torch.uint8, device="cuda")
@@ -58,12 +58,16 @@ def main():
     ybad = ys.clone()
     if rank == 1:
         ybad[32 * (n - 1) + 31] ^= 1
-    pipe = ShardedPipeline(ctx, srs, slots=2, lanes=1)
-    out = []
-    for b in range(4):
-        out += pipe.submit(Cs, zs, ybad if b % 2 else ys, Ps, n, off, seed)
-    out += pipe.drain()
-    assert out == [True, False, True, False], (rank, out)
+    # both schedules: deferred (host waits each partial, 1 combine lane) and eager (gather +
+    # combine enqueued behind the partial, ordered on the GPU by kzgmi_slot_signal, the combine
+    # chained on the partial's own slot)
+    for lanes, eager in ((1, False), (0, True)):
+        pipe = ShardedPipeline(ctx, srs, slots=2, lanes=lanes, eager=eager)
+        out = []
+        for b in range(5):
+            out += pipe.submit(Cs, zs, ybad if b % 2 else ys, Ps, n, off, seed)
+        out += pipe.drain()
+        assert out == [True, False, True, False, True], (rank, eager, out)
     dist.barrier()
     dist.destroy_process_group()
     print("RANK OK", rank, flush=True)

@@ -1,5 +1,5 @@
 """The drop-in boundary of SURVEY.md 8b on the GPU: the SRS's G1 element, the multi-device
-context (kzgmi_ctx_create_multi), stream ordering against torch, slot-0 guards, argument
+context (kzgmi_ctx_create over a device list), stream ordering against torch, slot-0 guards, argument
 checks, and shard partials compared one by one with the oracle.
 
 Bar: bit-exact against the C oracle (oracle/c) for every point; verdicts as the oracle's.
@@ -223,7 +223,7 @@ def test_slot0_busy_guard_and_args(ctx, golden):
 
 @pytest.mark.parametrize("curve", ["bls12_381", "bn254"])
 def test_multi_device_context(curve):
-    """kzgmi_ctx_create_multi over the device list [0, 0] (two shard contexts on the one GPU of
+    """kzgmi_ctx_create over the device list [0, 0] (two shard contexts on the one GPU of
     the test box; on a node the list names distinct GPUs): host-buffer batch_verify and msm_g1
     are split over both, partials gathered with hipMemcpyPeer and combined on the primary --
     A, B and the MSM bit-exact vs the oracle, the negative batch rejected, Fiat-Shamir mode
