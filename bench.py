@@ -307,9 +307,10 @@ def main():
         else:
             dist.init_process_group(backend)
     curve, n = args.curve, args.n
-    # measured (profiles/r01/slots_sweep.txt, sharded_sweep.txt): single 12 slots; sharded at
-    # world 1 over RCCL, 6/8/10 slots + 2 combine lanes: 135.0/136.3/134.3 batch-verifies/s,
-    # MSM 193/217/220 M pts/s (12+2 streams exceed the hardware queues: 70/s)
+    # 16 slots on 24 hardware queues (profiles/r01/prio_sweep.txt, r02/slots_sweep.txt).  Sharded
+    # runs use the eager ShardedPipeline schedule (combine chained on each partial's slot, no
+    # extra lanes): at world 1 over RCCL, 2^17-tuple shards run 968/s on 16 slots vs 832/s on 8
+    # and 851/s with round 3's deferred 8 slots + 2 lanes (profiles/r04/bench_s1_legs_serial_h2d.json)
     slots = args.slots if args.slots else 16
     lanes = 0  # the eager ShardedPipeline schedule chains each combine on its partial's slot
     ctx = kzgmi.Context(local, slots + lanes)  # + the combine lanes
