@@ -19,6 +19,7 @@
 #include <omp.h>
 #endif
 #include "consts_gen.h"
+#include "tmul_x86_gen.h"
 
 #define KZGO_OK 0
 #define KZGO_ERR_ARG (-1)
@@ -154,6 +155,9 @@ static const uint64_t BLS_LOOPW[2] = {BLS_LOOP, 0};
 #define PRAW BLS_P_MOD
 #define RRAW BLS_FR_MOD
 #include "curve_tmpl.h"
+#define PINV_T BLS_P_INV
+#include "pippenger_tuned_tmpl.h"
+#undef PINV_T
 #undef PRAW
 #undef RRAW
 #undef FP
@@ -238,6 +242,9 @@ static const uint64_t BLS_LOOPW[2] = {BLS_LOOP, 0};
 #define PRAW BN_P_MOD
 #define RRAW BN_FR_MOD
 #include "curve_tmpl.h"
+#define PINV_T BN_P_INV
+#include "pippenger_tuned_tmpl.h"
+#undef PINV_T
 
 /* ================================================================== C API (ctypes) */
 #define CURVE_DISPATCH(curve, call_bls, call_bn) \
@@ -258,6 +265,18 @@ int kzgo_batch_verify(int curve, const uint8_t* cm, const uint8_t* zs, const uin
   if (!ok || !seed || !g2 || !tau_g2 || (n && (!cm || !zs || !ys || !pf))) return KZGO_ERR_ARG;
   return CURVE_DISPATCH(curve, bls_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, 1, NULL, NULL),
                         bn_batch_verify(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, 1, NULL, NULL));
+}
+
+/* The tuned CPU verifier (pippenger_tuned_tmpl.h): same A, B and verdict as kzgo_batch_verify
+ * (seeded randomisers), signed c-bit windows, XYZZ buckets, tasks of `chunk` points (0 = 2^19).
+ * do_pairing = 0 computes A, B only (ok untouched). */
+int kzgo_batch_verify_tuned(int curve, const uint8_t* cm, const uint8_t* zs, const uint8_t* ys, const uint8_t* pf,
+                            size_t n, const uint8_t* g2, const uint8_t* tau_g2, const uint8_t* seed, int wbits,
+                            size_t chunk, int do_pairing, int* ok, uint8_t* a_out, uint8_t* b_out) {
+  if (!ok || !seed || !g2 || !tau_g2 || (n && (!cm || !zs || !ys || !pf))) return KZGO_ERR_ARG;
+  return CURVE_DISPATCH(
+      curve, bls_batch_verify_tuned(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, do_pairing, wbits, chunk),
+      bn_batch_verify_tuned(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, do_pairing, wbits, chunk));
 }
 
 /* Powers mode (Fiat-Shamir / caller-supplied challenge): r_i = r^(offset + i), r = int_be(r32) < r.

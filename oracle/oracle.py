@@ -51,6 +51,9 @@ def lib():
         L.kzgo_batch_verify_g1.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p, c.c_size_t,
                                            c.c_uint64, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p, c.c_int,
                                            c.POINTER(c.c_int), c.c_char_p, c.c_char_p]
+        L.kzgo_batch_verify_tuned.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p, c.c_size_t,
+                                              c.c_char_p, c.c_char_p, c.c_char_p, c.c_int, c.c_size_t, c.c_int,
+                                              c.POINTER(c.c_int), c.c_char_p, c.c_char_p]
         L.kzgo_fr_dot.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_size_t, c.c_char_p]
         L.kzgo_set_threads.argtypes = [c.c_int]
         L.kzgo_get_threads.restype = c.c_int
@@ -88,6 +91,20 @@ def batch_verify(curve, commitments: bytes, zs: bytes, ys: bytes, proofs: bytes,
     if want_ab:
         return bool(ok.value), a.raw, b.raw
     return bool(ok.value)
+
+
+def batch_verify_tuned(curve, commitments: bytes, zs: bytes, ys: bytes, proofs: bytes, n: int,
+                       g2: bytes, tau_g2: bytes, seed: bytes, wbits: int = 13, chunk: int = 0, pairing: bool = True):
+    """The tuned CPU verifier (c/pippenger_tuned_tmpl.h: signed windows, XYZZ buckets, fused
+    MSMs, OpenMP tasks) -- the CPU baseline bench.py quotes; same A, B and verdict as
+    batch_verify.  Returns (ok or None, A, B)."""
+    g1b = 2 * FP_BYTES[curve]
+    ok = ctypes.c_int(-1)
+    a = ctypes.create_string_buffer(g1b)
+    b = ctypes.create_string_buffer(g1b)
+    _check(lib().kzgo_batch_verify_tuned(CURVE_IDS[curve], commitments, zs, ys, proofs, n, g2, tau_g2, seed,
+                                         int(wbits), int(chunk), 1 if pairing else 0, ctypes.byref(ok), a, b))
+    return (bool(ok.value) if pairing else None), a.raw, b.raw
 
 
 def batch_combination(curve, commitments, zs, ys, proofs, n, offset, g2, tau_g2, seed):

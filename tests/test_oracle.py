@@ -60,6 +60,54 @@ def test_batch_golden(curve, golden):
 
 
 @pytest.mark.parametrize("curve", CURVES)
+def test_tuned_verifier_golden(curve, golden):
+    """The tuned CPU verifier (oracle/c/pippenger_tuned_tmpl.h, bench.py's CPU baseline) gives
+    the golden A, B and verdict bit for bit -- at several window widths and with point ranges
+    cut into several tasks (chunk 3: ragged last chunks, G1 only in the first)."""
+    for n in SIZES[curve]:
+        g = golden("%s_batch_n%d.json" % (curve, n))
+        for key in ["valid", "neg_flip_y", "neg_swap_proofs"]:
+            src = g if key == "valid" else g[key]
+            exp = g[key]
+            for c, chunk in ((4, 3), (9, 0), (13, 0), (11, 5)):
+                ok, A, B = O.batch_verify_tuned(curve, h(src["commitments"]), h(src["zs"]), h(src["ys"]),
+                                                h(src["proofs"]), n, h(g["g2"]), h(g["tau_g2"]), h(g["seed"]),
+                                                wbits=c, chunk=chunk, pairing=c == 13)
+                assert (A.hex(), B.hex()) == (exp["A"], exp["B"]), (n, key, c, chunk)
+                assert ok == (exp["ok"] if c == 13 else None), (n, key, c, chunk)
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_tuned_verifier_vs_oracle_random(curve):
+    """Random points (not openings: the verdict is False) with repeated and infinity points,
+    A, B of the tuned verifier == the oracle's; empty batch accepts; errors as the oracle's."""
+    C = pc.CURVES[curve]
+    rng = random.Random(7)
+    n = 300
+    ks = [rng.randrange(C.r) for _ in range(n)]
+    ks[5] = ks[9] = ks[17]   # equal points: doublings inside the buckets
+    ks[11] = 0               # the point at infinity
+    ks[12] = C.r - ks[13]    # P and -P
+    pts = O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(k) for k in ks), n)
+    cm, pf = pts, O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(k * 3 % C.r) for k in ks), n)
+    zs = b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(n))
+    ys = b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(n))
+    g2 = pk.g2_to_bytes(C.g2, C)
+    tg2 = O.g2_mul(curve, g2, 99)
+    seed = bytes(range(32))
+    want = O.batch_verify(curve, cm, zs, ys, pf, n, g2, tg2, seed, want_ab=True)
+    assert O.batch_verify_tuned(curve, cm, zs, ys, pf, n, g2, tg2, seed) == want
+    assert O.batch_verify_tuned(curve, cm, zs, ys, pf, n, g2, tg2, seed, wbits=7, chunk=64,
+                                pairing=False) == (None,) + want[1:]
+    assert O.batch_verify_tuned(curve, b"", b"", b"", b"", 0, g2, tg2, seed)[0] is True
+    bad = bytearray(zs)
+    bad[32:64] = C.r.to_bytes(32, "big")
+    with pytest.raises(O.OracleError) as e:
+        O.batch_verify_tuned(curve, cm, bytes(bad), ys, pf, n, g2, tg2, seed)
+    assert e.value.code == -4
+
+
+@pytest.mark.parametrize("curve", CURVES)
 def test_genuine_kzg(curve, golden):
     g = golden("%s_genuine_kzg.json" % curve)
     ok = O.batch_verify(curve, h(g["commitments"]), h(g["zs"]), h(g["ys"]), h(g["proofs"]), g["n"],
