@@ -282,7 +282,7 @@ def main():
                     help="batches in flight per GPU (default 16; sharded runs chain each combine on its slot)")
     ap.add_argument("--msm-steps", type=int, default=96,
                     help="configs[1]: pipelined 2^20 MSMs timed (the drain of the last in-flight MSMs is "
-                         "inside the region: 24 steps read 356-358 M pts/s, 96 steps 372-374, tools/msm_steps_check.sh; 0 = skip)")
+                         "inside the region: 24 steps read 356-358 M pts/s, 96 steps 372-374, tools/ab.py --key msm_pts_per_s; 0 = skip)")
     ap.add_argument("--trusted-steps", type=int, default=96,
                     help="secondary: pipelined batches with KZGMI_FLAG_TRUSTED_G1 (GLV on BLS12-381; 0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -956,7 +956,7 @@ def main():
     # algorithmic Fp products in the accumulation: 32 n window-terms x (8M + 2S) per mixed
     # addition (the kernel shares one reduction between two of them)
     acc_fpmuls = 32 * n * 10
-    # PMC traffic of the same kernel and config from the committed profile (tools/profile.sh:
+    # PMC traffic of the same kernel and config from the committed profile (tools/prof.sh traffic:
     # separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE x 2 as MI355X_MICROARCH.md prescribes)
     traffic, traffic_src, rocprof_ms, rocprof_src, gather_bytes = None, None, None, None, None
     prof_dir = os.path.join("profiles", PROFILE_ROUND, "rocprof_single")

@@ -131,7 +131,7 @@ struct kzgmi_ctx {
   bool msm_trusted_g1 = false;
   // accumulation grid cap: one resident round (CUs x 4 SIMDs x kAccWaves<Cv> waves x 64 lanes)
   // of equal chunks instead of 64-entry chunks in 2-3 partial rounds: 113 -> 116
-  // batch-verifies/s pipelined when introduced (tools/ab_env.sh).
+  // batch-verifies/s pipelined when introduced (tools/ab.py).
   int ncu = 0;                // compute units: the accumulation grid cap (kAccWaves, msm.hpp)
   size_t acc_threads_env = 0;  // KZGMI_ACC_THREADS override of that cap (0 = none)
   int acc_queue = ACC_QUEUE_FACTOR;  // KZGMI_ACC_QUEUE: chunks per capped thread (<= 1: static grid)

@@ -1,4 +1,4 @@
-"""Summarise tools/profile.sh output into profiles/<round>/rocprof/:
+"""Summarise tools/prof.sh pipelined output into profiles/<round>/rocprof/:
 kernel_stats.csv (rocprofv3 --stats), kernel_stats_top.txt and pmc_accumulate_pipelined.json (per-launch
 HBM traffic of k_accumulate: FETCH_SIZE x 2 per MI355X_MICROARCH.md 'HBM' (gfx950 tallies
 128-B read requests at 64 B) + WRITE_SIZE; FETCH/WRITE_SIZE are in KiB)."""

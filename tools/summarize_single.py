@@ -1,4 +1,4 @@
-"""Summarise tools/kt_single.sh (rocprofv3 --kernel-trace --stats of non-pipelined single
+"""Summarise tools/prof.sh kernel (rocprofv3 --kernel-trace --stats of non-pipelined single
 batches, tools/phase_timing.py) into profiles/<round>/rocprof_single/: the stats CSV, a top
 list, and kernel_single.json with the average k_accumulate + k_fixup duration that bench.py's
 roofline.kernel_ms (single-batch HIP events around the same two kernels) must agree with.
@@ -41,7 +41,7 @@ json.dump(out, open(os.path.join(dst, "kernel_single.json"), "w"), indent=1)
 print(json.dumps(out))
 
 
-# ---- PMC passes of tools/profile_single.sh (absent for the plain kt_single.sh trace)
+# ---- PMC passes of tools/prof.sh kernel / traffic (absent for the plain kt_single.sh trace)
 def per_launch(kind, counter=None):
     files = glob.glob(os.path.join(src, kind, "**", "*counter_collection.csv"), recursive=True)
     if not files:

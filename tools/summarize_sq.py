@@ -1,4 +1,4 @@
-"""Summarise tools/pmc_sq_accumulate.sh (SQ counters of k_accumulate on single batches) into
+"""Summarise tools/prof.sh sq (SQ counters of k_accumulate on single batches) into
 profiles/<round>/pmc_sq_accumulate.json: per-launch averages and the per-addition VALU count.
 
 python3 tools/summarize_sq.py gpurun_out/pmc_sq profiles/r02/pmc_sq_accumulate.json [n]
@@ -19,7 +19,7 @@ for f in glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive
         acc[(r["Kernel_Name"].split("(")[0].replace("void ", ""), r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
     for (k, _, c), v in acc.items():
         per[k][c].append(v)
-out = {"command": "tools/pmc_sq_accumulate.sh: rocprofv3 --pmc <SQ counters> | FETCH_SIZE | WRITE_SIZE (separate passes, "
+out = {"command": "tools/prof.sh sq: rocprofv3 --pmc <SQ counters> | FETCH_SIZE | WRITE_SIZE (separate passes, "
                   "--kernel-include-regex) -- python3 tools/phase_timing.py --reps 2 (n = 2^20 BLS12-381, single batches)",
        "per_launch": {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in per.items()}}
 acc = out["per_launch"].get("kzgmi::k_accumulate<kzgmi::Bls12_381>")
