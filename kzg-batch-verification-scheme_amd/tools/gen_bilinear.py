@@ -530,9 +530,17 @@ class Prog:
         self.code.append([K_ROUND, OPNUM[name], a, NONE if b is None else b, out, 0, 0, 0, 0, 0])
 
     def op2(self, n1, a1, b1, o1, n2, a2, b2, o2):
+        # the two ops of a round run concurrently and write their outputs straight into the register
+        # file (pairing_par.hpp): neither output block may overlap any input block of the round or
+        # the other output block
         self._check_alias(n1, a1, b1, o1)
         self._check_alias(n2, a2, b2, o2)
-        assert o1 not in (a2, b2) and o2 not in (a1, b1)
+        wa1, wb1, no1 = op_shape(n1, self.cv)
+        wa2, wb2, no2 = op_shape(n2, self.cv)
+        for o, no, name in ((o1, no1, n1), (o2, no2, n2)):
+            for x, w in ((a1, wa1), (b1, wb1), (a2, wa2), (b2, wb2)):
+                assert not _overlap(o, no, x, w), "%s: output block overlaps an input block of the round" % name
+        assert not _overlap(o1, no1, o2, no2), "%s/%s: output blocks overlap" % (n1, n2)
         self.code.append([K_ROUND2, OPNUM[n1], a1, NONE if b1 is None else b1, o1,
                           OPNUM[n2], a2, NONE if b2 is None else b2, o2, 0])
 
@@ -542,9 +550,41 @@ class Prog:
     def inv(self, dst, src):
         self.code.append([K_INV, 0, src, NONE, dst, 0, 0, 0, 0, 0])
 
-    @staticmethod
-    def _check_alias(name, a, b, out):
-        assert out != a and out != b, "%s: output aliases an input" % name
+    def _check_alias(self, name, a, b, out):
+        # outputs are written straight into the register file with no barrier after the round's
+        # reads (pairing_par.hpp): the output block [out, out + no) must be disjoint from every
+        # input block [a, a + wa), [b, b + wb) -- as ranges, not just distinct starts (an operand may
+        # address into the middle of a block, like LL's e(idx) + 6)
+        wa, wb, no = op_shape(name, self.cv)
+        assert not _overlap(out, no, a, wa), "%s: output block overlaps input A" % name
+        assert not _overlap(out, no, b, wb), "%s: output block overlaps input B" % name
+
+
+def _overlap(x, nx, y, ny):
+    """[x, x + nx) and [y, y + ny) intersect (y None or ny 0: no operand)."""
+    if y is None or nx == 0 or ny == 0:
+        return False
+    return x < y + ny and y < x + nx
+
+
+_SHAPES = {}
+
+
+def op_shape(name, cv):
+    """(words read from A, words read from B, words written) of an op, from its symbolic form."""
+    key = (name, cv)
+    if key not in _SHAPES:
+        saved = S.ctx
+        prods, outs = build_op(dict(OPS)[name], cv)
+        S.ctx = saved
+        w = {"A": 0, "B": 0}
+        forms = [f for L, R in prods for f in (L, R)] + [getattr(o, "d", {}) for o in outs]
+        for f in forms:
+            for k in f:
+                if isinstance(k, tuple) and k[0] in w:
+                    w[k[0]] = max(w[k[0]], k[1] + 1)
+        _SHAPES[key] = (w["A"], w["B"], len(outs))
+    return _SHAPES[key]
 
 
 def build_program(cv):

@@ -45,3 +45,27 @@ def test_bound_checker_rejects_a_short_bias():
     except AssertionError:
         return
     raise AssertionError("check_bounds accepted ACC_NEG = 1p on BN254")
+
+
+def test_bilinear_program_alias_ranges():
+    """tools/gen_bilinear.py: every round's output block is disjoint from its input blocks as
+    RANGES (pairing_par.hpp writes outputs straight into the register file with no barrier after
+    the round's reads), for the shipped programs of both curves; an op whose output starts inside
+    an input block (same start or not) is rejected."""
+    import pytest
+    sys.path.insert(0, os.path.join(PKG, "tools"))
+    try:
+        import gen_bilinear as g
+    finally:
+        sys.path.pop(0)
+    for cv in ("bls12_381", "bn254"):
+        g.build_program(cv)  # asserts on every op / op2
+        P = g.Prog(cv)
+        assert g.op_shape("LL", cv) == (6, 6, 12)
+        with pytest.raises(AssertionError):
+            P.op("MUL", P.g(0), P.g(1), P.g(0) + 6)   # output starts inside input A
+        with pytest.raises(AssertionError):
+            P.op("LL", P.e(0), P.e(0) + 6, P.e(0) + 3)
+        with pytest.raises(AssertionError):
+            P.op2("SQR", P.g(0), None, P.g(1), "LL", P.e(0), P.e(0) + 6, P.g(1) + 6)  # outputs overlap
+        P.op("MUL", P.g(0), P.g(1), P.g(2))             # disjoint: accepted
