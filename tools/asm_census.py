@@ -39,7 +39,8 @@ def main():
     lines = open(path).read().splitlines()
     start = None
     for i, l in enumerate(lines):
-        if l.startswith("_Z") and sym in l and l.rstrip().endswith(":") or (l.startswith("_Z") and sym in l and ": ;" in l):
+        m = re.match(r"^(_Z\S*):", l)
+        if m and sym in m.group(1):
             start = i
             break
     if start is None:
