@@ -271,6 +271,17 @@ def cpu_baseline(curve, Cm, z, y, P, n_full, seed, target_s):
     }
 
 
+def _ensure_world1_pg(local):
+    """A world-1 RCCL process group for the single-GPU run's sharded-path legs (the per-rank
+    work of the N-GPU runs through the real collectives); True if this call created it."""
+    if dist.is_initialized():
+        return False
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29541")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+    return True
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -728,11 +739,7 @@ def main():
         v17 = (Cm[: n17 * g1b], z[: n17 * 32], y[: n17 * 32], P[: n17 * g1b])
         rate_unsharded = pipelined_rate(ctx, slots, args.shard17_steps,
                                         lambda s_: ctx.batch_verify_async(srs, s_, *v17, n17, seed=vseed))
-        own_pg = not dist.is_initialized()
-        if own_pg:
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", "29541")
-            dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+        own_pg = _ensure_world1_pg(local)
         res17 = {}
         for mode, (sl17, ln17) in (("eager", (16, 0)), ("eager8", (8, 0)), ("deferred", (8, 2))):
             pipe17 = ShardedPipeline(ctx, srs, sl17, ln17, eager=mode != "deferred")
@@ -934,6 +941,35 @@ def main():
                 "method": "point-range shards, kzgmi_msm_partial_device_async + RCCL all-gather of partial "
                           "sums + kzgmi_msm_combine_device_async, 2 MSMs in flight per rank" if world > 1 or sharded
                           else "one device, kzgmi_msm_g1_device_async, 2 MSMs in flight"}
+        # per-rank share of the 8-GPU run (2^24 / 8 = 2^21 points) through the real sharded path
+        # (ShardedMsmPipeline: partial + RCCL all-gather + combine, eager schedule) at world 1:
+        # its rate x 2^24 over the one-GPU rate above projects configs[3]'s 8-GPU strong speed-up
+        if world == 1 and not sharded and args.cfg4_n >= 8:
+            m8 = args.cfg4_n // 8
+            own_pg = _ensure_world1_pg(local)
+            mp8 = ShardedMsmPipeline(ctx, curve, slots=4, lanes=0)
+            r8 = []
+            for _ in range(4):
+                r8.extend(mp8.submit(p4[: m8 * 2 * kzgmi.FP_BYTES[curve]], s4[: 32 * m8], m8))
+            r8.extend(mp8.drain())
+            torch.cuda.synchronize()
+            n8 = 4 * args.cfg4_msms
+            a = time.perf_counter()
+            for _ in range(n8):
+                r8.extend(mp8.submit(p4[: m8 * 2 * kzgmi.FP_BYTES[curve]], s4[: 32 * m8], m8))
+            r8.extend(mp8.drain())
+            torch.cuda.synchronize()
+            dt8 = time.perf_counter() - a
+            assert len(set(r8)) == 1, "sharded 2^21 MSM results differ"
+            del mp8
+            if own_pg:
+                dist.destroy_process_group()
+            cfg4["per_rank_share_at_8_gpus"] = {
+                "n_points": m8, "msms": n8, "msms_per_s": n8 / dt8, "ms_per_msm": 1e3 * dt8 / n8,
+                "projected_8gpu_pts_per_s": n8 / dt8 * args.cfg4_n,
+                "projected_8gpu_strong_speedup": (n8 / dt8 * args.cfg4_n) / cfg4["pts_per_s"],
+                "method": "kzgmi.distributed.ShardedMsmPipeline (eager schedule, 4 MSMs in flight) over RCCL at "
+                          "world 1 on the first 2^21 points: the per-rank work of the 8-GPU configs[3] run"}
         del p4, s4
 
     if rank != 0:
