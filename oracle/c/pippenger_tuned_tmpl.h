@@ -229,6 +229,11 @@ static int C_(batch_verify_tuned)(const uint8_t* cm, const uint8_t* zs, const ui
   if ((e = C_(g2_decode)(&g2, g2b))) return e;
   if ((e = C_(g2_decode)(&tg2, tg2b))) return e;
   C_(generator)(&g1);
+  if (c == 0) {  /* auto: about n / 8 buckets per window (16 at n = 2^20, 5 at n = 256) */
+    int lg = 0;
+    while (((size_t)2 << lg) <= n) ++lg;
+    c = lg - 3 < 5 ? 5 : lg - 3 > 16 ? 16 : lg - 3;
+  }
   if (c < 4 || c > 20) return KZGO_ERR_ARG;
   if (chunk == 0) chunk = (size_t)1 << 19;
   if (n == 0) {

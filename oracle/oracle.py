@@ -94,10 +94,10 @@ def batch_verify(curve, commitments: bytes, zs: bytes, ys: bytes, proofs: bytes,
 
 
 def batch_verify_tuned(curve, commitments: bytes, zs: bytes, ys: bytes, proofs: bytes, n: int,
-                       g2: bytes, tau_g2: bytes, seed: bytes, wbits: int = 13, chunk: int = 0, pairing: bool = True):
+                       g2: bytes, tau_g2: bytes, seed: bytes, wbits: int = 0, chunk: int = 0, pairing: bool = True):
     """The tuned CPU verifier (c/pippenger_tuned_tmpl.h: signed windows, XYZZ buckets, fused
     MSMs, OpenMP tasks) -- the CPU baseline bench.py quotes; same A, B and verdict as
-    batch_verify.  Returns (ok or None, A, B)."""
+    batch_verify.  wbits = 0 picks the window width from n.  Returns (ok or None, A, B)."""
     g1b = 2 * FP_BYTES[curve]
     ok = ctypes.c_int(-1)
     a = ctypes.create_string_buffer(g1b)
