@@ -275,7 +275,8 @@ def cpu_baseline(curve, Cm, z, y, P, n_full, seed, target_s):
 
 def _ensure_world1_pg(local):
     """A world-1 RCCL process group for the single-GPU run's sharded-path legs (the per-rank
-    work of the N-GPU runs through the real collectives); True if this call created it."""
+    work of the N-GPU runs through the real collectives), created once and kept to the end of
+    the run (one communicator, one set of RCCL streams); True if this call created it."""
     if dist.is_initialized():
         return False
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -741,7 +742,7 @@ def main():
         v17 = (Cm[: n17 * g1b], z[: n17 * 32], y[: n17 * 32], P[: n17 * g1b])
         rate_unsharded = pipelined_rate(ctx, slots, args.shard17_steps,
                                         lambda s_: ctx.batch_verify_async(srs, s_, *v17, n17, seed=vseed))
-        own_pg = _ensure_world1_pg(local)
+        _ensure_world1_pg(local)
         res17 = {}
         for mode, (sl17, ln17) in (("eager", (16, 0)), ("eager8", (8, 0)), ("deferred", (8, 2))):
             pipe17 = ShardedPipeline(ctx, srs, sl17, ln17, eager=mode != "deferred")
@@ -760,8 +761,6 @@ def main():
             torch.cuda.synchronize()
             res17[mode] = args.shard17_steps / (time.perf_counter() - a)
             del pipe17
-        if own_pg:
-            dist.destroy_process_group()
         shard17 = {
             "n_per_rank": n17, "steps": args.shard17_steps,
             "batch_verifies_per_s_sharded_rccl_world1": res17["eager"],
@@ -948,7 +947,7 @@ def main():
         # its rate x 2^24 over the one-GPU rate above projects configs[3]'s 8-GPU strong speed-up
         if world == 1 and not sharded and args.cfg4_n >= 8:
             m8 = args.cfg4_n // 8
-            own_pg = _ensure_world1_pg(local)
+            _ensure_world1_pg(local)
             mp8 = ShardedMsmPipeline(ctx, curve, slots=4, lanes=0)
             r8 = []
             for _ in range(4):
@@ -964,8 +963,6 @@ def main():
             dt8 = time.perf_counter() - a
             assert len(set(r8)) == 1, "sharded 2^21 MSM results differ"
             del mp8
-            if own_pg:
-                dist.destroy_process_group()
             cfg4["per_rank_share_at_8_gpus"] = {
                 "n_points": m8, "msms": n8, "msms_per_s": n8 / dt8, "ms_per_msm": 1e3 * dt8 / n8,
                 "projected_8gpu_pts_per_s": n8 / dt8 * args.cfg4_n,
@@ -1145,6 +1142,7 @@ def main():
     print(json.dumps(out), flush=True)
     if sharded:
         dist.barrier()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -32,6 +32,21 @@ from typing import Tuple
 
 FS_CHUNK = 4096  # Fiat-Shamir transcript subtree (csrc/fs.hpp): shard offsets must align to it
 
+_COMM_STREAMS = {}
+
+
+def comm_stream(device):
+    """The side stream the eager schedules gather on: ONE per device for the process.  HIP maps
+    streams onto GPU_MAX_HW_QUEUES hardware queues round-robin at creation; a stream that shares
+    a queue with a slot stream blocks the slot behind its GPU-side wait for a partial (a run that
+    made a new side stream per pipeline wrapped the 24 queues and serialised its MSMs), so the
+    pipelines share this one."""
+    import torch
+    key = str(device)
+    if key not in _COMM_STREAMS:
+        _COMM_STREAMS[key] = torch.cuda.Stream(device=device)
+    return _COMM_STREAMS[key]
+
 
 def shard_range(n_total: int, world: int, rank: int, align: int = 1) -> Tuple[int, int]:
     """Contiguous balanced split: (offset, count) of rank's tuples; offsets are multiples of
@@ -133,7 +148,7 @@ class ShardedPipeline:
         self.dev = backend.tensor_device()
         on_gpu = getattr(self.dev, "type", str(self.dev)) == "cuda"
         self.eager = (on_gpu and hasattr(backend, "signal")) if eager is None else eager
-        self.comm = torch.cuda.Stream(device=self.dev) if self.eager else None
+        self.comm = comm_stream(self.dev) if self.eager else None
         self.local = [torch.empty(2 * pb, dtype=torch.uint8, device=self.dev) for _ in range(slots)]
         # one gather buffer per slot (eager) / lane (deferred): the combine reads it until the
         # slot / lane is reused
@@ -238,7 +253,7 @@ class ShardedMsmPipeline:
         self.dev = backend.tensor_device()
         on_gpu = getattr(self.dev, "type", str(self.dev)) == "cuda"
         self.eager = (on_gpu and hasattr(backend, "signal")) if eager is None else eager
-        self.comm = torch.cuda.Stream(device=self.dev) if self.eager else None
+        self.comm = comm_stream(self.dev) if self.eager else None
         self.local = [torch.empty(pb, dtype=torch.uint8, device=self.dev) for _ in range(slots)]
         nbuf = slots if self.eager else lanes
         self.gathered = [torch.empty(self.world * pb, dtype=torch.uint8, device=self.dev) for _ in range(nbuf)]

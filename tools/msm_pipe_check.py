@@ -12,7 +12,9 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "kzg-batch-verification-scheme_amd"))
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "24")
+# as bench.py: the box exports GPU_MAX_HW_QUEUES=4 (HIP's default); force the pipeline's 24 --
+# with 4, streams share hardware queues and a stream's GPU-side wait blocks the others behind it
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("KZGMI_HW_QUEUES", "24")
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
