@@ -20,6 +20,7 @@
 #endif
 #include "consts_gen.h"
 #include "tmul_x86_gen.h"
+#include "fexp_gen.h"
 
 #define KZGO_OK 0
 #define KZGO_ERR_ARG (-1)
@@ -156,8 +157,14 @@ static const uint64_t BLS_LOOPW[2] = {BLS_LOOP, 0};
 #define RRAW BLS_FR_MOD
 #include "curve_tmpl.h"
 #define PINV_T BLS_P_INV
+#define HARD_L BLS_HARD_L
+#define HARD_NEG BLS_HARD_NEG
+#define HARD_BITS BLS_HARD_BITS
 #include "pippenger_tuned_tmpl.h"
 #undef PINV_T
+#undef HARD_L
+#undef HARD_NEG
+#undef HARD_BITS
 #undef PRAW
 #undef RRAW
 #undef FP
@@ -243,8 +250,14 @@ static const uint64_t BLS_LOOPW[2] = {BLS_LOOP, 0};
 #define RRAW BN_FR_MOD
 #include "curve_tmpl.h"
 #define PINV_T BN_P_INV
+#define HARD_L BN_HARD_L
+#define HARD_NEG BN_HARD_NEG
+#define HARD_BITS BN_HARD_BITS
 #include "pippenger_tuned_tmpl.h"
 #undef PINV_T
+#undef HARD_L
+#undef HARD_NEG
+#undef HARD_BITS
 
 /* ================================================================== C API (ctypes) */
 #define CURVE_DISPATCH(curve, call_bls, call_bn) \
@@ -277,6 +290,22 @@ int kzgo_batch_verify_tuned(int curve, const uint8_t* cm, const uint8_t* zs, con
   return CURVE_DISPATCH(
       curve, bls_batch_verify_tuned(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, do_pairing, wbits, chunk),
       bn_batch_verify_tuned(cm, zs, ys, pf, n, g2, tau_g2, seed, ok, a_out, b_out, 0, do_pairing, wbits, chunk));
+}
+
+/* e(P, Q) by the tuned verifier's pairing (precomputed Miller program, easy part + Frobenius
+ * multi-exponent hard part): the same 12 Fp values as kzgo_pairing */
+#define DEF_PFAST(C)                                                                           \
+  static int C##_pairing_fast_api(const uint8_t* g1, const uint8_t* g2, uint8_t* out) {        \
+    C##_aff P; C##_aff2 Q; int e;                                                              \
+    if ((e = C##_g1_decode(&P, g1)) || (e = C##_g2_decode(&Q, g2))) return e;                  \
+    C##_fp12 f; C##_pairing_fast(&f, &P, &Q); C##_fp12_encode(out, &f);                        \
+    return 0;                                                                                  \
+  }
+DEF_PFAST(bls)
+DEF_PFAST(bn)
+int kzgo_pairing_fast(int curve, const uint8_t* g1, const uint8_t* g2, uint8_t* out) {
+  if (!g1 || !g2 || !out) return KZGO_ERR_ARG;
+  return CURVE_DISPATCH(curve, bls_pairing_fast_api(g1, g2, out), bn_pairing_fast_api(g1, g2, out));
 }
 
 /* Powers mode (Fiat-Shamir / caller-supplied challenge): r_i = r^(offset + i), r = int_be(r32) < r.

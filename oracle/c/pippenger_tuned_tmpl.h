@@ -19,10 +19,16 @@
  *     lazy by one subtraction because the moduli leave a spare top bit (p < 2^381 / 2^254);
  *   - OpenMP over (MSM, window, point-range) tasks with dynamic scheduling, one bucket array
  *     per task (c = 13 keeps 4096 x 192 B of buckets in a core's L2).
- * The pairing check reuses C_(pairing_check) (two Miller loops + final exponentiation, a few
- * ms: not the cost at n = 2^20).  Reference: none (/root/reference/LICENSE:1-201 only).
+ * The pairing check (C_(pairing_check_fast), below) uses the same Miller loop as the oracle
+ * with its line functions precomputed once per SRS G2 pair (the T sequence depends only on Q),
+ * and a final exponentiation split into the easy part (conjugate / inverse / Frobenius^2) and
+ * the hard part as a 4-term Frobenius multi-exponent with Granger-Scott cyclotomic squarings
+ * (fexp_gen.h, oracle/gen_fexp.py) -- the same value as the oracle's plain-pow exponentiation.
+ * Reference: none (/root/reference/LICENSE:1-201 only).
  */
 typedef struct { FP x, y, zz, zzz; } C_(xyzz);  /* x = X/ZZ, y = Y/ZZZ (ZZ^3 = ZZZ^2); ZZ = 0 <=> O */
+static void C_(pairing_check_fast)(const C_(aff)* A, const C_(aff)* B, const C_(aff2)* g2, const C_(aff2)* tg2,
+                                   int* ok);
 
 /* Montgomery product (a b) / 2^(64 FN) mod p, result < p.  x86-64 with BMI2 + ADX: the
  * generated mulx/adcx/adox CIOS (tmul_x86_gen.h, two interleaved carry chains); otherwise a
@@ -330,6 +336,282 @@ static int C_(batch_verify_tuned)(const uint8_t* cm, const uint8_t* zs, const ui
   if (a_out) C_(g1_encode)(a_out, &A);
   if (b_out) C_(g1_encode)(b_out, &B);
   *ok = -1;
-  if (do_pairing) C_(pairing_check)(&A, &B, &g2, &tg2, ok);
+  if (do_pairing) C_(pairing_check_fast)(&A, &B, &g2, &tg2, ok);
   return 0;
+}
+
+/* ================================================================== fast pairing check */
+/* Frobenius f -> f^p on the tower (w^2 = v, v^3 = xi): coefficient of w^k conjugated and
+ * multiplied by g_k = xi^(k (p - 1) / 6) (computed once) */
+typedef struct { T_(fp2) g[6]; int ready; } C_(frobk);
+static C_(frobk) C_(frob_consts);
+
+static void C_(frob_init)(void) {
+  if (C_(frob_consts).ready) return;
+  enum { N = (int)(sizeof(FP) / 8) };
+  uint64_t e[N];
+  memcpy(e, PRAW, sizeof(e));
+  e[0] -= 1;  /* p - 1 (p odd: no borrow) */
+  unsigned __int128 rem = 0;
+  for (int i = N - 1; i >= 0; --i) {
+    const unsigned __int128 cur = (rem << 64) | e[i];
+    e[i] = (uint64_t)(cur / 6);
+    rem = cur % 6;
+  }
+  T_(fp2) xi, base;
+  T_(fp2_small)(&xi, XI_A, 1);
+  T_(fp2_pow)(&base, &xi, e, 64 * N);
+  C_(frobk) k;
+  T_(fp2_one)(&k.g[0]);
+  for (int i = 1; i < 6; ++i) T_(fp2_mul)(&k.g[i], &k.g[i - 1], &base);
+  k.ready = 1;
+  #pragma omp critical(kzgo_frob)
+  C_(frob_consts) = k;
+}
+
+static void C_(frob12)(T_(fp12)* r, const T_(fp12)* a) {
+  const T_(fp2)* g = C_(frob_consts).g;
+  T_(fp2)* dst[6] = {&r->c0.c0, &r->c1.c0, &r->c0.c1, &r->c1.c1, &r->c0.c2, &r->c1.c2};  /* w^0 .. w^5 */
+  const T_(fp2)* src[6] = {&a->c0.c0, &a->c1.c0, &a->c0.c1, &a->c1.c1, &a->c0.c2, &a->c1.c2};
+  T_(fp12) t;
+  T_(fp2)* tdst[6] = {&t.c0.c0, &t.c1.c0, &t.c0.c1, &t.c1.c1, &t.c0.c2, &t.c1.c2};
+  for (int k = 0; k < 6; ++k) {
+    T_(fp2) c;
+    T_(fp2_conj)(&c, src[k]);
+    T_(fp2_mul)(tdst[k], &c, &g[k]);
+  }
+  for (int k = 0; k < 6; ++k) *dst[k] = *tdst[k];
+}
+
+static void C_(fp6_sub)(T_(fp6)* r, const T_(fp6)* a, const T_(fp6)* b) {
+  T_(fp2_sub)(&r->c0, &a->c0, &b->c0); T_(fp2_sub)(&r->c1, &a->c1, &b->c1); T_(fp2_sub)(&r->c2, &a->c2, &b->c2);
+}
+
+/* (a0 + a1 v + a2 v^2)^-1 = (A + B v + C v^2) / F: A = a0^2 - xi a1 a2, B = xi a2^2 - a0 a1,
+ * C = a1^2 - a0 a2, F = a0 A + xi (a2 B + a1 C) */
+static void C_(fp6_inv)(T_(fp6)* r, const T_(fp6)* a) {
+  T_(fp2) A, B, C, F, t, u;
+  T_(fp2_mul)(&A, &a->c0, &a->c0); T_(fp2_mul)(&t, &a->c1, &a->c2); T_(fp2_mul_xi)(&t, &t); T_(fp2_sub)(&A, &A, &t);
+  T_(fp2_mul)(&B, &a->c2, &a->c2); T_(fp2_mul_xi)(&B, &B); T_(fp2_mul)(&t, &a->c0, &a->c1); T_(fp2_sub)(&B, &B, &t);
+  T_(fp2_mul)(&C, &a->c1, &a->c1); T_(fp2_mul)(&t, &a->c0, &a->c2); T_(fp2_sub)(&C, &C, &t);
+  T_(fp2_mul)(&t, &a->c2, &B); T_(fp2_mul)(&u, &a->c1, &C); T_(fp2_add)(&t, &t, &u); T_(fp2_mul_xi)(&t, &t);
+  T_(fp2_mul)(&F, &a->c0, &A); T_(fp2_add)(&F, &F, &t);
+  T_(fp2_inv)(&F, &F);
+  T_(fp2_mul)(&r->c0, &A, &F); T_(fp2_mul)(&r->c1, &B, &F); T_(fp2_mul)(&r->c2, &C, &F);
+}
+
+/* (c0 + c1 w)^-1 = (c0 - c1 w) / (c0^2 - v c1^2) */
+static void C_(fp12_inv)(T_(fp12)* r, const T_(fp12)* a) {
+  T_(fp6) t0, t1, ti;
+  T_(fp6_mul)(&t0, &a->c0, &a->c0);
+  T_(fp6_mul)(&t1, &a->c1, &a->c1);
+  T_(fp6_mul_v)(&t1, &t1);
+  C_(fp6_sub)(&t0, &t0, &t1);
+  C_(fp6_inv)(&ti, &t0);
+  T_(fp6_mul)(&r->c0, &a->c0, &ti);
+  T_(fp6_mul)(&t1, &a->c1, &ti);
+  T_(fp6_neg)(&r->c1, &t1);
+}
+
+/* Granger-Scott squaring in the cyclotomic subgroup (the formula of
+ * kzg-batch-verification-scheme_amd/tools/gen_bilinear.py cyclo_sqr, in this tower) */
+static void C_(fp4_sqr)(T_(fp2)* r0, T_(fp2)* r1, const T_(fp2)* a, const T_(fp2)* b) {
+  T_(fp2) t0, t1, s;
+  T_(fp2_mul)(&t0, a, a);
+  T_(fp2_mul)(&t1, b, b);
+  T_(fp2_add)(&s, a, b); T_(fp2_mul)(&s, &s, &s); T_(fp2_sub)(&s, &s, &t0); T_(fp2_sub)(r1, &s, &t1);
+  T_(fp2_mul_xi)(&t1, &t1); T_(fp2_add)(r0, &t1, &t0);
+}
+static void C_(cyc_sqr)(T_(fp12)* r, const T_(fp12)* f) {
+  const T_(fp2) z0 = f->c0.c0, z1 = f->c1.c1, z2 = f->c1.c0, z3 = f->c0.c2, z4 = f->c0.c1, z5 = f->c1.c2;
+  T_(fp2) t0, t1, t2, t3, t4, t5, u;
+  C_(fp4_sqr)(&t0, &t1, &z0, &z1);
+  C_(fp4_sqr)(&t2, &t3, &z2, &z3);
+  C_(fp4_sqr)(&t4, &t5, &z4, &z5);
+  /* r00 = 3 t0 - 2 z0; r11 = 3 t1 + 2 z1; r10 = 3 xi t5 + 2 z2; r02 = 3 t4 - 2 z3; r01 = 3 t2 - 2 z4; r12 = 3 t3 + 2 z5 */
+#define KZGO_CYC(dst, tv, zv, sign)                                            \
+  do {                                                                         \
+    if (sign) T_(fp2_add)(&u, &tv, &zv); else T_(fp2_sub)(&u, &tv, &zv);        \
+    T_(fp2_add)(&u, &u, &u); T_(fp2_add)(&dst, &u, &tv);                         \
+  } while (0)
+  T_(fp12) o;
+  KZGO_CYC(o.c0.c0, t0, z0, 0);
+  KZGO_CYC(o.c1.c1, t1, z1, 1);
+  T_(fp2) xt5; T_(fp2_mul_xi)(&xt5, &t5);
+  KZGO_CYC(o.c1.c0, xt5, z2, 1);
+  KZGO_CYC(o.c0.c2, t4, z3, 0);
+  KZGO_CYC(o.c0.c1, t2, z4, 0);
+  KZGO_CYC(o.c1.c2, t3, z5, 1);
+#undef KZGO_CYC
+  *r = o;
+}
+
+/* f^((p^12 - 1) / r * k): easy part, then the hard part as prod_i frob^i(g)^(l_i) by a joint
+ * square-and-multiply over a 16-entry table (fexp_gen.h: k = 3 on BLS12-381, as the oracle) */
+static void C_(final_exp_fast)(T_(fp12)* r, const T_(fp12)* f) {
+  C_(frob_init)();
+  T_(fp12) a, b, g;
+  C_(fp12_inv)(&a, f);
+  T_(fp12_conj)(&b, f);
+  T_(fp12_mul)(&a, &b, &a);          /* f^(p^6 - 1) */
+  C_(frob12)(&b, &a);
+  C_(frob12)(&b, &b);
+  T_(fp12_mul)(&g, &b, &a);          /* ^(p^2 + 1) */
+  T_(fp12) base[4], tab[16];
+  base[0] = g;
+  for (int i = 1; i < 4; ++i) C_(frob12)(&base[i], &base[i - 1]);
+  for (int i = 0; i < 4; ++i)
+    if (HARD_NEG[i]) T_(fp12_conj)(&base[i], &base[i]);  /* cyclotomic inverse */
+  T_(fp12_one)(&tab[0]);
+  for (int m = 1; m < 16; ++m) {
+    int lo = 0;
+    while (!((m >> lo) & 1)) ++lo;
+    T_(fp12_mul)(&tab[m], &tab[m & (m - 1)], &base[lo]);
+  }
+  T_(fp12) acc;
+  T_(fp12_one)(&acc);
+  for (int bit = HARD_BITS - 1; bit >= 0; --bit) {
+    C_(cyc_sqr)(&acc, &acc);
+    int m = 0;
+    for (int i = 0; i < 4; ++i) m |= (int)((HARD_L[i][bit >> 6] >> (bit & 63)) & 1) << i;
+    if (m) T_(fp12_mul)(&acc, &acc, &tab[m]);
+  }
+  *r = acc;
+}
+
+/* Miller loop of C_(miller) as a program precomputed from Q alone: every T step's line
+ * (slope lam, c = yT - lam xT) or vertical (xT), the squarings and the final conjugation */
+enum { C_(OP_SQR) = 0, C_(OP_LINE) = 1, C_(OP_VERT) = 2, C_(OP_CONJ) = 3 };
+typedef struct { int op; T_(fp2) lam, c; } C_(mop);
+#define KZGO_MAXOPS 320
+typedef struct { int n; C_(mop) ops[KZGO_MAXOPS]; } C_(mprog);
+
+static void C_(pre_step)(C_(mprog)* pr, C_(aff2)* T, const C_(aff2)* Q) {
+  if (T->inf) { *T = *Q; return; }
+  if (Q->inf) return;
+  T_(fp2) lam, t, u;
+  if (T_(fp2_eq)(&T->x, &Q->x)) {
+    T_(fp2_add)(&t, &T->y, &Q->y);
+    if (T_(fp2_is_zero)(&t)) {
+      C_(mop)* o = &pr->ops[pr->n++];
+      o->op = C_(OP_VERT); o->c = T->x;
+      memset(T, 0, sizeof(*T)); T->inf = 1; return;
+    }
+    T_(fp2_mul)(&t, &T->x, &T->x); T_(fp2_add)(&u, &t, &t); T_(fp2_add)(&t, &u, &t);
+    T_(fp2_add)(&u, &T->y, &T->y); T_(fp2_inv)(&u, &u); T_(fp2_mul)(&lam, &t, &u);
+  } else {
+    T_(fp2_sub)(&t, &Q->y, &T->y); T_(fp2_sub)(&u, &Q->x, &T->x);
+    T_(fp2_inv)(&u, &u); T_(fp2_mul)(&lam, &t, &u);
+  }
+  C_(mop)* o = &pr->ops[pr->n++];
+  o->op = C_(OP_LINE); o->lam = lam;
+  T_(fp2_mul)(&o->c, &lam, &T->x); T_(fp2_sub)(&o->c, &T->y, &o->c);   /* yT - lam xT */
+  T_(fp2) x3, y3;
+  T_(fp2_mul)(&x3, &lam, &lam); T_(fp2_sub)(&x3, &x3, &T->x); T_(fp2_sub)(&x3, &x3, &Q->x);
+  T_(fp2_sub)(&t, &T->x, &x3); T_(fp2_mul)(&y3, &lam, &t); T_(fp2_sub)(&y3, &y3, &T->y);
+  T->x = x3; T->y = y3;
+}
+
+static void C_(miller_pre)(C_(mprog)* pr, const C_(aff2)* Q) {
+  pr->n = 0;
+  if (Q->inf) return;
+  C_(aff2) T = *Q;
+  for (int i = LOOP_BITS - 2; i >= 0; --i) {
+    pr->ops[pr->n++].op = C_(OP_SQR);
+    C_(aff2) Tc = T;
+    C_(pre_step)(pr, &T, &Tc);
+    if ((LOOP_WORDS[i / 64] >> (i % 64)) & 1) C_(pre_step)(pr, &T, Q);
+  }
+#if IS_BLS
+  pr->ops[pr->n++].op = C_(OP_CONJ);
+#else
+  C_(aff2) Q1, Q2;
+  C_(frob_twist)(&Q1, Q);
+  C_(frob_twist)(&Q2, &Q1);
+  T_(fp2_neg)(&Q2.y, &Q2.y);
+  C_(pre_step)(pr, &T, &Q1);
+  C_(pre_step)(pr, &T, &Q2);
+#endif
+}
+
+static void C_(miller_eval)(T_(fp12)* f, const C_(mprog)* pr, const C_(aff)* P) {
+  T_(fp12_one)(f);
+  if (P->inf || pr->n == 0) return;
+  for (int k = 0; k < pr->n; ++k) {
+    const C_(mop)* o = &pr->ops[k];
+    T_(fp12) l;
+    if (o->op == C_(OP_SQR)) {
+      T_(fp12_mul)(f, f, f);
+    } else if (o->op == C_(OP_CONJ)) {
+      T_(fp12_conj)(f, f);
+    } else if (o->op == C_(OP_LINE)) {
+      memset(&l, 0, sizeof(l));
+      T_(fp2) b, c;
+      T_(fp2_mul_fp)(&b, &o->lam, &P->x);                  /* lam xP */
+      T_(fp2_zero)(&c); FP_(neg)(&c.c0, &P->y);            /* -yP */
+#if IS_BLS
+      l.c0.c0 = o->c; l.c0.c1 = b; l.c1.c1 = c;
+#else
+      l.c0.c0 = c; l.c1.c0 = b; l.c1.c1 = o->c;
+#endif
+      T_(fp12_mul)(f, f, &l);
+    } else {
+      C_(aff2) Tv;
+      memset(&Tv, 0, sizeof(Tv));
+      Tv.x = o->c;
+      C_(vertical)(&l, &Tv, P);
+      T_(fp12_mul)(f, f, &l);
+    }
+  }
+}
+
+/* line programs of the last SRS G2 pair seen (the SRS is fixed across a run's batches) */
+typedef struct { int valid; uint8_t key[8 * FPB]; C_(mprog) g2, tg2; } C_(pcache_t);
+static C_(pcache_t) C_(pcache);
+
+static void C_(pairing_check_fast)(const C_(aff)* A, const C_(aff)* B, const C_(aff2)* g2, const C_(aff2)* tg2,
+                                   int* ok) {
+  uint8_t key[8 * FPB];
+  C_(g2_encode)(key, g2);
+  C_(g2_encode)(key + 4 * FPB, tg2);
+  const C_(mprog)* pg2;
+  const C_(mprog)* ptg2;
+  C_(mprog)* own = NULL;
+  int hit = 0;
+  #pragma omp critical(kzgo_pcache)
+  {
+    if (!C_(pcache).valid || memcmp(C_(pcache).key, key, sizeof(key))) {
+      C_(miller_pre)(&C_(pcache).g2, g2);
+      C_(miller_pre)(&C_(pcache).tg2, tg2);
+      memcpy(C_(pcache).key, key, sizeof(key));
+      C_(pcache).valid = 1;
+    }
+    own = (C_(mprog)*)malloc(2 * sizeof(C_(mprog)));  /* private copy: the cache may be refilled */
+    memcpy(&own[0], &C_(pcache).g2, sizeof(C_(mprog)));
+    memcpy(&own[1], &C_(pcache).tg2, sizeof(C_(mprog)));
+    hit = 1;
+  }
+  (void)hit;
+  pg2 = &own[0];
+  ptg2 = &own[1];
+  C_(aff) nB;
+  C_(aff_neg)(&nB, B);
+  T_(fp12) f1, f2, f;
+  C_(miller_eval)(&f1, ptg2, A);
+  C_(miller_eval)(&f2, pg2, &nB);
+  T_(fp12_mul)(&f, &f1, &f2);
+  C_(final_exp_fast)(&f, &f);
+  *ok = T_(fp12_is_one)(&f);
+  free(own);
+}
+
+/* e(P, Q) through the fast Miller program + final exponentiation (tests compare it with the
+ * oracle's C_(miller) + plain-pow exponentiation) */
+static void C_(pairing_fast)(T_(fp12)* r, const C_(aff)* P, const C_(aff2)* Q) {
+  C_(mprog)* pr = (C_(mprog)*)malloc(sizeof(C_(mprog)));
+  C_(miller_pre)(pr, Q);
+  T_(fp12) f;
+  C_(miller_eval)(&f, pr, P);
+  free(pr);
+  C_(final_exp_fast)(r, &f);
 }

@@ -54,6 +54,7 @@ def lib():
         L.kzgo_batch_verify_tuned.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p, c.c_char_p, c.c_size_t,
                                               c.c_char_p, c.c_char_p, c.c_char_p, c.c_int, c.c_size_t, c.c_int,
                                               c.POINTER(c.c_int), c.c_char_p, c.c_char_p]
+        L.kzgo_pairing_fast.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_char_p]
         L.kzgo_fr_dot.argtypes = [c.c_int, c.c_char_p, c.c_char_p, c.c_size_t, c.c_char_p]
         L.kzgo_set_threads.argtypes = [c.c_int]
         L.kzgo_get_threads.restype = c.c_int
@@ -189,6 +190,13 @@ def g1_mul_gen(curve, scalars: bytes, n: int) -> bytes:
 def pairing(curve, g1: bytes, g2: bytes) -> bytes:
     out = ctypes.create_string_buffer(12 * FP_BYTES[curve])
     _check(lib().kzgo_pairing(CURVE_IDS[curve], g1, g2, out))
+    return out.raw
+
+
+def pairing_fast(curve, g1: bytes, g2: bytes) -> bytes:
+    """The tuned verifier's pairing (same value as pairing())."""
+    out = ctypes.create_string_buffer(12 * FP_BYTES[curve])
+    _check(lib().kzgo_pairing_fast(CURVE_IDS[curve], g1, g2, out))
     return out.raw
 
 

@@ -78,6 +78,18 @@ def test_tuned_verifier_golden(curve, golden):
 
 
 @pytest.mark.parametrize("curve", CURVES)
+def test_tuned_pairing_equals_oracle(curve, golden):
+    """The tuned verifier's pairing (Miller program precomputed from Q, easy part + 4-term
+    Frobenius multi-exponent hard part with cyclotomic squarings, oracle/gen_fexp.py) gives the
+    oracle's 12 Fp values bit for bit, on the golden pairs and on the point at infinity."""
+    g = golden("%s_pairing.json" % curve)
+    for P, Q in ((g["g1"], g["g2"]), (g["aP"], g["bQ"]), (g["g1"], g["bQ"])):
+        assert O.pairing_fast(curve, h(P), h(Q)) == O.pairing(curve, h(P), h(Q))
+    inf = bytes([0x40]) + bytes(95) if curve == "bls12_381" else bytes(64)
+    assert O.pairing_fast(curve, inf, h(g["g2"])) == O.pairing(curve, inf, h(g["g2"]))
+
+
+@pytest.mark.parametrize("curve", CURVES)
 def test_tuned_verifier_vs_oracle_random(curve):
     """Random points (not openings: the verdict is False) with repeated and infinity points,
     A, B of the tuned verifier == the oracle's; empty batch accepts; errors as the oracle's."""
