@@ -692,8 +692,11 @@ def main():
             cts.append(e0.elapsed_time(e1))
         copy_ms = statistics.median(cts[1:])
         del hp, dp
+        ctx.set_profiling(True)
         rate_pinned = pipelined_rate(ctx, slots, args.h2d_steps,
                                      lambda s_: ctx.batch_verify_host_async(srs, s_, *views, seed=vseed))
+        ph_pipe_pin = ctx.phase_ms()
+        ctx.set_profiling(False)
         rate_pageable = pipelined_rate(ctx, slots, max(1, args.h2d_steps // 2),
                                        lambda s_: ctx.batch_verify_host_async(srs, s_, *host_np, seed=vseed))
         # one synchronous host-buffer batch per kind, phases on the slot's stream (h2d = the copy)
@@ -718,6 +721,7 @@ def main():
             "pcie_probe": "one %d-B pinned -> HBM copy (torch non_blocking copy, HIP events), median of 5" % batch_bytes,
             "copy_ms_per_batch_probe": copy_ms,
             "h2d_ms_single_batch_pinned": ph_pin.get("h2d"),
+            "phase_ms_avg_in_timed_region_pinned": ph_pipe_pin,
             "h2d_ms_single_batch_pageable": ph_page.get("h2d"),
             "single_batch_latency_ms_pageable": lat_pageable,
             "kernel_ms_per_step_hbm_resident": kernel_step_ms,
