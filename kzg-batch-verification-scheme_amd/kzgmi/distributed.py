@@ -148,7 +148,7 @@ class ShardedPipeline:
         self.dev = backend.tensor_device()
         on_gpu = getattr(self.dev, "type", str(self.dev)) == "cuda"
         self.eager = (on_gpu and hasattr(backend, "signal")) if eager is None else eager
-        self.comm = comm_stream(self.dev) if self.eager else None
+        self.comm = comm_stream(self.dev) if self.eager and on_gpu else None  # CPU test doubles: no stream
         self.local = [torch.empty(2 * pb, dtype=torch.uint8, device=self.dev) for _ in range(slots)]
         # one gather buffer per slot (eager) / lane (deferred): the combine reads it until the
         # slot / lane is reused
@@ -178,9 +178,10 @@ class ShardedPipeline:
         self.lane_pending[lane] = True
 
     def _enqueue_eager(self, s: int):
+        import contextlib
         import torch
         import torch.distributed as dist
-        with torch.cuda.stream(self.comm):
+        with (torch.cuda.stream(self.comm) if self.comm is not None else contextlib.nullcontext()):
             self.backend.signal(s, self.comm)                  # the side stream waits for the partial
             dist.all_gather_into_tensor(self.gathered[s], self.local[s], group=self.group)
             # chained on slot s, ordered after torch's current stream (= the side stream)
@@ -253,7 +254,7 @@ class ShardedMsmPipeline:
         self.dev = backend.tensor_device()
         on_gpu = getattr(self.dev, "type", str(self.dev)) == "cuda"
         self.eager = (on_gpu and hasattr(backend, "signal")) if eager is None else eager
-        self.comm = comm_stream(self.dev) if self.eager else None
+        self.comm = comm_stream(self.dev) if self.eager and on_gpu else None
         self.local = [torch.empty(pb, dtype=torch.uint8, device=self.dev) for _ in range(slots)]
         nbuf = slots if self.eager else lanes
         self.gathered = [torch.empty(self.world * pb, dtype=torch.uint8, device=self.dev) for _ in range(nbuf)]
@@ -279,9 +280,10 @@ class ShardedMsmPipeline:
         self.lane_pending[lane] = True
 
     def _enqueue_eager(self, s: int):
+        import contextlib
         import torch
         import torch.distributed as dist
-        with torch.cuda.stream(self.comm):
+        with (torch.cuda.stream(self.comm) if self.comm is not None else contextlib.nullcontext()):
             self.backend.signal(s, self.comm)
             dist.all_gather_into_tensor(self.gathered[s], self.local[s], group=self.group)
             self.backend.msm_combine_async(self.curve, s, self.gathered[s], self.world)

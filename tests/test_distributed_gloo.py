@@ -159,7 +159,16 @@ def _worker(rank, world, port, curve, n_total, corrupt_index, result_q):
     dist.destroy_process_group()
 
 
-def _pipeline_worker(rank, world, port, curve, n_total, corrupt_batches, result_q):
+class EagerOracleBackend(OracleBackend):
+    """The double with kzgmi_slot_signal (a no-op on CPU) and chained combines -- a combine on a
+    slot whose pending job is a partial replaces that slot's result, as the library's chaining
+    does -- so ShardedPipeline runs its eager schedule."""
+
+    def signal(self, slot, stream=None):
+        pass
+
+
+def _pipeline_worker(rank, world, port, curve, n_total, corrupt_batches, result_q, eager=False):
     """4 global batches through a 2-slot ShardedPipeline; batch b corrupts tuple b*3 if listed."""
     import sys
     sys.path.insert(0, ROOT)
@@ -176,8 +185,9 @@ def _pipeline_worker(rank, world, port, curve, n_total, corrupt_batches, result_
     C, z, y, P = (h(g[k]) for k in ("commitments", "zs", "ys", "proofs"))
     off, cnt = shard_range(n_total, world, rank)
     g1b = len(C) // n_total
-    be = OracleBackend(curve, h(g["g2"]), h(g["tau_g2"]))
-    pipe = ShardedPipeline(be, FakeSrs(curve), slots=2, lanes=2)
+    be = (EagerOracleBackend if eager else OracleBackend)(curve, h(g["g2"]), h(g["tau_g2"]))
+    pipe = ShardedPipeline(be, FakeSrs(curve), slots=2, lanes=0 if eager else 2, eager=eager)
+    assert pipe.eager is eager
     verdicts = []
     for b in range(4):
         yb = bytearray(y)
@@ -243,7 +253,7 @@ def _fs_worker(rank, world, port, curve, n_total, tau, corrupt, result_q):
     dist.destroy_process_group()
 
 
-def _msm_worker(rank, world, port, curve, n_total, result_q):
+def _msm_worker(rank, world, port, curve, n_total, result_q, eager=False):
     import random
     import sys
     sys.path.insert(0, ROOT)
@@ -267,7 +277,9 @@ def _msm_worker(rank, world, port, curve, n_total, result_q):
     t = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8)  # noqa: E731
     lp = t(pts[off * g1b:(off + cnt) * g1b] or bytes(1))
     ls = [t(sc[off * 32:(off + cnt) * 32] or bytes(1)) for sc in scs]
-    pipe = ShardedMsmPipeline(OracleBackend(curve, None, None), curve, slots=2, lanes=2)
+    be = (EagerOracleBackend if eager else OracleBackend)(curve, None, None)
+    pipe = ShardedMsmPipeline(be, curve, slots=2, lanes=0 if eager else 2, eager=eager)
+    assert pipe.eager is eager
     order = [0, 1, 1, 0, 0]
     out = []
     for b in order:
@@ -306,12 +318,17 @@ def test_sharded_verify_world2(curve, n, corrupt, expect):
     assert [ok for _, ok in res] == [expect, expect]
 
 
-def test_sharded_pipeline_world2():
+@pytest.mark.parametrize("eager", [False, True])
+def test_sharded_pipeline_world2(eager):
+    """Both schedules of ShardedPipeline across 2 gloo ranks: deferred (host waits each partial,
+    2 combine lanes) and eager (gather + combine enqueued right behind the partial, the combine
+    chained on the partial's slot): verdicts in submission order on every rank."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipeline_worker, args=(r, 2, port, "bls12_381", 16, (1, 2), q)) for r in range(2)]
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, 2, port, "bls12_381", 16, (1, 2), q, eager))
+             for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -340,14 +357,16 @@ def test_sharded_fiat_shamir_world2(n_total, corrupt, expect):
     assert [(same, ok) for _, same, ok in res] == [(True, expect)] * 2
 
 
-def test_sharded_msm_pipeline_world2():
-    """ShardedMsmPipeline across 2 gloo ranks: shard partials, all-gather, combine lanes;
-    every rank gets the global MSM of every submission, in order."""
+@pytest.mark.parametrize("eager", [False, True])
+def test_sharded_msm_pipeline_world2(eager):
+    """ShardedMsmPipeline across 2 gloo ranks, both schedules: shard partials, all-gather,
+    combine lanes (deferred) or combines chained on the partial's slot (eager); every rank gets
+    the global MSM of every submission, in order."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_msm_worker, args=(r, 2, port, "bls12_381", 37, q)) for r in range(2)]
+    procs = [ctx.Process(target=_msm_worker, args=(r, 2, port, "bls12_381", 37, q, eager)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
