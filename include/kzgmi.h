@@ -121,7 +121,10 @@ int kzgmi_ctx_num_devices(const kzgmi_ctx* ctx);
  * steady state calls this first.  No job may be in flight.  On a multi-device context each
  * peer is sized for its share of the library's own balanced split (what the host-buffer entry
  * points use): shards passed to kzgmi_batch_verify_multi_device that are larger than
- * ceil(n / n_devices) rounded up to 4096 still grow the peer's workspace on first use. */
+ * ceil(n / n_devices) rounded up to 4096 still grow the peer's workspace on first use.  The
+ * host-buffer entry points also use a per-slot device staging buffer (n x (2 G1 + 64) B) and,
+ * for pageable inputs, a per-slot pinned ring (2 x 16 MiB): these are made on a slot's first
+ * host-buffer call, so a timed steady state of host-buffer calls warms every slot once first. */
 int kzgmi_ctx_reserve(kzgmi_ctx* ctx, kzgmi_curve curve, size_t n, uint32_t flags);
 /* Process-wide number of device workspace allocations the library has made so far (a timed
  * region that leaves it unchanged allocated nothing). */
