@@ -399,6 +399,29 @@ def test_generated_batch_vs_oracle(ctx, curve, torch_dev):
 
 
 @pytest.mark.parametrize("curve", CURVES)
+def test_evaluation_point_at_tau(ctx, curve, torch_dev):
+    """SURVEY.md 4.4's last negative case: one tuple opened at z_i = tau (the trapdoor itself) with
+    its proof left as generated.  The check must reject, and A, B match the oracle bit for bit (the
+    point is a regular scalar to both: nothing special-cases z = tau)."""
+    torch = torch_dev
+    C = pc.CURVES[curve]
+    n, tau = 300, 0x1234567890ABCDEF1234567890
+    Cm, z, y, P = _gen_batch(ctx, torch, curve, n, tau, hashlib.sha256(b"z-at-tau").digest())
+    g2 = pk.g2_to_bytes(C.g2, C)
+    tg2 = O.g2_mul(curve, g2, tau)
+    srs = ctx.load_srs(curve, g2, tg2)
+    vseed = hashlib.sha256(b"verify-tau").digest()
+    assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n) is True
+    z2 = z.clone()
+    z2[32 * 77:32 * 78] = torch.frombuffer(bytearray(tau.to_bytes(32, "big")), dtype=torch.uint8).cuda()
+    assert ctx.batch_verify(srs, Cm, z2, y, P, seed=vseed, n=n) is False
+    A, B = ctx.last_combination(curve)
+    hb = [t.cpu().numpy().tobytes() for t in (Cm, z2, y, P)]
+    ok, Ao, Bo = O.batch_verify(curve, hb[0], hb[1], hb[2], hb[3], n, g2, tg2, vseed, want_ab=True)
+    assert ok is False and A == Ao and B == Bo
+
+
+@pytest.mark.parametrize("curve", CURVES)
 def test_async_slots(ctx, curve, torch_dev):
     torch = torch_dev
     C = pc.CURVES[curve]
