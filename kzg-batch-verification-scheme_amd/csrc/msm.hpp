@@ -860,6 +860,22 @@ __device__ __noinline__ Xy29<Q> dbl_affine29(const F29<Q> qx, const F29<Q> qy, u
   return o;
 }
 
+// R29 mod p (Montgomery one) in registers from literal moves at the point of use: two limbs per
+// asm statement (one s_nop pad each), nothing the compiler can hoist and keep live (or spill)
+// across the accumulation loop.
+template <class Q, int K>
+KZ_DEV void one_pair(F29<Q>& r) {
+  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=v"(r.v[2 * K]), "=v"(r.v[2 * K + 1])
+               : "i"(Q::ONE[2 * K]), "i"(Q::ONE[2 * K + 1]));
+}
+template <class Q, int... K>
+KZ_DEV F29<Q> one_literals(std::integer_sequence<int, K...>) {
+  F29<Q> r;
+  (one_pair<Q, K>(r), ...);
+  if constexpr (Q::N % 2) asm volatile("v_mov_b32 %0, %1" : "=v"(r.v[Q::N - 1]) : "i"(Q::ONE[Q::N - 1]));
+  return r;
+}
+
 // The mixed-addition loop.  Bounds (values, all normalised), BLS12-381: q.x < p, q.y < 8p;
 // x < 10p; y < 16p; zz, zzz < 2p; products < 2p -- only two biased multiples of p (8p, 16p),
 // so few constants stay live across the loop.  BN254 (R29 / p ~ 169, no such headroom): q.y <
@@ -943,11 +959,33 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
     // their use; chunks start 16-B aligned, acc_chunk_len): each lane walks its own run, so a
     // per-entry 4-B load re-fetched the run's sector from beyond L2 for most entries.  A bucket
     // change is the SV_FIRST bit of the value; the key is read only then (a flush).
+#ifndef KZ_ACC_VQ_REGS  // (A/B reference: the 4 values in registers, spilled to scratch and back
+    // around the addition at 128 VGPRs: 177.1 vs 179.4 batch-verifies/s, profiles/r04/ab_acc_vq_lds.txt)
+    // The 4 values of a group land in LDS by an asynchronous global_load_lds_dwordx4, one group
+    // ahead; no VGPR holds them across the addition.
+    __shared__ uint4 s_vq[256];
+    uint4* const vq_wave = &s_vq[tx & ~63u];  // each lane's 16 B land at vq_wave[lane]
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(sorted_val + (e & ~3u)), vq_wave, 16, 0, 0);
+    for (; e < end; ++e) {
+      const uint32_t j = e & 3u;
+#ifdef KZ_ACC_VQ_MBCNT  // A/B: the lane's slot from v_mbcnt each iteration (no loop-invariant address VGPR)
+      uint32_t lane;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+      const uint32_t v = reinterpret_cast<const uint32_t*>(&s_vq[(tx & ~63u) + lane])[j];
+#else
+      const uint32_t v = reinterpret_cast<const uint32_t*>(&s_vq[tx])[j];
+#endif
+      if (j == 3) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): v is read before the next group lands over it
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(sorted_val + e + 1), vq_wave, 16, 0, 0);
+      }
+#else
     uint4 vq = *reinterpret_cast<const uint4*>(sorted_val + (e & ~3u));  // may read 3 past total: padded
     for (; e < end; ++e) {
       const uint32_t j = e & 3u;  // wave-uniform (every lane's chunk starts at a multiple of 4)
       const uint32_t v = j == 0 ? vq.x : j == 1 ? vq.y : j == 2 ? vq.z : vq.w;
       if (j == 3) vq = *reinterpret_cast<const uint4*>(sorted_val + e + 1);
+#endif
       if ((v & SV_FIRST) && e != start) {
         flush(x, y, cur, inf, false);
         inf = true;
@@ -959,8 +997,16 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
       if (inf) {
         x = qx;
         y = qy;
+#ifdef KZ_ACC_ONE_LIT  // A/B: ONE as literal moves here (no VGPRs holding it across the loop)
+        {
+          const G one = one_literals<Q>(std::make_integer_sequence<int, N / 2>{});
+          st(s_zz, one);
+          st(s_zzz, one);
+        }
+#else
         st(s_zz, G::from_const(Q::ONE));
         st(s_zzz, G::from_const(Q::ONE));
+#endif
         inf = false;
         continue;
       }
