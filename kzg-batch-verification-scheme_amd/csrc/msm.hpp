@@ -962,19 +962,19 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
 #ifndef KZ_ACC_VQ_REGS  // (A/B reference: the 4 values in registers, spilled to scratch and back
     // around the addition at 128 VGPRs: 177.1 vs 179.4 batch-verifies/s, profiles/r04/ab_acc_vq_lds.txt)
     // The 4 values of a group land in LDS by an asynchronous global_load_lds_dwordx4, one group
-    // ahead; no VGPR holds them across the addition.
+    // ahead; no VGPR holds them across the addition.  With the lane slot from v_mbcnt and ONE
+    // from literals (below) the loop has no scratch traffic at all and needs 123 VGPRs (180.4 vs
+    // 179.4/s, profiles/r04/ab_acc_spill_free.txt).
     __shared__ uint4 s_vq[256];
     uint4* const vq_wave = &s_vq[tx & ~63u];  // each lane's 16 B land at vq_wave[lane]
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(sorted_val + (e & ~3u)), vq_wave, 16, 0, 0);
     for (; e < end; ++e) {
       const uint32_t j = e & 3u;
-#ifdef KZ_ACC_VQ_MBCNT  // A/B: the lane's slot from v_mbcnt each iteration (no loop-invariant address VGPR)
+      // the lane's slot from v_mbcnt every iteration: a loop-invariant address VGPR was spilled
+      // and reloaded from scratch around the addition
       uint32_t lane;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
       const uint32_t v = reinterpret_cast<const uint32_t*>(&s_vq[(tx & ~63u) + lane])[j];
-#else
-      const uint32_t v = reinterpret_cast<const uint32_t*>(&s_vq[tx])[j];
-#endif
       if (j == 3) {
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): v is read before the next group lands over it
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(sorted_val + e + 1), vq_wave, 16, 0, 0);
@@ -997,16 +997,11 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
       if (inf) {
         x = qx;
         y = qy;
-#ifdef KZ_ACC_ONE_LIT  // A/B: ONE as literal moves here (no VGPRs holding it across the loop)
-        {
+        {  // ONE from literal moves here: the constant held in VGPRs across the loop was spilled
           const G one = one_literals<Q>(std::make_integer_sequence<int, N / 2>{});
           st(s_zz, one);
           st(s_zzz, one);
         }
-#else
-        st(s_zz, G::from_const(Q::ONE));
-        st(s_zzz, G::from_const(Q::ONE));
-#endif
         inf = false;
         continue;
       }
