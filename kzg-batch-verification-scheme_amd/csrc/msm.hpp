@@ -1054,8 +1054,11 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
 #ifndef KZ_ACC29_WAVES
 #define KZ_ACC29_WAVES 4
 #endif
+#ifndef KZ_ACC29_WAVES_BN  // BN254's 9-limb loop (A/B knob)
+#define KZ_ACC29_WAVES_BN KZ_ACC29_WAVES
+#endif
 template <class Cv>
-constexpr int kAccWaves = kAcc29<Cv> ? KZ_ACC29_WAVES : 4;
+constexpr int kAccWaves = kAcc29<Cv> ? (Cv::ID == 1 ? KZ_ACC29_WAVES_BN : KZ_ACC29_WAVES) : 4;
 
 template <class Cv>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWaves<Cv>))) k_accumulate(const uint32_t* __restrict__ total_p,
