@@ -469,7 +469,7 @@ def main():
         lat = 1e3 * ts[len(ts) // 2]
         lat_runs = [1e3 * t for t in ts]
         ctx.set_profiling(True)
-        for _ in range(2):
+        for _ in range(6):  # phase means over 6 batches (2 read up to ~3 % apart run to run)
             assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n)
         phases_single = ctx.phase_ms()
         ctx.set_profiling(False)
