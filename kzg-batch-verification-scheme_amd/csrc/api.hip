@@ -136,6 +136,7 @@ struct kzgmi_ctx {
   size_t acc_threads_env = 0;  // KZGMI_ACC_THREADS override of that cap (0 = none)
   int acc_queue = ACC_QUEUE_FACTOR;  // KZGMI_ACC_QUEUE: chunks per capped thread (<= 1: static grid)
   size_t acc_queue_min = ACC_QUEUE_MIN_LEN;  // KZGMI_ACC_QUEUE_MIN: shortest queue chunk (entries)
+  size_t acc_queue_from = ACC_QUEUE_FROM;    // KZGMI_ACC_QUEUE_FROM: calls with fewer entries keep the static grid
   bool sort_split = false;     // KZGMI_SORT_SPLIT: split coarse-pass entries at every size (tests)
   int wbits_env = 0;           // KZGMI_WBITS: 13 or 16 forces the window width (tests, A/B)
   double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
@@ -284,7 +285,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   // another slot's still ends on every CU at about the same time.  The part arrays and k_fixup
   // are sized for the chunk count.
   size_t acc_threads = 0;
-  if (kAcc29<Cv> && c->acc_queue > 1 && cap && nchunks == cap && cap % 256 == 0) {
+  if (kAcc29<Cv> && c->acc_queue > 1 && cap && nchunks == cap && cap % 256 == 0 && emax >= c->acc_queue_from) {
     acc_threads = cap;
     nchunks = std::min(cap * (size_t)c->acc_queue, std::max(cap, emax / c->acc_queue_min));
     if (nchunks <= cap) acc_threads = 0;
@@ -779,6 +780,7 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
   if (const char* e = getenv("KZGMI_ACC_THREADS")) c->acc_threads_env = (size_t)strtoull(e, nullptr, 10);
   if (const char* e = getenv("KZGMI_ACC_QUEUE")) c->acc_queue = atoi(e);
   if (const char* e = getenv("KZGMI_ACC_QUEUE_MIN")) c->acc_queue_min = std::max<size_t>(4, strtoull(e, nullptr, 10));
+  if (const char* e = getenv("KZGMI_ACC_QUEUE_FROM")) c->acc_queue_from = strtoull(e, nullptr, 10);
   if (const char* e = getenv("KZGMI_SORT_SPLIT")) c->sort_split = atoi(e) != 0;
   if (const char* e = getenv("KZGMI_WBITS")) c->wbits_env = atoi(e);
   c->slots.resize(pipeline_slots);

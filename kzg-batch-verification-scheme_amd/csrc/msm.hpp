@@ -593,6 +593,15 @@ KZ_DEV Xyzz<Cv> load_xyzz(const Xyzz<Cv>* src) {
 #endif
 constexpr int ACC_QUEUE_FACTOR = KZ_ACC_QUEUE_FACTOR;
 constexpr size_t ACC_QUEUE_MIN_LEN = 64;
+// ... and only for calls of at least ACC_QUEUE_FROM entries (window terms).  Since the loop stopped
+// spilling (round 4) the static one-round grid is faster for 2^20-tuple batches (2^25 entries:
+// 184.3 vs 181.9 batch-verifies/s) and 2^20-point MSMs (2^24: 378.7 vs 375.7 M pts/s), while the
+// queue still pays for configs[3]'s 2^24-point MSMs (2^28 entries, two in flight: 42.6 vs 44.3
+// ms; profiles/r04/ab_acc_queue.txt).
+#ifndef KZ_ACC_QUEUE_FROM
+#define KZ_ACC_QUEUE_FROM (size_t(1) << 26)
+#endif
+constexpr size_t ACC_QUEUE_FROM = KZ_ACC_QUEUE_FROM;
 KZ_DEV uint32_t acc_chunk_len(uint32_t total, uint32_t nthreads) {
   const uint32_t per = ((total + nthreads - 1) / nthreads + 3) & ~3u;
   return per > 4u ? per : 4u;
