@@ -278,13 +278,14 @@ def test_split_sort_entries(curve, golden):
 @pytest.mark.parametrize("curve", CURVES)
 def test_accumulation_work_queue(curve, golden):
     """k_accumulate's work-queue form (calls whose grid reaches the cap): a context whose cap is
-    256 threads (KZGMI_ACC_THREADS) with 8 chunks per thread (KZGMI_ACC_QUEUE) makes every wave
-    take several 64-chunk groups from the counter.  Random and skewed MSMs (one bucket cut into
+    256 threads (KZGMI_ACC_THREADS) with 8 chunks per thread (KZGMI_ACC_QUEUE), and the queue
+    enabled at every size (KZGMI_ACC_QUEUE_FROM=0; by default only calls of >= 2^26 entries use it),
+    makes every wave take several 64-chunk groups from the counter.  Random and skewed MSMs (one bucket cut into
     many chunk pieces: the two-level join) against the oracle, and the largest golden batch
     (below the queue's 32-entry minimum chunk: the static grid) through the same context."""
     import kzgmi
-    saved = {k: os.environ.get(k) for k in ("KZGMI_ACC_THREADS", "KZGMI_ACC_QUEUE")}
-    os.environ.update(KZGMI_ACC_THREADS="256", KZGMI_ACC_QUEUE="8")
+    saved = {k: os.environ.get(k) for k in ("KZGMI_ACC_THREADS", "KZGMI_ACC_QUEUE", "KZGMI_ACC_QUEUE_FROM")}
+    os.environ.update(KZGMI_ACC_THREADS="256", KZGMI_ACC_QUEUE="8", KZGMI_ACC_QUEUE_FROM="0")
     try:
         c = kzgmi.Context(0, 1)
     finally:
