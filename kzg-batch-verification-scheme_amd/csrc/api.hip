@@ -12,6 +12,8 @@
 
 #include <sys/random.h>
 #include <cstdio>
+#define KZ_STR2(x) #x
+#define KZ_STR(x) KZ_STR2(x)
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -759,7 +761,7 @@ int h2d(Slot& s, hipStream_t cs, void* dst, const void* src, size_t bytes) {
 // ================================================================================ C ABI
 extern "C" {
 
-const char* kzgmi_version(void) { return "kzgmi 0.4 (abi 3, gfx950, HIP)"; }
+const char* kzgmi_version(void) { return "kzgmi 0.5 (abi " KZ_STR(KZGMI_ABI_VERSION) ", gfx950, HIP)"; }
 int kzgmi_abi_version(void) { return KZGMI_ABI_VERSION; }
 uint64_t kzgmi_alloc_count(void) { return g_allocs.load(std::memory_order_relaxed); }
 const char* kzgmi_last_error(void) { return g_err.c_str(); }
@@ -783,6 +785,18 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
   if (const char* e = getenv("KZGMI_ACC_QUEUE_FROM")) c->acc_queue_from = strtoull(e, nullptr, 10);
   if (const char* e = getenv("KZGMI_SORT_SPLIT")) c->sort_split = atoi(e) != 0;
   if (const char* e = getenv("KZGMI_WBITS")) c->wbits_env = atoi(e);
+  {
+    // HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 unless set before the runtime
+    // starts) and serialises the streams of one queue: slots + the copy stream need queues of
+    // their own (16 slots on 24 queues pipeline; 24 on 24 ran 3.6x slower)
+    const char* q = getenv("GPU_MAX_HW_QUEUES");
+    const int queues = q ? atoi(q) : 4;
+    static std::atomic<bool> warned{false};
+    if (pipeline_slots > 1 && pipeline_slots + 1 > queues && !getenv("KZGMI_QUIET") && !warned.exchange(true))
+      fprintf(stderr, "kzgmi: %d pipeline slots on %d hardware queues (GPU_MAX_HW_QUEUES): slots sharing a "
+                      "queue run one after another; set GPU_MAX_HW_QUEUES above the slot count before HIP starts\n",
+              pipeline_slots, queues);
+  }
   c->slots.resize(pipeline_slots);
   for (auto& s : c->slots) {
     if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
