@@ -25,6 +25,9 @@ def test_library_exports_every_header_symbol():
     for s in header_symbols():
         assert hasattr(lib, s), s
     assert b"gfx950" in lib.kzgmi_version()
+    # the version string reports the header's ABI revision (it is built from KZGMI_ABI_VERSION)
+    assert ("abi %d" % lib.kzgmi_abi_version()).encode() in lib.kzgmi_version()
+    assert lib.kzgmi_abi_version() == kzgmi.ABI_VERSION
 
 
 def test_library_contains_gfx950_code_object():
