@@ -355,7 +355,7 @@ def main():
     # runs use the eager ShardedPipeline schedule (combine chained on each partial's slot, no
     # extra lanes): at world 1 over RCCL, 2^17-tuple shards run 968/s on 16 slots vs 832/s on 8
     # and 851/s with round 3's deferred 8 slots + 2 lanes (profiles/r04/bench_s1_legs_serial_h2d.json)
-    slots = args.slots if args.slots else 16
+    slots = args.slots if args.slots else int(os.environ.get("KZGMI_BENCH_SLOTS", "16"))  # (A/B knob)
     lanes = 0  # the eager ShardedPipeline schedule chains each combine on its partial's slot
     ctx = kzgmi.Context(local, slots + lanes)  # + the combine lanes
     g2 = kzgmi.G2_GENERATOR[curve]
