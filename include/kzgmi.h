@@ -20,10 +20,14 @@
  *   - Return value 0 = OK, negative = error (see KZGMI_ERR_*).  Invalid input is an error,
  *     never "ok = 0".  kzgmi_last_error() gives a thread-local message.
  *   - Threading: one ctx per host thread; calls on one ctx are serialised by the caller.
- *   - Device-memory ordering: the library runs on its own non-blocking HIP streams (one per
- *     pipeline slot).  A caller that produced device inputs on another stream (e.g. a torch
- *     stream) must order the slot after it -- kzgmi_stream_wait(ctx, slot, stream) (no host
- *     sync), or synchronise that stream -- before the call that reads them.  Device outputs
+ *   - Device-memory ordering: the library runs on its own non-blocking HIP streams: three
+ *     shared "lanes" per context (front end / bucket accumulation / tail), which every slot's
+ *     jobs hop between in order, so the pipeline needs 3 hardware queues (+1 for host-buffer
+ *     copies) whatever the slot count -- HIP's default GPU_MAX_HW_QUEUES = 4 suffices
+ *     (KZGMI_LANES=0 in the environment selects rounds 1-4's stream per slot instead).  A caller
+ *     that produced device inputs on another stream (e.g. a torch stream) must order the slot's
+ *     next job after it -- kzgmi_stream_wait(ctx, slot, stream) (no host sync), or synchronise
+ *     that stream -- before the call that reads them.  Device outputs
  *     (partials, digests, generated points) are complete when the call, or the
  *     kzgmi_slot_wait / kzgmi_msm_wait that completes it, returns.  Device buffers passed to
  *     an async call must stay allocated until its wait returns.
@@ -52,9 +56,11 @@ typedef enum { KZGMI_BLS12_381 = 0, KZGMI_BN254 = 1 } kzgmi_curve;
  * SURVEY.md 8b device list (the single-device form is kzgmi_ctx_create_device; the ABI-3
  * kzgmi_ctx_create_multi is gone), and the pipelined host-buffer entry
  * kzgmi_batch_verify_ex_async, the pinned-host helpers kzgmi_host_* and kzgmi_slot_signal were
- * added.  A caller built against another revision must not bind the library: compare with
- * kzgmi_abi_version(). */
-#define KZGMI_ABI_VERSION 4
+ * added.  5: partial records carry their shard's error (KZGMI_ERR_SHARD; combines fail on a
+ * marked record), kzgmi_stream_wait orders the slot's NEXT job, multi-device contexts pipeline
+ * whole batches per device through the async entry points (kzgmi_slot_device).  A caller built
+ * against another revision must not bind the library: compare with kzgmi_abi_version(). */
+#define KZGMI_ABI_VERSION 5
 
 #define KZGMI_OK 0
 #define KZGMI_ERR_ARG (-1)
@@ -64,6 +70,7 @@ typedef enum { KZGMI_BLS12_381 = 0, KZGMI_BN254 = 1 } kzgmi_curve;
 #define KZGMI_ERR_DEVICE (-5)
 #define KZGMI_ERR_OOM (-6)
 #define KZGMI_ERR_NOT_IN_SUBGROUP (-7)
+#define KZGMI_ERR_SHARD (-8) /* a gathered partial record marks a shard that failed on its own device */
 
 /* flags of the *_ex entry points */
 #define KZGMI_FLAG_COMPRESSED 1u     /* commitments/proofs are compressed G1 encodings */
@@ -97,22 +104,31 @@ const char* kzgmi_last_error(void);
 /* SURVEY.md 8b kzgmi_ctx_create(out, device_ids, n_devices), plus the pipeline depth: one
  * context over a device list (one process driving several GPUs; a device id may repeat;
  * n_devices = 1 is the common single-GPU context).  device_ids[0] is the primary device: every
- * single-device entry point below runs there.  `pipeline_slots` >= 1 (at most 64) is the number
- * of independent workspaces/streams for the async entry points on the primary (1 is enough for
- * the synchronous calls); each holds ~1.3 GiB at n = 2^20.  With n_devices > 1 the host-buffer
+ * synchronous single-device entry point below runs there.  `pipeline_slots` >= 1 (at most 64) is
+ * the number of independent workspaces for the async entry points (1 is enough for the
+ * synchronous calls; over several devices see kzgmi_slot_device); each holds ~1.3 GiB at
+ * n = 2^20.  With n_devices > 1 the synchronous host-buffer
  * entry points kzgmi_batch_verify / kzgmi_batch_verify_ex / kzgmi_msm_g1 split their input by
  * point range over all devices (balanced, in units of 4096), run the shards concurrently and
  * combine the partial sums on the primary; kzgmi_batch_verify_multi_device /
  * kzgmi_msm_g1_multi_device take shards already resident on each device.  The exchange is 2
  * (batch) or 1 (MSM) partial records per device, copied to the primary with hipMemcpyPeerAsync
- * (xGMI) on the primary's slot-0 stream after every shard completed; processes that own one GPU
- * each instead all-gather kzgmi_batch_partial_device records over RCCL.  Peer
- * devices get one workspace each (their shard). */
+ * (xGMI) on the primary after every shard completed; processes that own one GPU each instead
+ * all-gather kzgmi_batch_partial_device records over RCCL.  Every device gets
+ * ceil(pipeline_slots / n_devices) workspaces, and the async entry points run whole batches per
+ * device (kzgmi_slot_device). */
 int kzgmi_ctx_create(kzgmi_ctx** out, const int* device_ids, int n_devices, int pipeline_slots);
 /* The n_devices = 1 case of kzgmi_ctx_create, by device id (>= 0). */
 int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots);
 void kzgmi_ctx_destroy(kzgmi_ctx* ctx);
 int kzgmi_ctx_num_devices(const kzgmi_ctx* ctx);
+/* Multi-device context: the async entry points (kzgmi_*_async, kzgmi_slot_wait, kzgmi_msm_wait,
+ * kzgmi_stream_wait, kzgmi_slot_signal) pipeline WHOLE batches per device -- caller slot `slot`
+ * (0 <= slot < pipeline_slots) runs on device device_ids[slot % n_devices], which this returns;
+ * device pointers passed to that slot must live there.  Each device holds
+ * ceil(pipeline_slots / n_devices) slots; caller slots 0 .. n_devices-1 are the devices' first
+ * slots, which the synchronous split calls use.  Single-device context: device_ids[0]. */
+int kzgmi_slot_device(const kzgmi_ctx* ctx, int slot);
 
 /* Size every pipeline slot's device workspace (and, on a multi-device context, each device's
  * shard workspace) for batches of up to n tuples of `curve` verified with `flags`
@@ -130,8 +146,9 @@ int kzgmi_ctx_reserve(kzgmi_ctx* ctx, kzgmi_curve curve, size_t n, uint32_t flag
  * region that leaves it unchanged allocated nothing). */
 uint64_t kzgmi_alloc_count(void);
 
-/* Order slot `slot`'s stream after all work enqueued so far on `hip_stream` (a hipStream_t of
- * the ctx's primary device, passed as void*; NULL = the null stream), without a host sync. */
+/* Order the next job issued on slot `slot` after all work enqueued so far on `hip_stream` (a
+ * hipStream_t of the ctx's primary device, passed as void*; NULL = the null stream), without a
+ * host sync.  Several calls before one job all apply. */
 int kzgmi_stream_wait(kzgmi_ctx* ctx, int slot, void* hip_stream);
 /* The other direction: order all work enqueued later on `hip_stream` (a hipStream_t of the
  * primary device; NULL = the null stream) after everything enqueued so far on slot `slot`,
@@ -196,8 +213,9 @@ int kzgmi_batch_verify_device_ex_async(kzgmi_ctx* ctx, const kzgmi_srs* srs, int
  * Arrays inside pinned memory (kzgmi_host_alloc / kzgmi_host_register) are DMA'd directly and
  * the call returns at once -- they must stay allocated and unmodified until the wait returns.
  * Pageable arrays are copied through the slot's pinned staging ring before the call returns
- * (they may be reused at once; the call then costs the host-side copy).  Single-device
- * contexts only (a multi-device context shards host buffers in kzgmi_batch_verify_ex).
+ * (they may be reused at once; the call then costs the host-side copy).  On a multi-device
+ * context the whole batch runs on the slot's device (kzgmi_slot_device); kzgmi_batch_verify_ex
+ * splits one batch over all devices instead.
  * kzgmi_batch_verify / kzgmi_batch_verify_ex are this on slot 0 followed by the wait. */
 int kzgmi_batch_verify_ex_async(kzgmi_ctx* ctx, const kzgmi_srs* srs, int slot,
                                 const uint8_t* commitments, const uint8_t* zs, const uint8_t* ys,
@@ -259,7 +277,13 @@ int kzgmi_msm_wait(kzgmi_ctx* ctx, int slot, uint8_t* out);
 /* ---- multi-GPU point-range sharding ----------------------------
  * A rank verifying tuples [index_offset, index_offset + n) of a global batch writes its
  * partial (A_k, B_k) as 2 opaque partial-point records (kzgmi_partial_bytes() each) to
- * device memory; the records are all-gathered over RCCL and any rank combines them. */
+ * device memory; the records are all-gathered over RCCL and any rank combines them.
+ * A shard that fails validation on its own device (an error reported by its wait) still writes
+ * its records, MARKED as failed; a shard rejected before anything ran (an error returned by the
+ * enqueue call) is marked by the caller filling its records with 0xFF bytes.  Every combine
+ * that reads a marked record fails -- with the shard's own error code, or KZGMI_ERR_SHARD -- so
+ * no rank can accept a batch one of whose shards was rejected, and every rank still takes part
+ * in the collective (kzgmi/distributed.py). */
 size_t kzgmi_partial_bytes(kzgmi_curve curve);
 /* Encode `count` device-resident partial records (e.g. a shard's A_k, B_k) as G1 encodings
  * (count x G1 bytes, host) -- for checking partials against a CPU reference. */

@@ -92,10 +92,28 @@ enum Phase { PH_CONVERT = 0, PH_SCALARS, PH_SORT, PH_ACCUM, PH_REDUCE, PH_COMBIN
 constexpr int EV_H2D0 = kNumBatchPhases + 1, EV_H2D1 = kNumBatchPhases + 2;  // Slot::ev indices
 constexpr size_t kRingBytes = size_t(16) << 20;  // pinned staging ring of pageable host inputs (x 2 per slot)
 
+// Lanes: the streams a job's phases are issued on.  In lane mode (the default) the context owns
+// ONE accumulation stream and NJ "job" streams; a job on slot s runs its front end (decode,
+// randomisers, sort) and its tail (reduce, window combination, pairing / partial out) on job
+// stream s % NJ and hops to the accumulation stream in between, ordered by events.  So the front
+// end of batch k+1 and the tails of earlier batches run beside the accumulation of batch k, and
+// the pipeline needs NJ + 1 hardware queues (+1 for host-buffer copies) whatever the slot count:
+// NJ = GPU_MAX_HW_QUEUES - 2 (at least 2, at most 8) reaches its rate at HIP's default of 4
+// queues.  KZGMI_LANES=<NJ> sets NJ; KZGMI_LANES=0 selects slot mode: each slot has a stream of
+// its own and a job stays on it (rounds 1-4; needs a hardware queue per slot in flight).
+enum Lane { LANE_FRONT = 0, LANE_ACC = 1, LANE_TAIL = 2, kNumLanes = 3 };
+
 struct Slot {
-  hipStream_t stream = nullptr;
+  int idx = 0;                   // index in the context's slots (lane mode: job stream idx % NJ)
+  hipStream_t own = nullptr;     // slot mode: this slot's stream
+  hipStream_t stream = nullptr;  // the stream the slot's current job issues on (begin_job / hop)
+  hipEvent_t hop_ev[kNumLanes] = {};  // a job's hand-over into lane l (recorded on the lane it leaves)
+  hipEvent_t done_ev = nullptr;       // the slot's last job issued so far has completed
+  bool done_rec = false;
+  std::vector<hipEvent_t> dep_pool;   // entry dependencies of the slot's next job (kzgmi_stream_wait, the
+  int ndep = 0;                        // H2D copy of host inputs): dep_pool[0, ndep)
   DevBuf pts, inf, scal_r, scal_s, scal_t, tpart, cnt, off, coarse, ent, total, sval, skey;
-  DevBuf buckets, pfirst, plast, R, U, scratch, winsum, res, flags, stage, outb;
+  DevBuf R, U, scratch, winsum, res, flags, stage, outb;
   DevBuf acc29;                                  // radix-29 bucket records (msm.hpp)
   DevBuf accq;                                   // k_accumulate's work-queue counter (large calls)
   DevBuf fs_leaves, fs_tmp, fs_top, pow, chal;  // Fiat-Shamir / powers-of-r randomisers
@@ -106,9 +124,7 @@ struct Slot {
   uint8_t* ring[2] = {};        // pinned staging of pageable host inputs (kRingBytes each, lazily)
   hipEvent_t ring_ev[2] = {};   // the DMA that last read ring[b]
   int ring_next = 0;
-  hipEvent_t h2d_ev = nullptr;  // this slot's inputs copied (on the context's H2D stream)
   hipEvent_t ev[kNumBatchPhases + 3] = {};  // phase marks 0..7, then the H2D pair
-  hipEvent_t order_ev = nullptr;   // kzgmi_stream_wait: the caller's stream -> this slot's stream
   hipEvent_t signal_ev = nullptr;  // kzgmi_slot_signal: this slot's stream -> the caller's stream
   bool ev_used[kNumBatchPhases + 3] = {};
   bool pending = false;
@@ -123,6 +139,10 @@ struct Slot {
 struct kzgmi_ctx {
   int device = 0;
   std::vector<Slot> slots;
+  int user_slots = 0;                   // slots in the caller's numbering (multi-device: over all devices)
+  bool lanes = true;                    // lane mode (KZGMI_LANES; see Lane)
+  std::vector<hipStream_t> acc_lanes;   // lane mode: the NA accumulation streams
+  std::vector<hipStream_t> job_lanes;   // lane mode: the NJ front-end + tail streams
   bool profiling = false;
   // GLV split of full Fr scalars.  phi(P) = [lambda] P holds only on
   // G1, so BLS12-381 (cofactor > 1) uses it only for points known to be in G1: batch calls
@@ -145,7 +165,7 @@ struct kzgmi_ctx {
   // host-buffer inputs of every slot are copied on ONE stream, in submission order: each
   // batch's copy then gets the whole link and completes first-in first-out (16 concurrent
   // 256-MiB copies on the slots' own streams shared the link and all finished late)
-  hipStream_t h2d_stream = nullptr;
+  hipStream_t h2d_stream = nullptr;  // created with the context
   int phase_calls = 0;
   DevBuf table[2], table_base[2];
   bool table_ready[2] = {false, false};
@@ -184,6 +204,66 @@ int set_dev(kzgmi_ctx* c) {
 }
 
 inline unsigned grid(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+hipStream_t lane_stream(const kzgmi_ctx* c, const Slot& s, int l) {
+  if (!c->lanes) return s.own;
+  return l == LANE_ACC ? c->acc_lanes[(size_t)s.idx % c->acc_lanes.size()]
+                       : c->job_lanes[(size_t)s.idx % c->job_lanes.size()];
+}
+
+// Start a job on slot s in lane l: after the slot's previous job (its workspace is reused) and
+// the entry dependencies recorded since (kzgmi_stream_wait, the H2D copy of host inputs).  Every
+// entry point that issues work on a slot calls this first; the work then goes on s.stream.
+int begin_job(kzgmi_ctx* c, Slot& s, int l) {
+  hipStream_t st = lane_stream(c, s, l);
+  if (s.done_rec && st != s.stream) HIPCHK(hipStreamWaitEvent(st, s.done_ev, 0));
+  for (int k = 0; k < s.ndep; ++k) HIPCHK(hipStreamWaitEvent(st, s.dep_pool[k], 0));
+  s.ndep = 0;
+  s.stream = st;
+  return 0;
+}
+
+// Move the slot's current job to lane l (no-op in slot mode): l's later work waits for
+// everything the job issued so far
+int hop(kzgmi_ctx* c, Slot& s, int l) {
+  hipStream_t st = lane_stream(c, s, l);
+  if (st == s.stream) return 0;
+  HIPCHK(hipEventRecord(s.hop_ev[l], s.stream));
+  HIPCHK(hipStreamWaitEvent(st, s.hop_ev[l], 0));
+  s.stream = st;
+  return 0;
+}
+
+// The job's last operation is issued: done_ev marks its completion (kzgmi_slot_wait, the next
+// job's begin_job, kzgmi_slot_signal)
+int end_job(Slot& s) {
+  HIPCHK(hipEventRecord(s.done_ev, s.stream));
+  s.done_rec = true;
+  return 0;
+}
+
+// Host wait for the slot's last job (an event: the lanes are shared, so a stream sync would
+// also wait for other slots' later work)
+int sync_slot(Slot& s) {
+  if (s.done_rec) HIPCHK(hipEventSynchronize(s.done_ev));
+  return 0;
+}
+int sync_job(Slot& s) {
+  CHK(end_job(s));
+  return sync_slot(s);
+}
+
+// A new entry dependency of the slot's next job: work enqueued so far on `stream`
+int add_dep(Slot& s, hipStream_t stream) {
+  if (s.ndep == (int)s.dep_pool.size()) {
+    hipEvent_t e = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    s.dep_pool.push_back(e);
+  }
+  HIPCHK(hipEventRecord(s.dep_pool[s.ndep], stream));
+  s.ndep += 1;
+  return 0;
+}
 
 void mark(kzgmi_ctx* c, Slot& s, int idx) {
   if (!c->profiling) return;
@@ -234,6 +314,7 @@ int map_device_err(uint32_t e) {
     case DERR_NOT_ON_CURVE: return fail(KZGMI_ERR_NOT_ON_CURVE, "point not on curve");
     case DERR_SCALAR: return fail(KZGMI_ERR_SCALAR, "non-canonical scalar (>= r)");
     case DERR_NOT_IN_SUBGROUP: return fail(KZGMI_ERR_NOT_IN_SUBGROUP, "point not in the order-r subgroup");
+    case DERR_SHARD: return fail(KZGMI_ERR_SHARD, "a gathered partial record is marked failed (its shard was rejected)");
     default: return fail(KZGMI_ERR_DEVICE, "unknown device error");
   }
 }
@@ -268,7 +349,6 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   size_t nchunks = (emax + chunk - 1) / chunk + 1;
   const size_t cap = c->acc_threads_env ? c->acc_threads_env : (size_t)c->ncu * 4 * kAccWaves<Cv> * 64;
   if (cap && nchunks > cap) nchunks = cap;
-#if !defined(KZ_NO_ACC_BALANCE)
   // A call with no other slot of the context in flight is latency-bound: below the cap, give
   // every SIMD the same whole number of waves (shorter equal chunks).  A 2^17 batch at 13 bits
   // is 1.25 waves per SIMD, and its SIMDs with two waves ran 1.5x longer than those with one:
@@ -281,13 +361,12 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   const size_t simd_lanes = (size_t)c->ncu * 4 * 64;
   if (alone && !c->acc_threads_env && emax > ACC_SMALL_ENTRIES && simd_lanes && nchunks < cap)
     nchunks = std::min(cap, (nchunks + simd_lanes - 1) / simd_lanes * simd_lanes);
-#endif
   // Large radix-29 calls (the grid at its cap): c->acc_queue x cap shorter chunks taken from a
   // work queue by the cap's threads (msm.hpp k_accumulate), so an accumulation that starts behind
   // another slot's still ends on every CU at about the same time.  The part arrays and k_fixup
   // are sized for the chunk count.
   size_t acc_threads = 0;
-  if (kAcc29<Cv> && c->acc_queue > 1 && cap && nchunks == cap && cap % 256 == 0 && emax >= c->acc_queue_from) {
+  if (c->acc_queue > 1 && cap && nchunks == cap && cap % 256 == 0 && emax >= c->acc_queue_from) {
     acc_threads = cap;
     nchunks = std::min(cap * (size_t)c->acc_queue, std::max(cap, emax / c->acc_queue_min));
     if (nchunks <= cap) acc_threads = 0;
@@ -302,15 +381,11 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   CHK(s.sval.ensure(emax * 4 + 16));  // + 16: k_accumulate reads values 4 at a time, up to 3 past the end
   CHK(s.skey.ensure(emax * 4));
   constexpr int W29 = kW29<Fp29Of<Cv>>;
-  if (!kAcc29<Cv>) {  // the radix-29 accumulation keeps buckets and pieces as records in acc29
-    CHK(s.buckets.ensure((size_t)NB * sizeof(XY)));
-    CHK(s.pfirst.ensure(nchunks * sizeof(XY)));
-    CHK(s.plast.ensure(nchunks * sizeof(XY)));
-  }
-  if constexpr (kAcc29<Cv>) CHK(s.acc29.ensure(((size_t)NB + 2 * nchunks) * W29 * 4));
-  const size_t seg_rec = std::max(sizeof(XY), (size_t)W29 * 4);  // 32-bit XYZZ or a radix-29 record
+  // buckets and bucket pieces are radix-29 records in acc29 (msm.hpp)
+  CHK(s.acc29.ensure(((size_t)NB + 2 * nchunks) * W29 * 4));
+  const size_t seg_rec = (size_t)W29 * 4;  // a radix-29 record
   CHK(s.R.ensure((size_t)NB / SEG * seg_rec));
-  CHK(s.U.ensure((size_t)NB / SEG * seg_rec * (kSegV ? 2 : 1)));  // U records, then the V records
+  CHK(s.U.ensure((size_t)NB / SEG * seg_rec * 2));  // U records, then the V records
   CHK(s.scratch.ensure((size_t)nsets * rb_parts * sizeof(XY)));  // k_reduce_bits partial sums
   CHK(s.winsum.ensure((size_t)nsets * sizeof(XY)));
   CHK(s.res.ensure(2 * sizeof(XY)));
@@ -328,13 +403,15 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
           s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.total.template as<uint32_t>(),
           s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(), wbits);
   mark(c, s, PH_SORT + 1);
+  CHK(hop(c, s, LANE_ACC));
+  st = s.stream;
   L::accumulate(st, nchunks, s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
-                s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts,
-                s.buckets.template as<XY>(), s.pfirst.template as<XY>(), s.plast.template as<XY>(),
-                s.acc29.template as<uint32_t>(), NB, acc_threads, acc_threads ? s.accq.template as<uint32_t>() : nullptr);
+                s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts, s.acc29.template as<uint32_t>(), NB,
+                acc_threads, acc_threads ? s.accq.template as<uint32_t>() : nullptr);
   mark(c, s, PH_ACCUM + 1);
-  L::reduce(st, nsets, s.cnt.template as<uint32_t>(), s.buckets.template as<XY>(), s.acc29.template as<uint32_t>(),
-            s.R.template as<XY>(),
+  CHK(hop(c, s, LANE_TAIL));
+  st = s.stream;
+  L::reduce(st, nsets, s.cnt.template as<uint32_t>(), s.acc29.template as<uint32_t>(), s.R.template as<XY>(),
             s.U.template as<XY>(), s.scratch.template as<XY>(), s.winsum.template as<XY>(), wbits);
   mark(c, s, PH_REDUCE + 1);
   L::window_combine(st, mw, s.winsum.template as<XY>(), s.res.template as<XY>(), wbits);
@@ -448,14 +525,14 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
     if (flags & KZGMI_FLAG_FIAT_SHAMIR) CHK(reserve_fs<Cv>(s, n));
     else if (flags & KZGMI_FLAG_POWERS) CHK(s.pow.ensure(FS_POW_BITS * sizeof(FrF)));
   }
-  hipStream_t st = s.stream;
+  hipStream_t st = nullptr;  // set by begin_job in front()
   uint32_t* err = s.flags.template as<uint32_t>() + 1;
   Affine<Cv>* pts = s.pts.template as<Affine<Cv>>();
   uint8_t* inf = s.inf.template as<uint8_t>();
   // points that only feed the radix-29 accumulation are converted straight into its format
   // (with GLV their images too: k_endo_points29); decompression and the subgroup check work in
   // the 32-bit form, converted afterwards by run_msm_core's k_pts_to29
-  const bool pts29 = kAcc29<Cv> && !(flags & (KZGMI_FLAG_COMPRESSED | KZGMI_FLAG_SUBGROUP_CHECK));
+  const bool pts29 = !(flags & (KZGMI_FLAG_COMPRESSED | KZGMI_FLAG_SUBGROUP_CHECK));
   const uint32_t nn = (uint32_t)n;
   uint32_t* gs = s.glv_s.template as<uint32_t>();
   uint32_t* gt = s.glv_t.template as<uint32_t>();
@@ -463,6 +540,8 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   // decode + validate the points, derive the randomisers and the MSM scalars
   auto front = [&]() -> int {
     Roctx rx("kzgmi.batch.convert+scalars");
+    CHK(begin_job(c, s, LANE_FRONT));
+    st = s.stream;
     mark(c, s, 0);
     HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
     if (flags & KZGMI_FLAG_COMPRESSED) {
@@ -557,8 +636,9 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   }
   if (dry) return 0;
   Roctx rx("kzgmi.batch.pairing");
+  st = s.stream;  // the tail lane (run_msm_core hopped there)
   if (d_partial_out) {
-    HIPCHK(hipMemcpyAsync(d_partial_out, s.res.p, 2 * sizeof(XY), hipMemcpyDeviceToDevice, st));
+    L::partial_out(st, s.res.template as<XY>(), 2, err, (XY*)d_partial_out);  // marked if this shard failed
   } else {
     L::pairing_check(st, s.res.template as<XY>(), srs->lines.template as<Line<Cv>>(), srs->q_inf.template as<uint8_t>(),
                      s.flags.template as<int>());
@@ -566,6 +646,7 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
+  CHK(end_job(s));
   s.pending = true;
   s.partial_job = d_partial_out != nullptr;
   s.partial_of = s.partial_job ? 1 : 0;
@@ -577,7 +658,7 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
 int finish_slot(kzgmi_ctx* c, Slot& s, int* ok_out) {
   {
     Roctx rx("kzgmi.slot_wait");
-    HIPCHK(hipStreamSynchronize(s.stream));
+    CHK(sync_slot(s));
   }
   s.pending = false;
   collect_phases(c, s);
@@ -603,6 +684,38 @@ int check_ctx(kzgmi_ctx* c, int slot = 0) {
   return set_dev(c);
 }
 
+kzgmi_ctx* dev_ctx(kzgmi_ctx* c, int d) { return d == 0 ? c : c->peers[d - 1]; }
+
+// Multi-device context (kzgmi_ctx_create with D > 1 devices): the caller's slot s runs on device
+// s % D as that device's local slot s / D -- whole batches / MSMs per device, each device with
+// its own lane pipeline; caller slot d < D is device d's local slot 0, which is also the
+// device's shard slot of the synchronous strong split.  Only the outermost C-ABI call of a
+// host thread translates (entry points calling each other pass local slots): t_route_depth.
+thread_local int t_route_depth = 0;
+struct RouteGuard {
+  RouteGuard() { ++t_route_depth; }
+  ~RouteGuard() { --t_route_depth; }
+  RouteGuard(const RouteGuard&) = delete;
+  RouteGuard& operator=(const RouteGuard&) = delete;
+};
+int route_slot(kzgmi_ctx*& c, const kzgmi_srs** srs, int& slot) {
+  if (t_route_depth != 1 || !c || c->peers.empty()) return 0;
+  const int D = 1 + (int)c->peers.size();
+  if (slot < 0 || slot >= c->user_slots) return fail(KZGMI_ERR_ARG, "bad slot");
+  const int d = slot % D;
+  if (srs && *srs) {
+    if ((*srs)->ctx != c || (*srs)->peers.size() != c->peers.size())
+      return fail(KZGMI_ERR_ARG, "srs does not belong to this context");
+    if (d > 0) *srs = (*srs)->peers[d - 1];
+  }
+  c = dev_ctx(c, d);
+  slot /= D;
+  return 0;
+}
+#define KZ_ROUTE(c, srsp, slot) \
+  RouteGuard route_guard_;       \
+  CHK(route_slot(c, srsp, slot))
+
 int batch_multi_host(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commitments, const uint8_t* zs,
                      const uint8_t* ys, const uint8_t* proofs, size_t n, const uint8_t* seed32, uint32_t flags,
                      int* ok_out);
@@ -612,7 +725,13 @@ int msm_multi_host(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* points, const
 // synchronous entry points that run on slot 0 must not overwrite a pending async job's
 // flags / result buffers (its later kzgmi_slot_wait would report theirs)
 int slot0_idle(kzgmi_ctx* c) {
-  return c->slots[0].pending ? fail(KZGMI_ERR_ARG, "slot 0 busy: complete its pending job (kzgmi_slot_wait / kzgmi_msm_wait) first") : 0;
+  if (c->slots[0].pending)
+    return fail(KZGMI_ERR_ARG, "slot 0 busy: complete its pending job (kzgmi_slot_wait / kzgmi_msm_wait) first");
+  for (size_t d = 0; d < c->peers.size(); ++d)  // multi-device: the shard slots (caller slots 1..D-1)
+    if (c->peers[d]->slots[0].pending)
+      return fail(KZGMI_ERR_ARG, "slot " + std::to_string(d + 1) + " busy: a synchronous multi-device call uses "
+                                 "every device's first slot");
+  return 0;
 }
 
 template <class Cv>
@@ -651,8 +770,12 @@ bool host_pinned(const void* p, size_t bytes) {
 // the caller.  One job at a time (contexts on several host threads take turns).
 class CopyPool {
  public:
+  CopyPool() {
+    const char* e = getenv("KZGMI_COPY_THREADS");
+    nthreads_ = e ? std::max(1, atoi(e)) : 8;
+  }
   void copy(void* dst, const void* src, size_t len) {
-    if (len < (size_t(2) << 20) || threads() <= 1) {
+    if (len < (size_t(2) << 20) || nthreads_ <= 1) {
       memcpy(dst, src, len);
       return;
     }
@@ -675,13 +798,6 @@ class CopyPool {
   }
 
  private:
-  int threads() {
-    if (nthreads_ < 0) {
-      const char* e = getenv("KZGMI_COPY_THREADS");
-      nthreads_ = e ? std::max(1, atoi(e)) : 8;
-    }
-    return nthreads_;
-  }
   void start() {
     if (!workers_.empty()) return;
     for (int i = 1; i < nthreads_; ++i) {
@@ -707,7 +823,7 @@ class CopyPool {
       if (--left_ == 0) done_.notify_one();
     }
   }
-  int nthreads_ = -1;
+  int nthreads_ = 8;  // fixed by the constructor (the pool is a function-local static: thread-safe)
   std::mutex job_mu_, mu_;
   std::condition_variable cv_, done_;
   std::vector<std::thread> workers_;
@@ -785,26 +901,58 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
   if (const char* e = getenv("KZGMI_ACC_QUEUE_FROM")) c->acc_queue_from = strtoull(e, nullptr, 10);
   if (const char* e = getenv("KZGMI_SORT_SPLIT")) c->sort_split = atoi(e) != 0;
   if (const char* e = getenv("KZGMI_WBITS")) c->wbits_env = atoi(e);
-  {
-    // HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 unless set before the runtime
-    // starts) and serialises the streams of one queue: slots + the copy stream need queues of
-    // their own (16 slots on 24 queues pipeline; 24 on 24 ran 3.6x slower)
-    const char* q = getenv("GPU_MAX_HW_QUEUES");
-    const int queues = q ? atoi(q) : 4;
+  const char* qenv = getenv("GPU_MAX_HW_QUEUES");
+  const int queues = qenv ? atoi(qenv) : 4;
+  int nj = 0;  // (A/B) slot mode unless KZGMI_LANES sets the job-lane count
+  if (const char* e = getenv("KZGMI_LANES")) nj = std::min(64, atoi(e));
+  c->lanes = nj > 0;
+  if (!c->lanes) {
+    // slot mode: HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 unless set before the
+    // runtime starts) and serialises the streams of one queue, so slots + the copy stream need
+    // queues of their own (16 slots on 24 queues pipeline; 24 on 24 ran 3.6x slower)
     static std::atomic<bool> warned{false};
     if (pipeline_slots > 1 && pipeline_slots + 1 > queues && !getenv("KZGMI_QUIET") && !warned.exchange(true))
-      fprintf(stderr, "kzgmi: %d pipeline slots on %d hardware queues (GPU_MAX_HW_QUEUES): slots sharing a "
-                      "queue run one after another; set GPU_MAX_HW_QUEUES above the slot count before HIP starts\n",
+      fprintf(stderr, "kzgmi: %d pipeline slots on %d hardware queues (GPU_MAX_HW_QUEUES) in slot mode "
+                      "(KZGMI_LANES=0): slots sharing a queue run one after another\n",
               pipeline_slots, queues);
   }
+  bool okc = true;
+  // lane streams first (the runtime hands hardware queues to streams in creation order), then the
+  // copy stream of host-buffer inputs
+  if (c->lanes) {
+    int na = 1;
+    if (const char* e = getenv("KZGMI_ACC_LANES")) na = std::max(1, std::min(64, atoi(e)));
+    c->acc_lanes.assign(na, nullptr);
+    c->job_lanes.assign(nj, nullptr);
+    for (auto& st : c->acc_lanes) okc = okc && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+    for (auto& st : c->job_lanes) okc = okc && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+  }
+  // KZGMI_STREAM_PRIO=1 (A/B): the slot streams cycle through the device's stream priorities
+  int prio_lo = 0, prio_hi = 0;
+  const bool spread = getenv("KZGMI_STREAM_PRIO") && atoi(getenv("KZGMI_STREAM_PRIO")) != 0 &&
+                      hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) == hipSuccess;
+  okc = okc && hipStreamCreateWithFlags(&c->h2d_stream, hipStreamNonBlocking) == hipSuccess;
   c->slots.resize(pipeline_slots);
+  c->user_slots = pipeline_slots;
+  for (size_t k = 0; k < c->slots.size(); ++k) c->slots[k].idx = (int)k;
   for (auto& s : c->slots) {
-    if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&s.host_flags, 16, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&s.host_out, 128, hipHostMallocDefault) != hipSuccess) {
-      kzgmi_ctx_destroy(c);
-      return fail(KZGMI_ERR_DEVICE, "stream/pinned allocation failed");
+    if (!c->lanes) {
+      const int nlev = std::abs(prio_lo - prio_hi) + 1;
+      const int pr = prio_hi < prio_lo ? prio_hi + s.idx % nlev : prio_hi - s.idx % nlev;
+      okc = okc && (spread ? hipStreamCreateWithPriority(&s.own, hipStreamNonBlocking, pr)
+                           : hipStreamCreateWithFlags(&s.own, hipStreamNonBlocking)) == hipSuccess;
     }
+    for (auto& e : s.hop_ev) okc = okc && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    okc = okc && hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming) == hipSuccess &&
+          hipEventCreateWithFlags(&s.signal_ev, hipEventDisableTiming) == hipSuccess &&
+          hipHostMalloc((void**)&s.host_flags, 16, hipHostMallocDefault) == hipSuccess &&
+          hipHostMalloc((void**)&s.host_out, 128, hipHostMallocDefault) == hipSuccess;
+    s.stream = lane_stream(c, s, LANE_FRONT);
+    if (!okc) break;
+  }
+  if (!okc) {
+    kzgmi_ctx_destroy(c);
+    return fail(KZGMI_ERR_DEVICE, "stream/event/pinned allocation failed");
   }
   *out = c;
   return 0;
@@ -813,26 +961,37 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
 void kzgmi_ctx_destroy(kzgmi_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  for (auto& s : c->slots) (void)sync_slot(s);
+  for (auto& st : c->acc_lanes)
+    if (st) (void)hipStreamSynchronize(st);
+  for (auto& st : c->job_lanes)
+    if (st) (void)hipStreamSynchronize(st);
   for (auto& s : c->slots) {
-    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.own) (void)hipStreamSynchronize(s.own);
     DevBuf* bufs[] = {&s.pts, &s.inf, &s.scal_r, &s.scal_s, &s.scal_t, &s.tpart, &s.cnt, &s.off, &s.coarse, &s.ent,
-                      &s.total, &s.sval, &s.skey, &s.buckets, &s.pfirst, &s.plast, &s.acc29, &s.accq, &s.R, &s.U, &s.scratch,
+                      &s.total, &s.sval, &s.skey, &s.acc29, &s.accq, &s.R, &s.U, &s.scratch,
                       &s.winsum, &s.res, &s.flags, &s.stage, &s.outb, &s.fs_leaves, &s.fs_tmp,
                       &s.fs_top, &s.pow, &s.chal, &s.glv_r, &s.glv_s, &s.glv_t, &s.digits};
     for (DevBuf* b : bufs) b->release();
     for (auto& e : s.ev)
       if (e) (void)hipEventDestroy(e);
-    if (s.order_ev) (void)hipEventDestroy(s.order_ev);
     if (s.signal_ev) (void)hipEventDestroy(s.signal_ev);
-    if (s.h2d_ev) (void)hipEventDestroy(s.h2d_ev);
+    if (s.done_ev) (void)hipEventDestroy(s.done_ev);
+    for (auto& e : s.dep_pool) (void)hipEventDestroy(e);
+    for (auto& e : s.hop_ev)
+      if (e) (void)hipEventDestroy(e);
     for (int b = 0; b < 2; ++b) {
       if (s.ring_ev[b]) (void)hipEventDestroy(s.ring_ev[b]);
       if (s.ring[b]) (void)hipHostFree(s.ring[b]);
     }
     if (s.host_flags) (void)hipHostFree(s.host_flags);
     if (s.host_out) (void)hipHostFree(s.host_out);
-    if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.own) (void)hipStreamDestroy(s.own);
   }
+  for (auto& st : c->acc_lanes)
+    if (st) (void)hipStreamDestroy(st);
+  for (auto& st : c->job_lanes)
+    if (st) (void)hipStreamDestroy(st);
   for (int k = 0; k < 2; ++k) { c->table[k].release(); c->table_base[k].release(); }
   if (c->h2d_stream) {
     (void)hipStreamSynchronize(c->h2d_stream);
@@ -877,10 +1036,9 @@ int kzgmi_ctx_reserve(kzgmi_ctx* c, kzgmi_curve curve, size_t n, uint32_t flags)
     for (auto& e : s.ev)  // the phase events kzgmi_set_profiling records
       if (!e) HIPCHK(hipEventCreate(&e));
   }
-  // multi-device context: each peer runs one shard of at most ceil(n / devices) (4096-aligned)
-  const size_t D = 1 + c->peers.size();
-  const size_t per = ((n + D - 1) / D + FS_CHUNK - 1) / FS_CHUNK * FS_CHUNK;
-  for (kzgmi_ctx* p : c->peers) CHK(kzgmi_ctx_reserve(p, curve, std::min(n, per), flags));
+  // multi-device context: every device's slots take whole batches of up to n (the async entry
+  // points pipeline them per device; the synchronous split runs smaller shards on the same slots)
+  for (kzgmi_ctx* p : c->peers) CHK(kzgmi_ctx_reserve(p, curve, n, flags));
   return set_dev(c);
 }
 
@@ -909,6 +1067,10 @@ int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uin
     memcpy(h.data(), tau_g2, gb);
     memcpy(h.data() + gb, g2, gb);
     if (g1) memcpy(h.data() + 2 * gb, g1, g1b);
+    if (int rb = begin_job(c, s, LANE_FRONT)) {
+      kzgmi_srs_free(srs);
+      return rb;
+    }
     hipStream_t st = s.stream;
     Affine<Cv>* g1p = srs->g1.template as<Affine<Cv>>();
     uint8_t* g1inf = srs->g1.template as<uint8_t>() + sizeof(Affine<Cv>);
@@ -932,8 +1094,7 @@ int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uin
       Launch<Cv>::pts_to29(st, g1p29, 1);
       okk = okk && hipGetLastError() == hipSuccess &&
             hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
-            hipMemcpyAsync(&g1inf_h, g1inf, 1, hipMemcpyDeviceToHost, st) == hipSuccess &&
-            hipStreamSynchronize(st) == hipSuccess;
+            hipMemcpyAsync(&g1inf_h, g1inf, 1, hipMemcpyDeviceToHost, st) == hipSuccess && sync_job(s) == 0;
     }
     if (!okk) {
       kzgmi_srs_free(srs);
@@ -986,6 +1147,7 @@ int kzgmi_batch_verify_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot
 int kzgmi_batch_verify_device_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const void* dC, const void* dz,
                                        const void* dy, const void* dpi, size_t n, const uint8_t* seed32,
                                        uint32_t flags) {
+  KZ_ROUTE(c, &srs, slot);
   if (flags & ~kAllFlags) return fail(KZGMI_ERR_ARG, "unknown flags");
   if ((flags & KZGMI_FLAG_POWERS) && (flags & KZGMI_FLAG_FIAT_SHAMIR))
     return fail(KZGMI_ERR_ARG, "KZGMI_FLAG_POWERS and KZGMI_FLAG_FIAT_SHAMIR are exclusive");
@@ -1000,7 +1162,7 @@ int kzgmi_batch_verify_device_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int s
   Seed seed = make_seed(seed32, sb);
   if (n == 0) {
     CHK(set_dev(c));
-    HIPCHK(hipStreamSynchronize(s.stream));  // host_flags may still be the target of a copy
+    CHK(sync_slot(s));  // host_flags may still be the target of a copy
     s.host_flags[0] = 1;
     s.host_flags[1] = 0;
     s.pending = true;
@@ -1016,6 +1178,7 @@ int kzgmi_batch_verify_device_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int s
 }
 
 int kzgmi_slot_wait(kzgmi_ctx* c, int slot, int* ok_out) {
+  KZ_ROUTE(c, nullptr, slot);
   CHK(check_ctx(c, slot));
   Slot& s = c->slots[slot];
   if (!s.pending) return fail(KZGMI_ERR_ARG, "slot has no pending batch");
@@ -1050,11 +1213,10 @@ int kzgmi_batch_verify_ex(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* com
 int kzgmi_batch_verify_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const uint8_t* commitments,
                                 const uint8_t* zs, const uint8_t* ys, const uint8_t* proofs, size_t n,
                                 const uint8_t* seed32, uint32_t flags) {
-  CHK(check_ctx(c, slot));
   if (!srs) return fail(KZGMI_ERR_ARG, "null argument");
+  KZ_ROUTE(c, &srs, slot);
+  CHK(check_ctx(c, slot));
   if (srs->ctx != c) return fail(KZGMI_ERR_ARG, "srs does not belong to this context");
-  if (!c->peers.empty())
-    return fail(KZGMI_ERR_ARG, "kzgmi_batch_verify_ex_async: single-device contexts only (use kzgmi_batch_verify_ex)");
   if (n && (!commitments || !zs || !ys || !proofs)) return fail(KZGMI_ERR_ARG, "null input");
   if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "batch too large (max 2^26 tuples per call)");
   if (flags & ~kAllFlags) return fail(KZGMI_ERR_ARG, "unknown flags");
@@ -1068,12 +1230,9 @@ int kzgmi_batch_verify_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, co
   uint8_t* dpi = dC + n * gb;
   uint8_t* dz = dC + 2 * n * gb;
   uint8_t* dy = dz + 32 * n;
-  if (!c->h2d_stream) HIPCHK(hipStreamCreateWithFlags(&c->h2d_stream, hipStreamNonBlocking));
   hipStream_t cs = c->h2d_stream;
-  if (!s.h2d_ev) HIPCHK(hipEventCreateWithFlags(&s.h2d_ev, hipEventDisableTiming));
-  // the copy overwrites s.stage: after everything already on the slot's stream
-  HIPCHK(hipEventRecord(s.h2d_ev, s.stream));
-  HIPCHK(hipStreamWaitEvent(cs, s.h2d_ev, 0));
+  // the copy overwrites s.stage: after the slot's previous job
+  if (s.done_rec) HIPCHK(hipStreamWaitEvent(cs, s.done_ev, 0));
   if (c->profiling) {
     if (!s.ev[EV_H2D0]) HIPCHK(hipEventCreate(&s.ev[EV_H2D0]));
     if (!s.ev[EV_H2D1]) HIPCHK(hipEventCreate(&s.ev[EV_H2D1]));
@@ -1084,8 +1243,7 @@ int kzgmi_batch_verify_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, co
   CHK(h2d(s, cs, dz, zs, n * 32));
   CHK(h2d(s, cs, dy, ys, n * 32));
   if (c->profiling) HIPCHK(hipEventRecord(s.ev[EV_H2D1], cs));
-  HIPCHK(hipEventRecord(s.h2d_ev, cs));  // the batch's kernels wait for its copy only
-  HIPCHK(hipStreamWaitEvent(s.stream, s.h2d_ev, 0));
+  CHK(add_dep(s, cs));  // the batch's kernels wait for its copy only
   const int r = kzgmi_batch_verify_device_ex_async(c, srs, slot, dC, dz, dy, dpi, n, seed32, flags);
   if (c->profiling) s.ev_used[EV_H2D0] = s.ev_used[EV_H2D1] = (r == 0);
   return r;
@@ -1147,11 +1305,12 @@ int kzgmi_last_combination(kzgmi_ctx* c, uint8_t* a_out, uint8_t* b_out) {
     using Cv = decltype(cv);
     const size_t gb = g1_bytes(Cv::ID);
     CHK(s.outb.ensure(2 * gb));
+    CHK(begin_job(c, s, LANE_TAIL));
     Launch<Cv>::encode_points(s.stream, s.res.template as<Xyzz<Cv>>(), 2, s.outb.template as<uint8_t>());
     HIPCHK(hipGetLastError());
     std::vector<uint8_t> h(2 * gb);
     HIPCHK(hipMemcpyAsync(h.data(), s.outb.p, 2 * gb, hipMemcpyDeviceToHost, s.stream));
-    HIPCHK(hipStreamSynchronize(s.stream));
+    CHK(sync_job(s));
     memcpy(a_out, h.data(), gb);
     memcpy(b_out, h.data() + gb, gb);
     return 0;
@@ -1169,13 +1328,14 @@ int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t
   CHK(s.scal_s.ensure(n * 32));
   if (glv) CHK(s.glv_s.ensure(n * 32));
   CHK(s.flags.ensure(16));
+  CHK(begin_job(c, s, LANE_FRONT));
   hipStream_t st = s.stream;
   mark(c, s, 0);
   HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
   uint32_t* err = s.flags.template as<uint32_t>() + 1;
   Affine<Cv>* pts = s.pts.template as<Affine<Cv>>();
   uint8_t* inf = s.inf.template as<uint8_t>();
-  const bool pts29 = kAcc29<Cv>;
+  const bool pts29 = true;
   if (glv && pts29)  // phi(P) stored by the converting pass
     Launch<Cv>::convert_points(st, (const uint8_t*)dpts, (uint32_t)n, pts, inf, err, true, pts + n, inf + n);
   else
@@ -1211,7 +1371,7 @@ int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t
 
 int read_flags_sync(kzgmi_ctx* c, Slot& s) {
   HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, s.stream));
-  HIPCHK(hipStreamSynchronize(s.stream));
+  CHK(sync_job(s));
   collect_phases(c, s);
   return map_device_err((uint32_t)s.host_flags[1]);
 }
@@ -1239,6 +1399,10 @@ int kzgmi_ck_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1_powers, siz
       delete ck;
       return r;
     }
+    if (int rb = begin_job(c, s, LANE_FRONT)) {
+      delete ck;
+      return rb;
+    }
     hipStream_t st = s.stream;
     Affine<Cv>* pts = ck->pts.template as<Affine<Cv>>();
     uint8_t* inf = ck->inf.template as<uint8_t>();
@@ -1251,8 +1415,7 @@ int kzgmi_ck_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1_powers, siz
                         inf + (size_t)w * n);
       L::pts_to29(st, pts, (uint32_t)(CK_ROWS * n));  // resident in the accumulation's format
       okk = okk && hipGetLastError() == hipSuccess &&
-            hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
-            hipStreamSynchronize(st) == hipSuccess;
+            hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st) == hipSuccess && sync_job(s) == 0;
     }
     if (!okk) {
       delete ck;
@@ -1281,6 +1444,7 @@ void kzgmi_ck_free(kzgmi_ck* ck) {
 }
 
 int kzgmi_commit_device_async(kzgmi_ctx* c, const kzgmi_ck* ck, int slot, const void* d_coeffs, size_t m) {
+  KZ_ROUTE(c, nullptr, slot);  // (commit keys live on the primary device: its slots only)
   CHK(check_ctx(c, slot));
   if (!ck || ck->ctx != c) return fail(KZGMI_ERR_ARG, "commit key does not belong to this context");
   if (m && !d_coeffs) return fail(KZGMI_ERR_ARG, "null argument");
@@ -1291,10 +1455,11 @@ int kzgmi_commit_device_async(kzgmi_ctx* c, const kzgmi_ck* ck, int slot, const 
     using Cv = decltype(cv);
     using L = Launch<Cv>;
     const size_t gb = g1_bytes(Cv::ID);
-    hipStream_t st = s.stream;
     CHK(s.flags.ensure(16));
     CHK(s.outb.ensure(gb));
     CHK(s.res.ensure(2 * sizeof(Xyzz<Cv>)));
+    CHK(begin_job(c, s, LANE_FRONT));
+    hipStream_t st = s.stream;
     HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
     if (m == 0) {
       HIPCHK(hipMemsetAsync(s.res.p, 0, sizeof(Xyzz<Cv>), st));  // zz = 0: infinity
@@ -1315,11 +1480,13 @@ int kzgmi_commit_device_async(kzgmi_ctx* c, const kzgmi_ck* ck, int slot, const 
       MsmWindows mw{1, {0, 0}, {1, 0}};
       CHK(run_msm_core<Cv>(c, s, tl, 1, (size_t)CK_ROWS * m + 16, mw, ck->pts.template as<Affine<Cv>>(),
                            ck->inf.template as<uint8_t>()));
+      st = s.stream;  // the tail lane
     }
     Launch<Cv>::encode_points(st, s.res.template as<Xyzz<Cv>>(), 1, s.outb.template as<uint8_t>());
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(s.host_out, s.outb.p, gb, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
+    CHK(end_job(s));
     s.pending = true;
     s.partial_job = false;
     s.partial_of = 0;
@@ -1342,6 +1509,7 @@ int kzgmi_commit(kzgmi_ctx* c, const kzgmi_ck* ck, const uint8_t* coeffs, size_t
   CHK(slot0_idle(c));
   Slot& s = c->slots[0];
   CHK(s.stage.ensure(m * 32));
+  CHK(begin_job(c, s, LANE_FRONT));  // the commit's job starts in the same lane, behind this copy
   HIPCHK(hipMemcpyAsync(s.stage.p, coeffs, m * 32, hipMemcpyHostToDevice, s.stream));
   return kzgmi_commit_device(c, ck, s.stage.p, m, out);
 }
@@ -1372,6 +1540,7 @@ int kzgmi_msm_g1_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dpts, const
 
 int kzgmi_msm_g1_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, const void* dpts, const void* dsc,
                               size_t n) {
+  KZ_ROUTE(c, nullptr, slot);
   CHK(check_ctx(c, slot));
   if (n && (!dpts || !dsc)) return fail(KZGMI_ERR_ARG, "null argument");
   if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "MSM too large (max 2^26 points per call)");
@@ -1382,7 +1551,7 @@ int kzgmi_msm_g1_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, const v
     using Cv = decltype(cv);
     const size_t gb = g1_bytes(Cv::ID);
     if (n == 0) {
-      HIPCHK(hipStreamSynchronize(s.stream));  // host_out/host_flags may still be copy targets
+      CHK(sync_slot(s));  // host_out/host_flags may still be copy targets
       memset(s.host_out, 0, gb);
       if (Cv::ID == 0) s.host_out[0] = 0x40;
       s.host_flags[0] = 1;
@@ -1394,6 +1563,7 @@ int kzgmi_msm_g1_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, const v
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemcpyAsync(s.host_out, s.outb.p, gb, hipMemcpyDeviceToHost, s.stream));
       HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, s.stream));
+      CHK(end_job(s));
     }
     s.pending = true;
     s.partial_job = false;
@@ -1405,6 +1575,7 @@ int kzgmi_msm_g1_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, const v
 }
 
 int kzgmi_msm_wait(kzgmi_ctx* c, int slot, uint8_t* out) {
+  KZ_ROUTE(c, nullptr, slot);
   CHK(check_ctx(c, slot));
   Slot& s = c->slots[slot];
   if (!s.pending || !s.msm_job) return fail(KZGMI_ERR_ARG, "slot has no pending MSM");
@@ -1427,6 +1598,7 @@ int kzgmi_msm_g1(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* points, const u
   CHK(s.stage.ensure(n * (gb + 32)));
   uint8_t* dp = s.stage.template as<uint8_t>();
   uint8_t* ds = dp + n * gb;
+  CHK(begin_job(c, s, LANE_FRONT));  // the MSM's job starts in the same lane, behind these copies
   HIPCHK(hipMemcpyAsync(dp, points, n * gb, hipMemcpyHostToDevice, s.stream));
   HIPCHK(hipMemcpyAsync(ds, scalars, n * 32, hipMemcpyHostToDevice, s.stream));
   return kzgmi_msm_g1_device(c, curve, dp, ds, n, out);
@@ -1440,6 +1612,7 @@ size_t kzgmi_partial_bytes(kzgmi_curve curve) {
 int kzgmi_batch_partial_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const void* dC, const void* dz,
                                      const void* dy, const void* dpi, size_t n, uint64_t index_offset,
                                      const uint8_t* seed32, uint32_t flags, void* d_partial_out) {
+  KZ_ROUTE(c, &srs, slot);
   Roctx rx("kzgmi_batch_partial_device_async");
   if (flags & ~kAllFlags) return fail(KZGMI_ERR_ARG, "unknown flags");
   if (flags & KZGMI_FLAG_FIAT_SHAMIR)
@@ -1461,9 +1634,10 @@ int kzgmi_batch_partial_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slo
     using Cv = decltype(cv);
     if (n == 0) {  // empty shard: both partials are the point at infinity (zz = 0)
       CHK(s.flags.ensure(16));
+      CHK(begin_job(c, s, LANE_TAIL));
       HIPCHK(hipMemsetAsync(d_partial_out, 0, 2 * sizeof(Xyzz<Cv>), s.stream));
       HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));  // a chained combine keeps the error word
-      HIPCHK(hipStreamSynchronize(s.stream));
+      CHK(sync_job(s));
       s.host_flags[0] = 1;
       s.host_flags[1] = 0;
       s.pending = true;
@@ -1486,6 +1660,7 @@ int kzgmi_batch_partial_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* d
 
 int kzgmi_batch_combine_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const void* d_partials,
                                      int n_parts) {
+  KZ_ROUTE(c, &srs, slot);
   CHK(check_ctx(c, slot));
   if (!srs || srs->ctx != c || !d_partials || n_parts < 1) return fail(KZGMI_ERR_ARG, "bad argument");
   Slot& s = c->slots[slot];
@@ -1499,17 +1674,20 @@ int kzgmi_batch_combine_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slo
     using XY = Xyzz<Cv>;
     CHK(s.res.ensure(2 * sizeof(XY)));
     CHK(s.flags.ensure(16));
+    CHK(begin_job(c, s, LANE_TAIL));  // chained: the lane the partial ended in
     hipStream_t st = s.stream;
     if (!chain) {
       HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
       mark(c, s, PH_COMBINE);
     }
-    Launch<Cv>::sum_partials(st, (const XY*)d_partials, (uint32_t)n_parts, 2, 2, s.res.template as<XY>());
+    Launch<Cv>::sum_partials(st, (const XY*)d_partials, (uint32_t)n_parts, 2, 2, s.res.template as<XY>(),
+                             s.flags.template as<uint32_t>() + 1);
     Launch<Cv>::pairing_check(st, s.res.template as<XY>(), srs->lines.template as<Line<Cv>>(),
                               srs->q_inf.template as<uint8_t>(), s.flags.template as<int>());
     mark(c, s, PH_PAIRING + 1);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
+    CHK(end_job(s));
     s.pending = true;
     s.partial_job = false;
     s.partial_of = 0;
@@ -1539,6 +1717,7 @@ int kzgmi_g1_validate_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_poin
     CHK(s.pts.ensure(n * sizeof(Affine<Cv>)));
     CHK(s.inf.ensure(n));
     CHK(s.flags.ensure(16));
+    CHK(begin_job(c, s, LANE_FRONT));
     hipStream_t st = s.stream;
     HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
     uint32_t* err = s.flags.template as<uint32_t>() + 1;
@@ -1552,6 +1731,7 @@ int kzgmi_g1_validate_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_poin
       L::subgroup_check(st, s.pts.template as<Affine<Cv>>(), s.inf.template as<uint8_t>(), (uint32_t)n, err);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
+    CHK(end_job(s));
     s.pending = true;
     s.partial_job = true;
     s.msm_job = false;
@@ -1571,19 +1751,19 @@ static int fs_chunk_digests_enqueue(kzgmi_ctx* c, kzgmi_curve curve, const void*
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     const uint32_t* dg = nullptr;
+    CHK(begin_job(c, s, LANE_FRONT));
     CHK(enqueue_fs_digests<Cv>(s, dC, dpi, dz, dy, n, index_offset, (flags & KZGMI_FLAG_COMPRESSED) != 0, &dg));
     const size_t nch = (n + FS_CHUNK - 1) / FS_CHUNK;
     HIPCHK(hipMemcpyAsync(d_out, dg, nch * 32, hipMemcpyDeviceToDevice, s.stream));
     HIPCHK(hipGetLastError());
-    return 0;
+    return end_job(s);
   });
 }
 
 int kzgmi_fs_chunk_digests_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dC, const void* dz, const void* dy,
                                   const void* dpi, size_t n, uint64_t index_offset, uint32_t flags, void* d_out) {
   CHK(fs_chunk_digests_enqueue(c, curve, dC, dz, dy, dpi, n, index_offset, flags, d_out));
-  HIPCHK(hipStreamSynchronize(c->slots[0].stream));
-  return 0;
+  return sync_slot(c->slots[0]);
 }
 
 int kzgmi_fs_challenge_from_digests_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_digests, size_t nchunks,
@@ -1595,11 +1775,12 @@ int kzgmi_fs_challenge_from_digests_device(kzgmi_ctx* c, kzgmi_curve curve, cons
   if (s.pending) return fail(KZGMI_ERR_ARG, "slot 0 busy: call kzgmi_slot_wait first");
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
+    CHK(begin_job(c, s, LANE_FRONT));
     CHK(enqueue_fs_challenge<Cv>(s, (const uint32_t*)d_digests, (uint32_t)nchunks, n_total));
     uint32_t w[8];
     HIPCHK(hipMemcpyAsync(w, s.chal.p, 32, hipMemcpyDeviceToHost, s.stream));
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(s.stream));
+    CHK(sync_job(s));
     for (int k = 0; k < 8; ++k)
       for (int b = 0; b < 4; ++b) r_out[4 * k + b] = (uint8_t)(w[k] >> (24 - 8 * b));
     return 0;
@@ -1616,12 +1797,13 @@ int kzgmi_fs_challenge_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dC, c
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     const uint32_t* dg = nullptr;
+    CHK(begin_job(c, s, LANE_FRONT));
     CHK(enqueue_fs_digests<Cv>(s, dC, dpi, dz, dy, n, 0, (flags & KZGMI_FLAG_COMPRESSED) != 0, &dg));
     CHK(enqueue_fs_challenge<Cv>(s, dg, (uint32_t)((n + FS_CHUNK - 1) / FS_CHUNK), n));
     uint32_t w[8];
     HIPCHK(hipMemcpyAsync(w, s.chal.p, 32, hipMemcpyDeviceToHost, s.stream));
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(s.stream));
+    CHK(sync_job(s));
     for (int k = 0; k < 8; ++k)
       for (int b = 0; b < 4; ++b) r_out[4 * k + b] = (uint8_t)(w[k] >> (24 - 8 * b));
     return 0;
@@ -1635,9 +1817,10 @@ int kzgmi_g1_compress_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_poin
   CHK(slot0_idle(c));
   Slot& s = c->slots[0];
   return dispatch(curve, [&](auto cv) -> int {
+    CHK(begin_job(c, s, LANE_FRONT));
     Launch<decltype(cv)>::compress_points(s.stream, (const uint8_t*)d_points, (uint32_t)n, (uint8_t*)d_out);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(s.stream));
+    CHK(sync_job(s));
     return 0;
   });
 }
@@ -1658,13 +1841,15 @@ int kzgmi_msm_partial_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dpts, 
       return 0;
     }
     CHK(enqueue_msm<Cv>(c, s, dpts, dsc, n));
-    HIPCHK(hipMemcpyAsync(d_partial_out, s.res.p, sizeof(Xyzz<Cv>), hipMemcpyDeviceToDevice, s.stream));
+    Launch<Cv>::partial_out(s.stream, s.res.template as<Xyzz<Cv>>(), 1, s.flags.template as<uint32_t>() + 1,
+                            (Xyzz<Cv>*)d_partial_out);
     return read_flags_sync(c, s);
   });
 }
 
 int kzgmi_msm_partial_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, const void* dpts, const void* dsc,
                                    size_t n, void* d_partial_out) {
+  KZ_ROUTE(c, nullptr, slot);
   CHK(check_ctx(c, slot));
   Roctx rx("kzgmi_msm_partial_device_async");
   if (!d_partial_out || (n && (!dpts || !dsc))) return fail(KZGMI_ERR_ARG, "bad argument");
@@ -1675,15 +1860,19 @@ int kzgmi_msm_partial_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, co
     using Cv = decltype(cv);
     if (n == 0) {
       CHK(s.flags.ensure(16));
-      HIPCHK(hipStreamSynchronize(s.stream));
+      CHK(sync_slot(s));  // host_flags may still be a copy target
+      CHK(begin_job(c, s, LANE_TAIL));
       HIPCHK(hipMemsetAsync(d_partial_out, 0, sizeof(Xyzz<Cv>), s.stream));  // ZZ = 0: infinity
       HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));  // a chained combine keeps the error word
+      CHK(end_job(s));
       s.host_flags[0] = 1;
       s.host_flags[1] = 0;
     } else {
       CHK(enqueue_msm<Cv>(c, s, dpts, dsc, n));
-      HIPCHK(hipMemcpyAsync(d_partial_out, s.res.p, sizeof(Xyzz<Cv>), hipMemcpyDeviceToDevice, s.stream));
+      Launch<Cv>::partial_out(s.stream, s.res.template as<Xyzz<Cv>>(), 1, s.flags.template as<uint32_t>() + 1,
+                              (Xyzz<Cv>*)d_partial_out);
       HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, s.stream));
+      CHK(end_job(s));
     }
     s.pending = true;
     s.partial_job = true;
@@ -1695,6 +1884,7 @@ int kzgmi_msm_partial_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, co
 }
 
 int kzgmi_msm_combine_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, const void* d_partials, int n_parts) {
+  KZ_ROUTE(c, nullptr, slot);
   CHK(check_ctx(c, slot));
   if (!d_partials || n_parts < 1) return fail(KZGMI_ERR_ARG, "bad argument");
   Slot& s = c->slots[slot];
@@ -1708,12 +1898,15 @@ int kzgmi_msm_combine_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, co
     CHK(s.res.ensure(2 * sizeof(XY)));
     CHK(s.outb.ensure(gb));
     CHK(s.flags.ensure(16));
+    CHK(begin_job(c, s, LANE_TAIL));  // chained: the lane the partial ended in
     if (!chain) HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));
-    Launch<Cv>::sum_partials(s.stream, (const XY*)d_partials, (uint32_t)n_parts, 1, 1, s.res.template as<XY>());
+    Launch<Cv>::sum_partials(s.stream, (const XY*)d_partials, (uint32_t)n_parts, 1, 1, s.res.template as<XY>(),
+                             s.flags.template as<uint32_t>() + 1);
     Launch<Cv>::encode_points(s.stream, s.res.template as<XY>(), 1, s.outb.template as<uint8_t>());
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(s.host_out, s.outb.p, gb, hipMemcpyDeviceToHost, s.stream));
     HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, s.stream));
+    CHK(end_job(s));
     s.pending = true;
     s.partial_job = false;
     s.partial_of = 0;
@@ -1734,10 +1927,14 @@ int kzgmi_msm_combine_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_part
     const size_t gb = g1_bytes(Cv::ID);
     CHK(s.res.ensure(2 * sizeof(XY)));
     CHK(s.outb.ensure(gb));
-    Launch<Cv>::sum_partials(s.stream, (const XY*)d_partials, (uint32_t)n_parts, 1, 1, s.res.template as<XY>());
+    CHK(s.flags.ensure(16));
+    CHK(begin_job(c, s, LANE_TAIL));
+    HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));
+    Launch<Cv>::sum_partials(s.stream, (const XY*)d_partials, (uint32_t)n_parts, 1, 1, s.res.template as<XY>(),
+                             s.flags.template as<uint32_t>() + 1);
     Launch<Cv>::encode_points(s.stream, s.res.template as<XY>(), 1, s.outb.template as<uint8_t>());
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(s.stream));
+    CHK(read_flags_sync(c, s));
     HIPCHK(hipMemcpy(out, s.outb.p, gb, hipMemcpyDeviceToHost));
     return 0;
   });
@@ -1762,6 +1959,7 @@ int kzgmi_pairing(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uint
     CHK(s.stage.ensure(96 + 32));
     CHK(s.outb.ensure(96));
     uint8_t* dp = s.stage.template as<uint8_t>();
+    CHK(begin_job(c, s, LANE_FRONT));  // the MSM's job starts in the same lane, behind these copies
     HIPCHK(hipMemcpyAsync(dp, g1, 96, hipMemcpyHostToDevice, s.stream));
     HIPCHK(hipMemcpyAsync(dp + 96, kInv3, 32, hipMemcpyHostToDevice, s.stream));
     CHK(enqueue_msm<Cv>(c, s, dp, dp + 96, 1, /*allow_glv=*/false));
@@ -1786,6 +1984,7 @@ int kzgmi_pairing(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uint
     memcpy(h.data(), g1, gb1);
     memcpy(h.data() + gb1, g2, gb2);
     memcpy(h.data() + gb1 + gb2, g2, gb2);
+    CHK(begin_job(c, s, LANE_FRONT));
     hipStream_t st = s.stream;
     uint8_t* d = s.stage.template as<uint8_t>();
     Line<Cv>* lines = c->lines_tmp.template as<Line<Cv>>();
@@ -1813,6 +2012,7 @@ int kzgmi_gen_g1(kzgmi_ctx* c, kzgmi_curve curve, const void* d_scalars, size_t 
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     Slot& s = c->slots[0];
+    CHK(begin_job(c, s, LANE_FRONT));
     CHK(ensure_table<Cv>(c, s.stream));
     CHK(s.flags.ensure(16));
     HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));
@@ -1833,6 +2033,7 @@ int kzgmi_gen_tuples(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* tau32, cons
     using Cv = decltype(cv);
     using FrF = Fp<typename Cv::FrP>;
     Slot& s = c->slots[0];
+    CHK(begin_job(c, s, LANE_FRONT));
     CHK(ensure_table<Cv>(c, s.stream));
     FrF tau;
     for (int k = 0; k < 8; ++k)
@@ -1849,7 +2050,7 @@ int kzgmi_gen_tuples(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* tau32, cons
       Launch<Cv>::gen_tuples(s.stream, seed, tau.v, (uint32_t)n, c->table[Cv::ID].template as<Affine<Cv>>(),
                                                            (uint8_t*)dC, (uint8_t*)dz, (uint8_t*)dy, (uint8_t*)dpi);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(s.stream));
+    CHK(sync_job(s));
     return 0;
   });
 }
@@ -1874,6 +2075,7 @@ int kzgmi_g2_mul(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g2, const uint8
       if (k[j] < Cv::FrP::MOD[j]) break;
       if (k[j] > Cv::FrP::MOD[j] || j == 0) return fail(KZGMI_ERR_SCALAR, "k >= r");
     }
+    CHK(begin_job(c, s, LANE_FRONT));
     hipStream_t st = s.stream;
     uint8_t* d = s.stage.template as<uint8_t>();
     HIPCHK(hipMemcpyAsync(d, g2, gb, hipMemcpyHostToDevice, st));
@@ -1900,11 +2102,12 @@ int kzgmi_probe_fpmul(kzgmi_ctx* c, kzgmi_curve curve, double* muls_per_s) {
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
+    CHK(begin_job(c, s, LANE_FRONT));
     Launch<Cv>::fpmul_probe(s.stream, blocks, 16, c->tmp.template as<uint32_t>());  // warm-up
     HIPCHK(hipEventRecord(e0, s.stream));
     Launch<Cv>::fpmul_probe(s.stream, blocks, iters, c->tmp.template as<uint32_t>());
     HIPCHK(hipEventRecord(e1, s.stream));
-    HIPCHK(hipEventSynchronize(e1));
+    CHK(sync_job(s));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);
@@ -1954,15 +2157,14 @@ int kzgmi_get_phase_ms(kzgmi_ctx* c, double* out, int max_n) {
 
 // ------------------------------------------------------------------------------ stream order
 int kzgmi_stream_wait(kzgmi_ctx* c, int slot, void* stream) {
+  KZ_ROUTE(c, nullptr, slot);
   CHK(check_ctx(c, slot));
-  Slot& s = c->slots[slot];
-  if (!s.order_ev) HIPCHK(hipEventCreateWithFlags(&s.order_ev, hipEventDisableTiming));
-  HIPCHK(hipEventRecord(s.order_ev, (hipStream_t)stream));
-  HIPCHK(hipStreamWaitEvent(s.stream, s.order_ev, 0));
-  return 0;
+  // an entry dependency of the slot's next job (begin_job), whichever lane that job starts in
+  return add_dep(c->slots[slot], (hipStream_t)stream);
 }
 
 int kzgmi_slot_signal(kzgmi_ctx* c, int slot, void* stream) {
+  KZ_ROUTE(c, nullptr, slot);
   CHK(check_ctx(c, slot));
   Slot& s = c->slots[slot];
   if (!s.signal_ev) HIPCHK(hipEventCreateWithFlags(&s.signal_ev, hipEventDisableTiming));
@@ -1980,10 +2182,11 @@ int kzgmi_partial_encode_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_r
     Slot& s = c->slots[0];
     const size_t gb = g1_bytes(Cv::ID);
     CHK(s.outb.ensure(count * gb));
+    CHK(begin_job(c, s, LANE_TAIL));
     Launch<Cv>::encode_points(s.stream, (const Xyzz<Cv>*)d_records, (uint32_t)count, s.outb.template as<uint8_t>());
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out, s.outb.p, count * gb, hipMemcpyDeviceToHost, s.stream));
-    HIPCHK(hipStreamSynchronize(s.stream));
+    CHK(sync_job(s));
     return 0;
   });
 }
@@ -1992,22 +2195,32 @@ int kzgmi_partial_encode_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_r
 int kzgmi_ctx_create(kzgmi_ctx** out, const int* device_ids, int n_devices, int pipeline_slots) {
   if (!out || !device_ids || n_devices < 1 || n_devices > 64) return fail(KZGMI_ERR_ARG, "bad ctx args");
   *out = nullptr;
+  if (pipeline_slots < 1 || pipeline_slots > 64) return fail(KZGMI_ERR_ARG, "bad ctx args");
   kzgmi_ctx* c = nullptr;
-  CHK(kzgmi_ctx_create_device(&c, device_ids[0], pipeline_slots));
+  // every device holds ceil(slots / n_devices) local slots (route_slot)
+  const int local = (pipeline_slots + n_devices - 1) / n_devices;
+  CHK(kzgmi_ctx_create_device(&c, device_ids[0], local));
   for (int k = 1; k < n_devices; ++k) {
     kzgmi_ctx* p = nullptr;
-    if (int r = kzgmi_ctx_create_device(&p, device_ids[k], 1)) {  // peers only ever run on their slot 0
+    if (int r = kzgmi_ctx_create_device(&p, device_ids[k], local)) {
       kzgmi_ctx_destroy(c);
       return r;
     }
     c->peers.push_back(p);
   }
+  c->user_slots = pipeline_slots;
   CHK(set_dev(c));
   *out = c;
   return 0;
 }
 
 int kzgmi_ctx_num_devices(const kzgmi_ctx* c) { return c ? 1 + (int)c->peers.size() : 0; }
+
+int kzgmi_slot_device(const kzgmi_ctx* c, int slot) {
+  if (!c || slot < 0 || slot >= c->user_slots) return fail(KZGMI_ERR_ARG, "bad slot");
+  const int D = 1 + (int)c->peers.size();
+  return slot % D == 0 ? c->device : c->peers[slot % D - 1]->device;
+}
 
 }  // extern "C"
 
@@ -2016,8 +2229,6 @@ int kzgmi_ctx_num_devices(const kzgmi_ctx* c) { return c ? 1 + (int)c->peers.siz
 // primary sums them and runs the pairing check -- the single-process form of the RCCL
 // all-gather that kzgmi/distributed.py does across processes.
 namespace {
-
-kzgmi_ctx* dev_ctx(kzgmi_ctx* c, int d) { return d == 0 ? c : c->peers[d - 1]; }
 
 // wait every device's slot 0 (first error wins; every slot is completed either way)
 int wait_all(kzgmi_ctx* c, int started) {
@@ -2040,6 +2251,7 @@ int wait_all(kzgmi_ctx* c, int started) {
 // runtime orders a null-stream peer copy against a non-blocking stream
 int gather_records(kzgmi_ctx* c, size_t rec) {
   CHK(set_dev(c));
+  CHK(begin_job(c, c->slots[0], LANE_TAIL));  // the combine's job starts in the same lane, behind these copies
   for (size_t d = 1; d <= c->peers.size(); ++d) {
     kzgmi_ctx* p = c->peers[d - 1];
     HIPCHK(hipMemcpyPeerAsync((uint8_t*)c->gath.p + d * rec, c->device, p->gath.p, p->device, rec, c->slots[0].stream));
@@ -2089,8 +2301,9 @@ int batch_multi(kzgmi_ctx* c, const kzgmi_srs* srs, const void* const* dC, const
       kzgmi_ctx* p = dev_ctx(c, d);
       const size_t nch = (nd[d] + FS_CHUNK - 1) / FS_CHUNK;
       CHK(set_dev(p));
-      HIPCHK(hipStreamSynchronize(p->slots[0].stream));
+      CHK(sync_slot(p->slots[0]));
       CHK(set_dev(c));
+      CHK(begin_job(c, c->slots[0], LANE_FRONT));  // the challenge's job follows in this lane
       HIPCHK(hipMemcpyPeerAsync((uint8_t*)c->mdig_all.p + at * 32, c->device, p->mdig.p, p->device, nch * 32,
                                 c->slots[0].stream));
       at += nch;
@@ -2185,6 +2398,7 @@ int batch_multi_host(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commitme
     ppi[d] = base + nd[d] * gb;
     pz[d] = base + 2 * nd[d] * gb;
     py[d] = base + 2 * nd[d] * gb + 32 * nd[d];
+    CHK(begin_job(p, s, LANE_FRONT));  // the shard's job starts in the same lane, behind these copies
     if (nd[d]) {
       HIPCHK(hipMemcpyAsync((void*)pC[d], commitments + lo * gb, nd[d] * gb, hipMemcpyHostToDevice, s.stream));
       HIPCHK(hipMemcpyAsync((void*)ppi[d], proofs + lo * gb, nd[d] * gb, hipMemcpyHostToDevice, s.stream));
@@ -2210,6 +2424,7 @@ int msm_multi_host(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* points, const
     CHK(s.stage.ensure(nd[d] * (gb + 32)));
     pp[d] = s.stage.p;
     ps[d] = s.stage.template as<uint8_t>() + nd[d] * gb;
+    CHK(begin_job(p, s, LANE_FRONT));
     if (nd[d]) {
       HIPCHK(hipMemcpyAsync((void*)pp[d], points + lo * gb, nd[d] * gb, hipMemcpyHostToDevice, s.stream));
       HIPCHK(hipMemcpyAsync((void*)ps[d], scalars + lo * 32, nd[d] * 32, hipMemcpyHostToDevice, s.stream));

@@ -9,7 +9,9 @@
 namespace kzgmi {
 
 // device-side error codes (atomicMax into the context's error word; host maps to KZGMI_ERR_*)
-enum : uint32_t { DERR_NONE = 0, DERR_ENCODING = 1, DERR_NOT_ON_CURVE = 2, DERR_SCALAR = 3, DERR_NOT_IN_SUBGROUP = 4 };
+// DERR_SHARD: a gathered partial record was marked failed without a code of its own (k_sum_partials)
+enum : uint32_t { DERR_NONE = 0, DERR_ENCODING = 1, DERR_NOT_ON_CURVE = 2, DERR_SCALAR = 3, DERR_NOT_IN_SUBGROUP = 4,
+                  DERR_SHARD = 5 };
 
 KZ_DEV void raise_err(uint32_t* err, uint32_t code) { atomicMax(err, code); }
 
@@ -17,11 +19,7 @@ KZ_DEV void raise_err(uint32_t* err, uint32_t code) { atomicMax(err, code); }
 // run one to a few waves per CU beside the accumulation of other pipelined batches (4 waves
 // per SIMD).  Raising their wave priority lets the SIMD's issue arbiter pick them first, so a
 // batch's tail is not stretched ~4x while full-chip work shares its SIMDs.
-#ifdef KZ_NO_TAIL_PRIO
-#define KZ_TAIL_PRIO() ((void)0)
-#else
 #define KZ_TAIL_PRIO() __builtin_amdgcn_s_setprio(3)
-#endif
 
 // Fiat-Shamir transcript geometry (fs.hpp)
 constexpr uint32_t FS_CHUNK = 4096;  // leaves per shard-alignment subtree

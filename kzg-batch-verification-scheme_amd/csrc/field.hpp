@@ -91,40 +91,6 @@ KZ_DEV Fp<P> fp_select(bool c, const Fp<P>& a, const Fp<P>& b) {
   return r;
 }
 
-// ---------------------------------------------------------------------------- mul (CIOS)
-// t = a*b*R^-1 mod p.  Per outer i:
-//   (A, t[0]) = t[0] + a[0]*b[i];  m = t[0]*INV;  C = hi(t[0] + m*p[0])
-//   for j>0: (A, t[j]) = t[j] + a[j]*b[i] + A;  (C, t[j-1]) = t[j] + m*p[j] + C
-//   t[N-1] = C + A
-template <class P>
-KZ_DEV Fp<P> fp_mul_cios(const Fp<P>& a, const Fp<P>& b) {
-  constexpr int N = P::N;
-  uint32_t t[N];
-  _Pragma("unroll") for (int i = 0; i < N; ++i) t[i] = 0;
-  _Pragma("unroll") for (int i = 0; i < N; ++i) {
-    const uint32_t bi = b.v[i];
-    uint64_t x = (uint64_t)a.v[0] * bi + t[0];
-    uint32_t A = (uint32_t)(x >> 32);
-    uint32_t t0 = (uint32_t)x;
-    uint32_t m = t0 * P::INV;
-    uint64_t y = (uint64_t)m * P::MOD[0] + t0;
-    uint32_t C = (uint32_t)(y >> 32);
-    _Pragma("unroll") for (int j = 1; j < N; ++j) {
-      x = (uint64_t)a.v[j] * bi + t[j] + A;
-      A = (uint32_t)(x >> 32);
-      y = (uint64_t)m * P::MOD[j] + (uint32_t)x + C;
-      C = (uint32_t)(y >> 32);
-      t[j - 1] = (uint32_t)y;
-    }
-    t[N - 1] = C + A;
-  }
-  // result < 2p: one conditional subtraction
-  Fp<P> r, d;
-  uint32_t bw = 0;
-  _Pragma("unroll") for (int i = 0; i < N; ++i) d.v[i] = __builtin_subc(t[i], P::MOD[i], bw, &bw);
-  _Pragma("unroll") for (int i = 0; i < N; ++i) r.v[i] = bw ? t[i] : d.v[i];
-  return r;
-}
 
 // ---------------------------------------------------------------------------- mul (product scanning)
 // Same result as fp_mul (CIOS), different schedule: column-wise (FIPS) Montgomery with a
@@ -308,11 +274,7 @@ KZ_DEV Fp<P> fp_canon(const Fp<P>& a) {  // a < 2p -> a mod p
 // Default multiplication used by every kernel.
 template <class P>
 KZ_DEV Fp<P> fp_mul(const Fp<P>& a, const Fp<P>& b) {
-#ifdef KZ_MUL_CIOS
-  return fp_mul_cios(a, b);
-#else
   return fp_mul_ps(a, b);
-#endif
 }
 
 template <class P>
@@ -380,85 +342,11 @@ KZ_DEV Fp<P> fp_pow_sqrt(const Fp<P>& a) {
   return acc;
 }
 
-// A/B reference (KZ_INV_CLASSIC): the bit-serial binary extended Euclid, ~566 K cycles on one
-// lane for BLS12-381.  Returns a^-1 in Montgomery form; 0 -> 0.
-// Invariants: u*x == a_raw*R^? ...; implemented as the classic "u, v, x1, x2" binary
-// inversion on raw integers, then fixed up by two Montgomery multiplications.
-template <class P>
-KZ_DEV void big_rshift1(uint32_t (&x)[P::N]) {
-  _Pragma("unroll") for (int i = 0; i < P::N - 1; ++i) x[i] = (x[i] >> 1) | (x[i + 1] << 31);
-  x[P::N - 1] >>= 1;
-}
-template <class P>
-KZ_DEV bool big_is_one(const uint32_t (&x)[P::N]) {
-  uint32_t acc = x[0] ^ 1u;
-  _Pragma("unroll") for (int i = 1; i < P::N; ++i) acc |= x[i];
-  return acc == 0;
-}
-template <class P>
-KZ_DEV bool big_geq(const uint32_t (&a)[P::N], const uint32_t (&b)[P::N]) {
-  uint32_t bw = 0;
-  _Pragma("unroll") for (int i = 0; i < P::N; ++i) (void)__builtin_subc(a[i], b[i], bw, &bw);
-  return bw == 0;
-}
-template <class P>
-KZ_DEV void big_sub(uint32_t (&a)[P::N], const uint32_t (&b)[P::N]) {
-  uint32_t bw = 0;
-  _Pragma("unroll") for (int i = 0; i < P::N; ++i) a[i] = __builtin_subc(a[i], b[i], bw, &bw);
-}
-// x = x/2 mod p (x < p)
-template <class P>
-KZ_DEV void half_mod(uint32_t (&x)[P::N]) {
-  if (x[0] & 1) {
-    uint32_t c = 0;
-    _Pragma("unroll") for (int i = 0; i < P::N; ++i) x[i] = __builtin_addc(x[i], P::MOD[i], c, &c);
-    // x + p < 2^(32N) since p < 2^(32N-1)
-  }
-  big_rshift1<P>(x);
-}
-// x = x - y mod p (both < p)
-template <class P>
-KZ_DEV void sub_mod(uint32_t (&x)[P::N], const uint32_t (&y)[P::N]) {
-  uint32_t bw = 0;
-  _Pragma("unroll") for (int i = 0; i < P::N; ++i) x[i] = __builtin_subc(x[i], y[i], bw, &bw);
-  if (bw) {
-    uint32_t c = 0;
-    _Pragma("unroll") for (int i = 0; i < P::N; ++i) x[i] = __builtin_addc(x[i], P::MOD[i], c, &c);
-  }
-}
-
-template <class P>
-KZ_DEV Fp<P> fp_inv_classic(const Fp<P>& a) {
-  constexpr int N = P::N;
-  if (a.is_zero()) return a;
-  // a is a*R (Montgomery).  Binary EEA computes (aR)^-1 mod p on raw integers; then
-  // (aR)^-1 * R^3 (two mont-muls by R2... ) gives a^-1 R.
-  uint32_t u[N], v[N], x1[N], x2[N];
-  _Pragma("unroll") for (int i = 0; i < N; ++i) { u[i] = a.v[i]; v[i] = P::MOD[i]; x1[i] = 0; x2[i] = 0; }
-  x1[0] = 1;
-  // invariant: x1*a == u, x2*a == v (mod p)
-  while (!big_is_one<P>(u) && !big_is_one<P>(v)) {
-    while ((u[0] & 1) == 0) { big_rshift1<P>(u); half_mod<P>(x1); }
-    while ((v[0] & 1) == 0) { big_rshift1<P>(v); half_mod<P>(x2); }
-    if (big_geq<P>(u, v)) { big_sub<P>(u, v); sub_mod<P>(x1, x2); }
-    else { big_sub<P>(v, u); sub_mod<P>(x2, x1); }
-  }
-  Fp<P> r;
-  if (big_is_one<P>(u)) { _Pragma("unroll") for (int i = 0; i < N; ++i) r.v[i] = x1[i]; }
-  else { _Pragma("unroll") for (int i = 0; i < N; ++i) r.v[i] = x2[i]; }
-  // r = (aR)^-1 (raw).  Want a^-1 R = r * R^2:  mont(r, R2) = r R^2 R^-1 = rR; twice -> rR^2.
-  Fp<P> r2 = Fp<P>::from_const(P::R2);
-  return fp_mul(fp_mul(r, r2), r2);
-}
-
 // a^-1 in Montgomery form (0 -> 0) for the single-lane tails (MSM result -> affine, the
 // pairing's Fp inversion): the word-level binary GCD of bingcd.hpp on the raw Montgomery value
 // aR, giving (aR)^-1, then two Montgomery products by R^2: (aR)^-1 R^2 = a^-1 R.
 template <class P>
 KZ_DEV Fp<P> fp_inv(const Fp<P>& a) {
-#if defined(KZ_INV_CLASSIC)
-  return fp_inv_classic(a);
-#else
   constexpr int N = P::N;
   uint32_t y[N], m[N], r[N];
   _Pragma("unroll") for (int i = 0; i < N; ++i) { y[i] = a.v[i]; m[i] = P::MOD[i]; }
@@ -474,7 +362,6 @@ KZ_DEV Fp<P> fp_inv(const Fp<P>& a) {
   _Pragma("unroll") for (int i = 0; i < N; ++i) x.v[i] = r[i];
   const Fp<P> r2 = Fp<P>::from_const(P::R2);
   return fp_mul(fp_mul(x, r2), r2);
-#endif
 }
 
 // ---------------------------------------------------------------------------- bytes

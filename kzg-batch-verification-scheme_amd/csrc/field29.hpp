@@ -47,11 +47,6 @@ struct F29 {
   }
 };
 
-#ifdef KZ_MAD29_PLAIN
-// A/B variant: let hipcc emit the v_mad_u64_u32 (no inline-asm boundary s_nop padding)
-KZ_DEV void mad29(uint64_t& acc, uint32_t a, uint32_t b) { acc += (uint64_t)a * (uint64_t)b; }
-KZ_DEV void mad29s(uint64_t& acc, uint32_t a, uint32_t b_uniform) { acc += (uint64_t)a * (uint64_t)b_uniform; }
-#else
 KZ_DEV void mad29(uint64_t& acc, uint32_t a, uint32_t b) {
   uint64_t cc;  // carry-out unused: column sums stay below 2^64
   asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
@@ -60,7 +55,6 @@ KZ_DEV void mad29s(uint64_t& acc, uint32_t a, uint32_t b_uniform) {
   uint64_t cc;
   asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "s"(b_uniform));
 }
-#endif
 
 // Column terms issued up to 4 per asm statement: hipcc pads every inline-asm statement that
 // writes a VGPR with an s_nop before the next VALU reads it (it cannot see that the statement
@@ -69,11 +63,10 @@ KZ_DEV void mad29s(uint64_t& acc, uint32_t a, uint32_t b_uniform) {
 // early-clobber ("=&s": an "s" input read by a later instruction must not share it); the
 // accumulator is "+v" -- its register holds its own (64-bit, runtime) value on entry, so no
 // 32-bit input can share it (field.hpp mac32 note: the aliasing case is an accumulator whose
-// value equals an input).  KZ_MAD29_SINGLE: one mad per statement (A/B reference).
+// value equals an input).  (One mad per statement measured 1 % slower, profiles/HISTORY.md.)
 template <int K, int I, int CNT, int NX, int NY>
 KZ_DEV void vv_run(uint64_t& acc, const uint32_t (&x)[NX], const uint32_t (&y)[NY]) {
   uint64_t cc;
-#ifndef KZ_MAD29_SINGLE
   if constexpr (CNT >= 4) {
     asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n\tv_mad_u64_u32 %0, %1, %4, %5, %0\n\t"
         "v_mad_u64_u32 %0, %1, %6, %7, %0\n\tv_mad_u64_u32 %0, %1, %8, %9, %0"
@@ -93,19 +86,12 @@ KZ_DEV void vv_run(uint64_t& acc, const uint32_t (&x)[NX], const uint32_t (&y)[N
   } else if constexpr (CNT == 1) {
     mad29(acc, x[I], y[K - I]);
   }
-#else
-  if constexpr (CNT >= 1) {
-    mad29(acc, x[I], y[K - I]);
-    vv_run<K, I + 1, CNT - 1>(acc, x, y);
-  }
-#endif
   (void)cc;
 }
 // m_i MOD_{K-i}, i = I .. I+CNT-1 (MOD limbs: uniform, in SGPRs)
 template <class Q, int K, int I, int CNT>
 KZ_DEV void vs_run(uint64_t& acc, const uint32_t (&m)[Q::N]) {
   uint64_t cc;
-#ifndef KZ_MAD29_SINGLE
   if constexpr (CNT >= 4) {
     asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n\tv_mad_u64_u32 %0, %1, %4, %5, %0\n\t"
         "v_mad_u64_u32 %0, %1, %6, %7, %0\n\tv_mad_u64_u32 %0, %1, %8, %9, %0"
@@ -126,12 +112,6 @@ KZ_DEV void vs_run(uint64_t& acc, const uint32_t (&m)[Q::N]) {
   } else if constexpr (CNT == 1) {
     mad29s(acc, m[I], Q::MOD[K - I]);
   }
-#else
-  if constexpr (CNT >= 1) {
-    mad29s(acc, m[I], Q::MOD[K - I]);
-    vs_run<Q, K, I + 1, CNT - 1>(acc, m);
-  }
-#endif
   (void)cc;
 }
 

@@ -323,14 +323,54 @@ __global__ void k_encode_points(const Xyzz<Cv>* __restrict__ res, uint32_t count
   store_words(out + (size_t)i * 4 * NW, w);
 }
 
-// sum of partial records: out[k] = sum_j parts[j * stride + k] for k < nout
+// A shard partial record that failed on its own device (or rank) is marked, not dropped: its x
+// words are all ones (no Montgomery value < p has that top limb) and y.v[0] holds the device
+// error code.  Records the caller marks by filling every byte with 0xFF read as DERR_SHARD.
+// Every combine that reads the record then fails too, so no rank can accept a batch one of
+// whose shards was rejected (include/kzgmi.h, multi-GPU section).
+template <class Cv>
+KZ_DEV uint32_t partial_mark(const Xyzz<Cv>& p) {
+  if (p.x.v[Cv::FpP::N - 1] != 0xffffffffu) return DERR_NONE;
+  const uint32_t code = p.y.v[0];
+  return code >= DERR_ENCODING && code < DERR_SHARD ? code : DERR_SHARD;
+}
+
+// partial records out (count of them) = res, or marked records when *err != 0
+template <class Cv>
+__global__ void k_partial_out(const Xyzz<Cv>* __restrict__ res, uint32_t count, const uint32_t* __restrict__ err,
+                              Xyzz<Cv>* __restrict__ out) {
+  const uint32_t k = threadIdx.x;
+  if (k >= count) return;
+  const uint32_t e = *err;
+  Xyzz<Cv> p = load_xyzz(&res[k]);
+  if (e) {
+    using F = typename Xyzz<Cv>::F;
+    p.y = F::zero();
+    p.zz = F::zero();
+    p.zzz = F::zero();
+#pragma unroll
+    for (int i = 0; i < F::N; ++i) p.x.v[i] = 0xffffffffu;
+    p.y.v[0] = e;
+  }
+  store_xyzz(&out[k], p);
+}
+
+// sum of partial records: out[k] = sum_j parts[j * stride + k] for k < nout; a marked record
+// raises its error code into *err (and is left out of the sum)
 template <class Cv>
 __global__ void k_sum_partials(const Xyzz<Cv>* __restrict__ parts, uint32_t nparts, uint32_t stride,
-                               uint32_t nout, Xyzz<Cv>* __restrict__ out) {
+                               uint32_t nout, Xyzz<Cv>* __restrict__ out, uint32_t* __restrict__ err) {
   uint32_t k = threadIdx.x;
   if (k >= nout) return;
   Xyzz<Cv> acc = Xyzz<Cv>::inf();
-  for (uint32_t j = 0; j < nparts; ++j) acc = xyzz_add_c(acc, load_xyzz(&parts[j * stride + k]));
+  for (uint32_t j = 0; j < nparts; ++j) {
+    const Xyzz<Cv> p = load_xyzz(&parts[j * stride + k]);
+    if (const uint32_t m = partial_mark(p)) {
+      raise_err(err, m);
+      continue;
+    }
+    acc = xyzz_add_c(acc, p);
+  }
   store_xyzz(&out[k], acc);
 }
 

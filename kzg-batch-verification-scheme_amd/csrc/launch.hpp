@@ -18,14 +18,13 @@ struct Launch {
                    uint32_t* skey, int wbits = WBITS);
   // both curves accumulate in radix 2^29: pts in that format (convert_points(to29) or
   // pts_to29), acc29 = (nb + 2 x launched threads) records of W29 words that stay the bucket
-  // store (k_fixup joins pieces into them; reduce reads them); BN254 uses buckets/pfirst/plast
+  // store (k_fixup joins pieces into them; reduce reads them)
   static void accumulate(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* sval,
-                         const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts, XY* buckets,
-                         XY* pfirst, XY* plast, uint32_t* acc29, uint32_t nb, size_t acc_threads = 0,
-                         uint32_t* next_chunk = nullptr);
+                         const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts,
+                         uint32_t* acc29, uint32_t nb, size_t acc_threads = 0, uint32_t* next_chunk = nullptr);
   static void pts_to29(hipStream_t st, AF* pts, uint32_t n);  // in place
-  static void reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const XY* buckets, const uint32_t* acc29,
-                     XY* R, XY* U, XY* scratch, XY* winsum, int wbits = WBITS);
+  static void reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const uint32_t* acc29, XY* R, XY* U,
+                     XY* scratch, XY* winsum, int wbits = WBITS);
   static void window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res, int wbits = WBITS);
   // ---- I/O and scalars (launch_io.hip)
   // to29: store in the accumulation's radix-29 format, for
@@ -64,7 +63,11 @@ struct Launch {
                               const uint8_t* ys, uint32_t n, uint32_t* r_out, uint32_t* s_out, void* tpart,
                               uint32_t* negt, uint32_t* err);
   static void encode_points(hipStream_t st, const XY* res, uint32_t count, uint8_t* out);
-  static void sum_partials(hipStream_t st, const XY* parts, uint32_t nparts, uint32_t stride, uint32_t nout, XY* out);
+  // sum of gathered partial records; a record marked failed raises its code into *err
+  static void sum_partials(hipStream_t st, const XY* parts, uint32_t nparts, uint32_t stride, uint32_t nout, XY* out,
+                           uint32_t* err);
+  // count partial records out = res, marked failed (kernels.hpp partial_mark) when *err != 0
+  static void partial_out(hipStream_t st, const XY* res, uint32_t count, const uint32_t* err, XY* out);
   // ---- pairing (launch_pairing.hip)
   static int num_lines();
   static void precompute_lines(hipStream_t st, const G2Aff<Cv>* q, Line<Cv>* lines);

@@ -9,11 +9,9 @@ template <class Cv>
 void Launch<Cv>::convert_points(hipStream_t st, const uint8_t* bytes, uint32_t n, AF* pts, uint8_t* inf, uint32_t* err,
                                 bool to29, AF* img, uint8_t* img_inf) {
   if (!n) return;
-  if constexpr (kAcc29<Cv>) {
-    if (to29) {
-      k_convert_points<Cv, true><<<grid_for(n, 256), 256, 0, st>>>(bytes, n, pts, inf, err, img, img_inf);
-      return;
-    }
+  if (to29) {
+    k_convert_points<Cv, true><<<grid_for(n, 256), 256, 0, st>>>(bytes, n, pts, inf, err, img, img_inf);
+    return;
   }
   k_convert_points<Cv><<<grid_for(n, 256), 256, 0, st>>>(bytes, n, pts, inf, err);
 }
@@ -49,11 +47,9 @@ template <class Cv>
 void Launch<Cv>::endo_points(hipStream_t st, const AF* src, const uint8_t* src_inf, uint32_t n, AF* dst,
                              uint8_t* dst_inf, bool in29) {
   if (!n) return;
-  if constexpr (kAcc29<Cv>) {
-    if (in29) {
-      k_endo_points29<Cv><<<grid_for(n, 256), 256, 0, st>>>(src, src_inf, n, dst, dst_inf);
-      return;
-    }
+  if (in29) {
+    k_endo_points29<Cv><<<grid_for(n, 256), 256, 0, st>>>(src, src_inf, n, dst, dst_inf);
+    return;
   }
   k_endo_points<Cv><<<grid_for(n, 256), 256, 0, st>>>(src, src_inf, n, dst, dst_inf);
 }
@@ -127,8 +123,13 @@ void Launch<Cv>::encode_points(hipStream_t st, const XY* res, uint32_t count, ui
   k_encode_points<Cv><<<grid_for(count, 64), 64, 0, st>>>(res, count, out);
 }
 template <class Cv>
-void Launch<Cv>::sum_partials(hipStream_t st, const XY* parts, uint32_t nparts, uint32_t stride, uint32_t nout, XY* out) {
-  k_sum_partials<Cv><<<1, 64, 0, st>>>(parts, nparts, stride, nout, out);
+void Launch<Cv>::sum_partials(hipStream_t st, const XY* parts, uint32_t nparts, uint32_t stride, uint32_t nout, XY* out,
+                               uint32_t* err) {
+  k_sum_partials<Cv><<<1, 64, 0, st>>>(parts, nparts, stride, nout, out, err);
+}
+template <class Cv>
+void Launch<Cv>::partial_out(hipStream_t st, const XY* res, uint32_t count, const uint32_t* err, XY* out) {
+  k_partial_out<Cv><<<1, 64, 0, st>>>(res, count, err, out);
 }
 
 using C_ = KZ_CURVE_T;
@@ -154,6 +155,7 @@ template void Launch<C_>::scalar_prep_pow(hipStream_t, const void*, uint64_t, co
 template void Launch<C_>::encode_points(hipStream_t, const Xyzz<C_>*, uint32_t, uint8_t*);
 template void Launch<C_>::glv_split(hipStream_t, const uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t*);
 template void Launch<C_>::endo_points(hipStream_t, const Affine<C_>*, const uint8_t*, uint32_t, Affine<C_>*, uint8_t*, bool);
-template void Launch<C_>::sum_partials(hipStream_t, const Xyzz<C_>*, uint32_t, uint32_t, uint32_t, Xyzz<C_>*);
+template void Launch<C_>::sum_partials(hipStream_t, const Xyzz<C_>*, uint32_t, uint32_t, uint32_t, Xyzz<C_>*, uint32_t*);
+template void Launch<C_>::partial_out(hipStream_t, const Xyzz<C_>*, uint32_t, const uint32_t*, Xyzz<C_>*);
 
 }  // namespace kzgmi

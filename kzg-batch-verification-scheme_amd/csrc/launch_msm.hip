@@ -22,16 +22,7 @@ void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const 
     uint32_t* ccur = coarse + 2 * nbins;
     (void)hipMemsetAsync(ccnt, 0, (size_t)nbins * 4, st);
     const uint32_t tiles = num_tiles_host(tl);
-#ifdef KZ_SORT_SEPARATE_COUNT
-    if constexpr (WB == WBITS) {
-      if (tl.total) k_digits<<<grid_for(tl.total, 256), 256, 0, st>>>(tl, inf, digits);
-      if (tiles) k_bin_count<<<tiles, 256, 0, st>>>(tl, digits, ccnt);
-    } else {
-      if (tl.total) k_digits_count<WB><<<num_digit_groups_host(tl), 256, 0, st>>>(tl, inf, digits, ccnt);
-    }
-#else
     if (tl.total) k_digits_count<WB><<<num_digit_groups_host(tl), 256, 0, st>>>(tl, inf, digits, ccnt);
-#endif
     k_bin_scan<<<1, 1024, 0, st>>>(ccnt, nbins, coff, ccur, total);
     // coarse-pass entries (msm.hpp EntPacked / EntSplit): packed 4 B when every sorted value (point
     // index << 1 | sign) fits CV_BITS, else 4 B values + 1 B fine indices (ent holds emax x 8 B)
@@ -52,39 +43,35 @@ void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const 
 
 template <class Cv>
 void Launch<Cv>::accumulate(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* sval,
-                            const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts, XY* buckets,
-                            XY* pfirst, XY* plast, uint32_t* acc29, uint32_t nb, size_t acc_threads,
-                            uint32_t* next_chunk) {
+                            const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts,
+                            uint32_t* acc29, uint32_t nb, size_t acc_threads, uint32_t* next_chunk) {
   // nchunks threads (rounded up to whole 256-thread blocks); both kernels derive the chunk
   // length from the same grid -- except the radix-29 work-queue form: acc_threads (< nchunks,
   // whole blocks) threads take the nchunks chunks from the counter next_chunk, zeroed here
   const unsigned blocks = grid_for(nchunks, 256);
-  if (kAcc29<Cv> && next_chunk && acc_threads && acc_threads < nchunks) {
+  if (next_chunk && acc_threads && acc_threads < nchunks) {
     (void)hipMemsetAsync(next_chunk, 0, 4, st);
-    k_accumulate<Cv><<<grid_for(acc_threads, 256), 256, 0, st>>>(total, sval, skey, off, cnt, pts, buckets, pfirst,
-                                                                  plast, acc29, nb, (uint32_t)(blocks * 256u), next_chunk);
+    k_accumulate<Cv><<<grid_for(acc_threads, 256), 256, 0, st>>>(total, sval, skey, off, cnt, pts, acc29, nb,
+                                                                  (uint32_t)(blocks * 256u), next_chunk);
   } else {
-    k_accumulate<Cv><<<blocks, 256, 0, st>>>(total, sval, skey, off, cnt, pts, buckets, pfirst, plast, acc29, nb, 0u,
-                                             nullptr);
+    k_accumulate<Cv><<<blocks, 256, 0, st>>>(total, sval, skey, off, cnt, pts, acc29, nb, 0u, nullptr);
   }
-  if (kFixGroups) k_fixup_groups<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, pfirst, acc29, nb);
-  k_fixup<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, pfirst, plast, buckets, acc29, nb);
+  k_fixup_groups<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, acc29, nb);
+  k_fixup<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, acc29, nb);
 }
 
 template <class Cv>
 void Launch<Cv>::pts_to29(hipStream_t st, AF* pts, uint32_t n) {
-  if constexpr (kAcc29<Cv>) {
-    if (n) k_pts_to29<Cv><<<grid_for(n, 256), 256, 0, st>>>(pts, n);
-  }
+  if (n) k_pts_to29<Cv><<<grid_for(n, 256), 256, 0, st>>>(pts, n);
 }
 
 template <class Cv>
-void Launch<Cv>::reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const XY* buckets,
-                        const uint32_t* acc29, XY* R, XY* U, XY* scratch, XY* winsum, int wbits) {
+void Launch<Cv>::reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const uint32_t* acc29, XY* R, XY* U,
+                        XY* scratch, XY* winsum, int wbits) {
   with_wbits(wbits, [&](auto wb) {
     constexpr int WB = decltype(wb)::value;
     const uint32_t nseg = nsets * Win<WB>::NSEG;
-    k_reduce_segments<Cv><<<grid_for(2 * (size_t)nseg, 256), 256, 0, st>>>(nseg, cnt, buckets, acc29, R, U);  // 2 threads per segment
+    k_reduce_segments<Cv><<<grid_for(2 * (size_t)nseg, 256), 256, 0, st>>>(nseg, cnt, acc29, R, U);  // 2 threads per segment
     // scratch: nsets * RB_PARTS partial sums
     k_reduce_bits<Cv, WB><<<nsets * Win<WB>::RB_PARTS, 256, 0, st>>>(R, U, scratch);
     k_reduce_bits_finish<Cv, WB><<<nsets, 64, 0, st>>>(scratch, winsum);
@@ -102,13 +89,11 @@ void Launch<Cv>::window_combine(hipStream_t st, const MsmWindows& mw, const XY* 
 template void Launch<KZ_CURVE_T>::sort(hipStream_t, const TermList&, uint32_t, const uint8_t*, uint32_t*, uint32_t*,
                                        uint64_t*, size_t, bool, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
 template void Launch<KZ_CURVE_T>::accumulate(hipStream_t, size_t, const uint32_t*, const uint32_t*, const uint32_t*,
-                                             const uint32_t*, const uint32_t*, const Affine<KZ_CURVE_T>*,
-                                             Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, uint32_t*,
+                                             const uint32_t*, const uint32_t*, const Affine<KZ_CURVE_T>*, uint32_t*,
                                              uint32_t, size_t, uint32_t*);
 template void Launch<KZ_CURVE_T>::pts_to29(hipStream_t, Affine<KZ_CURVE_T>*, uint32_t);
-template void Launch<KZ_CURVE_T>::reduce(hipStream_t, uint32_t, const uint32_t*, const Xyzz<KZ_CURVE_T>*,
-                                         const uint32_t*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*,
-                                         int);
+template void Launch<KZ_CURVE_T>::reduce(hipStream_t, uint32_t, const uint32_t*, const uint32_t*, Xyzz<KZ_CURVE_T>*,
+                                         Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, int);
 template void Launch<KZ_CURVE_T>::window_combine(hipStream_t, const MsmWindows&, const Xyzz<KZ_CURVE_T>*,
                                                  Xyzz<KZ_CURVE_T>*, int);
 

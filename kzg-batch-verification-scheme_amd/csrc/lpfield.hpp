@@ -42,25 +42,13 @@ KZ_DEV int32_t lp_prev(int32_t x) { return __builtin_amdgcn_update_dpp(0, x, 0x1
 
 // acc += a b, signed 32 x 32 -> 64: one v_mad_i64_i32.  ROCm 7.2's hipcc selects it from the C++
 // form for gfx950 (earlier compilers lowered it to two unsigned mads plus sign fix-ups, hence the
-// inline asm of rounds 1-2, KZ_LP_ASM_MADS); the C++ form also spares the s_nop hipcc pads after
+// inline asm of rounds 1-2); the C++ form also spares the s_nop hipcc pads after
 // every VGPR-writing asm statement -- 14 per lane-parallel product (lp_mul_iter).
-#ifdef KZ_LP_ASM_MADS
-KZ_DEV void lp_mad_i64(int64_t& acc, int32_t a, int32_t b) {
-  uint64_t cc;
-  asm("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
-}
-// acc += a b for 0 <= a, b < 2^31 (two's complement acc: the unsigned sum wraps correctly)
-KZ_DEV void lp_mad_u64(int64_t& acc, int32_t a, int32_t b) {
-  uint64_t cc;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
-}
-#else
 KZ_DEV void lp_mad_i64(int64_t& acc, int32_t a, int32_t b) { acc += (int64_t)a * (int64_t)b; }
 // acc += a b for 0 <= a, b < 2^31 (two's complement acc: the unsigned sum wraps correctly)
 KZ_DEV void lp_mad_u64(int64_t& acc, int32_t a, int32_t b) {
   acc = (int64_t)((uint64_t)acc + (uint64_t)(uint32_t)a * (uint64_t)(uint32_t)b);
 }
-#endif
 
 // per-lane constants of a lane-parallel kernel (lane j = threadIdx.x % 16 of row threadIdx.x / 16 % 4)
 template <class Cv>

@@ -1,7 +1,7 @@
 // G1 Pippenger MSM kernels for gfx950 (hot-path rows a5/a6 of SURVEY.md 8a).
 //
 // Pipeline (all on one HIP stream; no host synchronisation inside):
-//   k_bin_count .. k_fine_sort  signed 16-bit window digits of every term, grouped by
+//   k_digits_count .. k_fine_sort  signed 16-bit window digits of every term, grouped by
 //                     bucket with a two-pass LDS-privatised MSD partition (see "sort")
 //   k_accumulate      load-balanced bucket accumulation: every thread owns exactly
 //                     ACC_CHUNK consecutive sorted entries (not a bucket), so Poisson bucket
@@ -60,10 +60,11 @@ struct TermList {
 // ------------------------------------------------------------------------------ sort
 // Entries (one per nonzero signed window digit) are grouped by global bucket id
 // key = set * 2^15 + (|d| - 1) with a two-pass MSD partition that keeps the atomics in LDS:
-//   k_bin_count   tile = (class, window, 4096 terms): LDS histogram over the window's 256
-//                 coarse bins (key >> 7), then one global atomic per non-empty bin
+//   k_digits_count every signed digit of every term, once, counted per (class, 4096 terms) into
+//                 LDS histograms of each window's 256 coarse bins (key >> 7), then one global
+//                 atomic per non-empty (window, bin)
 //   k_bin_scan    exclusive scan of the nsets*256 coarse counts (+ total entries)
-//   k_bin_scatter same digits; LDS ranks, one global atomic per bin reserves the tile's run,
+//   k_bin_scatter the stored digits; LDS ranks, one global atomic per bin reserves the tile's run,
 //                 entries (fine index, value: EntPacked / EntSplit) written into their coarse bin
 //   k_fine_sort   one workgroup per coarse bin (128 buckets): LDS counting sort, writes the
 //                 sorted (value, key) arrays and every bucket's offset/count; the value of
@@ -75,11 +76,6 @@ constexpr int COARSE_SHIFT = 7;
 constexpr int FINE = 1 << COARSE_SHIFT;                 // buckets per coarse bin
 constexpr int BINS_PER_SET = NBUCKETS >> COARSE_SHIFT;  // 256
 constexpr int TILE_TERMS = 4096;                        // terms per tile (16 per thread)
-#ifndef KZ_REDUCE_R8U  // (k_reduce_segments: V records, see there)
-constexpr bool kSegV = true;
-#else  // A/B reference: R_g = R_0 + (R_1 + 8 U_1) per segment, no V records
-constexpr bool kSegV = false;
-#endif
 // Window width c of a call (WBITS, NBUCKETS, BINS_PER_SET above are c = 16's): large calls use
 // c = 16; small ones (few entries per bucket) c = 13 -- 8x fewer buckets to reduce for 5/4 the
 // terms (api.hip call_wbits).  The sort, the window-sum reduction and the combination are
@@ -92,7 +88,7 @@ struct Win {
   static constexpr int NSEG = NBUCKETS / SEG;            // reduction segments per set
   static constexpr int SEG_BITS = C - 1 - 4;             // log2(NSEG)
   static constexpr int MAXW = 256 / C + 1;               // windows of a 256-bit scalar (+ carry)
-  static constexpr int RB_PARTS = SEG_BITS + (kSegV ? 6 : 4);  // k_reduce_bits parts per set
+  static constexpr int RB_PARTS = SEG_BITS + 6;         // k_reduce_bits parts per set
   static_assert(NSEG == (1 << SEG_BITS) && BINS <= 256 && BINS >= 1, "window width");
 };
 // sorted value = point index << 1 | sign, | SV_FIRST on the first entry of each bucket (point
@@ -194,26 +190,10 @@ KZ_DEV void term_digits(const TermClass& C, uint32_t i, const uint8_t* __restric
   }
 }
 
-// All signed digits of every term, once: one thread per term (the count and scatter passes used
-// to recompute the chain from the scalar for every window: nwin scalar reads per term per pass).
-// A/B reference of k_digits_count (KZ_SORT_SEPARATE_COUNT).
-static __global__ void __launch_bounds__(256) k_digits(TermList tl, const uint8_t* __restrict__ inf,
-                                                uint32_t* __restrict__ digits) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  int k = 0;
-  for (; k < (int)tl.nclass; ++k) {
-    if (i < tl.c[k].count) break;
-    i -= tl.c[k].count;
-  }
-  if (k >= (int)tl.nclass) return;
-  const TermClass& C = tl.c[k];
-  term_digits<WBITS>(C, i, inf, [&](int w, uint32_t code) { digits[C.dig_base + (size_t)w * C.count + i] = code; });
-}
-
-// k_digits and k_bin_count in one pass: workgroup = 4096 terms of one class (16 per thread),
-// every window's digits written as in k_digits and counted into an LDS histogram per window,
-// then one global atomic per non-empty (window, coarse bin) -- the same atomics as k_bin_count's
-// tiles, without its second read of the digit array (KZ_SORT_SEPARATE_COUNT: the two kernels).
+// Every signed digit of every term, once, and the coarse counts, in one pass: workgroup = 4096
+// terms of one class (16 per thread), every window's digits written (digit w of term i at
+// dig_base + w * count + i) and counted into an LDS histogram per window, then one global atomic
+// per non-empty (window, coarse bin); the scatter pass reads the digits back.
 inline uint32_t num_digit_groups_host(const TermList& tl) {
   uint32_t g = 0;
   for (uint32_t k = 0; k < tl.nclass; ++k) g += (tl.c[k].count + TILE_TERMS - 1) / TILE_TERMS;
@@ -254,25 +234,6 @@ __global__ void __launch_bounds__(256) k_digits_count(TermList tl, const uint8_t
     const uint32_t h = hist[w][t];
     if (h) atomicAdd(&coarse_cnt[(C.set_base + w) * W::BINS + t], h);
   }
-}
-
-static __global__ void __launch_bounds__(256) k_bin_count(TermList tl, const uint32_t* __restrict__ digits,
-                                                   uint32_t* __restrict__ coarse_cnt) {
-  __shared__ uint32_t hist[BINS_PER_SET];
-  const TileRef T = tile_decode(tl, blockIdx.x);
-  const TermClass& C = tl.c[T.k];
-  const uint32_t* dg = digits + C.dig_base + (size_t)T.w * C.count;
-  hist[threadIdx.x] = 0;
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < TILE_TERMS / 256; ++j) {
-    const uint32_t local = T.c * TILE_TERMS + j * 256 + threadIdx.x;
-    const uint32_t code = local < C.count ? dg[local] : 0u;
-    if (code) atomicAdd(&hist[((code & 0x7fffffffu) - 1) >> COARSE_SHIFT], 1u);
-  }
-  __syncthreads();
-  uint32_t h = hist[threadIdx.x];
-  if (h) atomicAdd(&coarse_cnt[(C.set_base + T.w) * BINS_PER_SET + threadIdx.x], h);
 }
 
 // single block: exclusive scan of nbins (<= 8192) coarse counts; cursor copy; total
@@ -380,7 +341,7 @@ __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t
 // the 2^24-point MSM: ~65 K) go through the same staging array a chunk of FINE_STAGE / 2 entries
 // at a time: the chunk is counting-sorted in LDS (the histogram atomics return the ranks), and each
 // bucket's run of the chunk is written at that bucket's running cursor -- runs of ~32 entries
-// instead of one scattered 4-byte store pair per entry (KZ_FINE_UNSTAGED: the direct stores).
+// instead of one scattered 4-byte store pair per entry.
 constexpr int FINE_ILP = 4;
 constexpr int FINE_STAGE = 8192;
 
@@ -490,14 +451,12 @@ __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ 
     cnt[key] = tot;
   }
   __syncthreads();
-#ifndef KZ_FINE_UNSTAGED
   if (!staged) {
     if (t < FINE) scan[t] -= fine[t];  // bucket starts (exclusive scan); cursor[] is a copy
     __syncthreads();
     fine_sort_chunks(g, start, count, tmp, scan, cursor, stage, sorted_val, sorted_key);
     return;
   }
-#endif
   for (uint32_t e0 = t; e0 < count; e0 += 256 * FINE_ILP) {
     using R = typename E::R;
     R v[FINE_ILP];
@@ -512,15 +471,9 @@ __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ 
       const uint32_t f = E::fine(v[j]);
       const uint32_t p = atomicAdd(&cursor[f], 1u);
       const uint32_t first = p == scan[f] - fine[f] ? SV_FIRST : 0u;
-      if (staged) {
-        stage[p] = E::val(v[j]) | first;
-      } else {
-        sorted_val[start + p] = E::val(v[j]) | first;
-        sorted_key[start + p] = g * FINE + f;
-      }
+      stage[p] = E::val(v[j]) | first;
     }
   }
-  if (!staged) return;
   __syncthreads();
   for (uint32_t p = t; p < count; p += 256) {
     uint32_t b = 0;  // smallest b with scan[b] > p
@@ -607,19 +560,6 @@ KZ_DEV uint32_t acc_chunk_len(uint32_t total, uint32_t nthreads) {
   return per > 4u ? per : 4u;
 }
 
-template <class Cv>
-KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_t start, uint32_t len,
-                      const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt,
-                      Xyzz<Cv>* __restrict__ buckets, Xyzz<Cv>* __restrict__ part_first,
-                      Xyzz<Cv>* __restrict__ part_last, bool inf = false) {
-  uint32_t o = off[key];
-  bool started_before = o < start;
-  bool ends_after = o + cnt[key] > start + len;
-  Xyzz<Cv>* dst = started_before ? &part_first[chunk] : ends_after ? &part_last[chunk] : &buckets[key];
-  // the loop keeps coordinates lazily reduced (< 2p)
-  store_xyzz(dst, inf ? Xyzz<Cv>::inf() : xyzz_canon(acc));
-}
-
 // ---- radix-2^29 accumulation (BLS12-381; field29.hpp) ------------------------------------
 // Points arrive in radix-29 form (x in words 0..13, y in 14..27 of each 128-B slot), written so
 // by k_convert_points<To29> or converted in place by k_pts_to29.  Finished buckets and bucket
@@ -629,16 +569,6 @@ KZ_DEV void acc_flush(const Xyzz<Cv>& acc, uint32_t key, uint32_t chunk, uint32_
 // addition (x29_add below), writing R/U as records too; k_reduce_bits converts to 32-bit limbs
 // as it reads them.  No conversion at the flushes: some lane of a wavefront changes bucket in
 // almost every step, so per-flush work runs on most iterations.
-#if defined(KZ_NO_ACC29)  // A/B reference: the 32-bit-limb loop for both curves
-template <class Cv>
-constexpr bool kAcc29 = false;
-#elif defined(KZ_NO_ACC29_BN254)  // A/B reference: BN254 on the 32-bit-limb loop
-template <class Cv>
-constexpr bool kAcc29 = Cv::ID == 0;
-#else
-template <class Cv>
-constexpr bool kAcc29 = true;
-#endif
 // words of a radix-29 XYZZ record: BLS12-381 56 (224 B), BN254 36 (144 B)
 template <class Q>
 constexpr int kW29 = 4 * Q::N;
@@ -948,29 +878,12 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
   uint32_t e = start;
   for (;;) {
     bool dbl = false;
-#ifdef KZ_ACC_KEYSTREAM  // A/B reference: keys and values streamed per entry
-    // entry e + 1's key and value are loaded one iteration ahead: the loop's memory chain is
-    // then the point gather alone instead of key -> value -> point
-    uint32_t key_n = e < end ? sorted_key[e] : 0u, val_n = e < end ? sorted_val[e] : 0u;
-    for (; e < end; ++e) {
-      const uint32_t key = key_n, v = val_n;
-      if (e + 1 < end) {
-        key_n = sorted_key[e + 1];
-        val_n = sorted_val[e + 1];
-      }
-      if (key != cur) {
-        flush(x, y, cur, inf, false);
-        inf = true;
-        cur = key;
-      }
-#else
     // The values stream 4 at a time (one 16-B load per 4 entries, issued an iteration ahead of
     // their use; chunks start 16-B aligned, acc_chunk_len): each lane walks its own run, so a
     // per-entry 4-B load re-fetched the run's sector from beyond L2 for most entries.  A bucket
     // change is the SV_FIRST bit of the value; the key is read only then (a flush).
-#ifndef KZ_ACC_VQ_REGS  // (A/B reference: the 4 values in registers, spilled to scratch and back
-    // around the addition at 128 VGPRs: 177.1 vs 179.4 batch-verifies/s, profiles/r04/ab_acc_vq_lds.txt)
-    // The 4 values of a group land in LDS by an asynchronous global_load_lds_dwordx4, one group
+    // (The 4 values in registers were spilled to scratch and back around the addition at 128
+    // VGPRs: 177.1 vs 179.4 batch-verifies/s, profiles/r04/ab_acc_vq_lds.txt.)  The 4 values of a group land in LDS by an asynchronous global_load_lds_dwordx4, one group
     // ahead; no VGPR holds them across the addition.  With the lane slot from v_mbcnt and ONE
     // from literals (below) the loop has no scratch traffic at all and needs 123 VGPRs (180.4 vs
     // 179.4/s, profiles/r04/ab_acc_spill_free.txt).
@@ -988,19 +901,11 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): v is read before the next group lands over it
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(sorted_val + e + 1), vq_wave, 16, 0, 0);
       }
-#else
-    uint4 vq = *reinterpret_cast<const uint4*>(sorted_val + (e & ~3u));  // may read 3 past total: padded
-    for (; e < end; ++e) {
-      const uint32_t j = e & 3u;  // wave-uniform (every lane's chunk starts at a multiple of 4)
-      const uint32_t v = j == 0 ? vq.x : j == 1 ? vq.y : j == 2 ? vq.z : vq.w;
-      if (j == 3) vq = *reinterpret_cast<const uint4*>(sorted_val + e + 1);
-#endif
       if ((v & SV_FIRST) && e != start) {
         flush(x, y, cur, inf, false);
         inf = true;
         cur = sorted_key[e];
       }
-#endif
       G qx, qy;
       load_q(v, qx, qy);
       if (inf) {
@@ -1031,14 +936,9 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
       st(s_zz, mul29(ld(s_zz), PP));
       st(s_zzz, mul29(ld(s_zzz), PPP));
       const G Q2 = mul29(x, PP);
-#ifdef KZ_ACC_CARRY_PASSES  // A/B reference: X3 in two carry passes, -PPP normalised
-      const G X3 = sub29(sqr29(R), add3_29(PPP, Q2, Q2), Q::ACC_X3_B);  // BLS12-381 < 10p
-      y = mul2_29(R, sub29(Q2, X3, Q::ACC_QX), y, sub29(G::zero(), PPP, Q::ACC_PPP));  // R (Q - X3) - Y1 PPP
-#else
       const G X3 = sub3_29(sqr29(R), PPP, Q2, Q::ACC_X3);  // one carry pass; BLS12-381 < 10p
       // R (Q - X3) - Y1 PPP, with -PPP as ACC_PPP - PPP limb by limb (no carry pass; neg_lazy29)
       y = mul2_29(R, sub29(Q2, X3, Q::ACC_QX), y, neg_lazy29(PPP, Q::ACC_PPP));
-#endif
       x = X3;
     }
     if (!dbl) break;
@@ -1056,9 +956,8 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
 
 // Waves per SIMD the accumulation is compiled for (VGPR budget 512 / waves per lane); the host
 // caps the grid at one resident round of CUs x 4 SIMDs x kAccWaves waves (api.hip).
-// 32-bit limbs (BN254): ZZ/ZZZ staged in LDS make 4 waves fit (128 VGPRs; the all-register
-// loop needed 168: 7.53 vs 7.28 ms, profiles/r01/acc_lds_ab.txt).  Radix 2^29 (BLS12-381):
-// 4 waves at 128 VGPRs once the rare doubling left the hot loop (7 VGPRs spilled outside it);
+// ZZ/ZZZ staged in LDS make 4 waves fit (the all-register 32-bit loop of round 1 needed 168
+// VGPRs: 7.53 vs 7.28 ms, profiles/r01/acc_lds_ab.txt); radix 2^29: 4 waves at 128 VGPRs once the rare doubling left the hot loop (7 VGPRs spilled outside it);
 // 3 waves / 167 VGPRs measured 6.94 vs 6.63 ms (profiles/r01/acc29_ab.txt).
 #ifndef KZ_ACC29_WAVES
 #define KZ_ACC29_WAVES 4
@@ -1067,7 +966,7 @@ KZ_DEV void acc_loop29(uint32_t start, uint32_t end, uint32_t total, uint32_t ch
 #define KZ_ACC29_WAVES_BN KZ_ACC29_WAVES
 #endif
 template <class Cv>
-constexpr int kAccWaves = kAcc29<Cv> ? (Cv::ID == 1 ? KZ_ACC29_WAVES_BN : KZ_ACC29_WAVES) : 4;
+constexpr int kAccWaves = Cv::ID == 1 ? KZ_ACC29_WAVES_BN : KZ_ACC29_WAVES;
 
 template <class Cv>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWaves<Cv>))) k_accumulate(const uint32_t* __restrict__ total_p,
@@ -1076,13 +975,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
                                                     const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ cnt,
                                                     const Affine<Cv>* __restrict__ pts,
-                                                    Xyzz<Cv>* __restrict__ buckets,
-                                                    Xyzz<Cv>* __restrict__ part_first,
-                                                    Xyzz<Cv>* __restrict__ part_last,
                                                     uint32_t* __restrict__ acc29, uint32_t nb,
                                                     uint32_t nchunks, uint32_t* __restrict__ next_chunk) {
   const uint32_t total = *total_p;
-  if constexpr (kAcc29<Cv>) {
+  {
     if (next_chunk) {
       // Work queue (large calls, Launch::accumulate): nchunks chunks, more than the launched
       // threads; every wavefront takes the next 64 consecutive chunks (one per lane, the same
@@ -1111,83 +1007,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
   const uint32_t start = chunk * len;
   if (start >= total) return;
   const uint32_t end = min(start + len, total);
-  uint32_t cur = sorted_key[start];
-  if constexpr (kAcc29<Cv>) {
-    acc_loop29<Cv>(start, end, total, chunk, cur, sorted_val, sorted_key,
-                   reinterpret_cast<const uint32_t*>(pts), acc29, nb, gridDim.x * blockDim.x);
-  } else {  // A/B reference (KZ_NO_ACC29*): 32-bit limbs
-  // ZZ and ZZZ of the running bucket sum live in LDS (word-major per thread: conflict-free
-  // 32-bit accesses), X and Y in registers.  ZZ/ZZZ are read only at the start (U2, S2) and the
-  // end (ZZ3, ZZZ3) of an addition, so taking them out of the register file keeps the loop
-  // within 128 VGPRs: 4 waves per SIMD instead of 3.  The empty asm with a memory clobber in
-  // every access keeps them real LDS accesses (no forwarding of a stored value through
-  // registers across iterations).
-  using F = Fp<typename Cv::FpP>;
-  constexpr int N = Cv::FpP::N;
-  __shared__ uint32_t s_zz[N][256], s_zzz[N][256];
-  const uint32_t tx = threadIdx.x;
-  auto ld = [tx](uint32_t (&a)[N][256]) {
-    asm volatile("" ::: "memory");
-    F r;
-    _Pragma("unroll") for (int k = 0; k < N; ++k) r.v[k] = a[k][tx];
-    return r;
-  };
-  auto st = [tx](uint32_t (&a)[N][256], const F& v) {
-    _Pragma("unroll") for (int k = 0; k < N; ++k) a[k][tx] = v.v[k];
-    asm volatile("" ::: "memory");
-  };
-#define zzp s_zz
-#define zzzp s_zzz
-  F x, y;
-  bool inf = true;
-  for (uint32_t e = start; e < end; ++e) {
-    uint32_t key = sorted_key[e];
-    if (key != cur) {
-      acc_flush(Xyzz<Cv>{x, y, ld(zzp), ld(zzzp)}, cur, chunk, start, len, off, cnt, buckets, part_first, part_last,
-                inf);
-      inf = true;
-      cur = key;
-    }
-    uint32_t v = sorted_val[e];
-    Affine<Cv> q = load_affine(pts, sv_point(v));
-    q.y = fp_select((v & 1) != 0, fp_rsub_mod(q.y), q.y);  // -y as p - y (see below)
-    if (inf) {
-      x = q.x;
-      y = q.y;
-      st(zzp, F::one());
-      st(zzzp, F::one());
-      inf = false;
-      continue;
-    }
-    const F U2 = fp_mul_lazy(q.x, ld(zzp));
-    const F S2 = fp_mul_lazy(q.y, ld(zzzp));
-    const F P = fp_sub_lazy(U2, x);
-    const F R = fp_sub_lazy(S2, y);
-    if (fp_is_zero_lazy(P)) {
-      if (fp_is_zero_lazy(R)) {
-        const Xyzz<Cv> d = xyzz_dbl_affine(Affine<Cv>{fp_canon(q.x), fp_canon(q.y)});
-        x = d.x;
-        y = d.y;
-        st(zzp, d.zz);
-        st(zzzp, d.zzz);
-      } else {
-        inf = true;
-      }
-      continue;
-    }
-    const F PP = fp_mul_lazy(P, P);
-    const F PPP = fp_mul_lazy(P, PP);
-    st(zzp, fp_mul_lazy(ld(zzp), PP));
-    st(zzzp, fp_mul_lazy(ld(zzzp), PPP));
-    const F Q = fp_mul_lazy(x, PP);
-    const F X3 = fp_sub_lazy(fp_sub_lazy(fp_mul_lazy(R, R), PPP), fp_add_lazy(Q, Q));
-    y = fp_mul2_lazy(R, fp_sub_lazy(Q, X3), y, fp_neg_lazy(PPP));  // R (Q - X3) - Y1 PPP
-    x = X3;
-  }
-  acc_flush(Xyzz<Cv>{x, y, ld(zzp), ld(zzzp)}, cur, chunk, start, len, off, cnt, buckets, part_first, part_last, inf);
-#undef zzp
-#undef zzzp
-  }
+  acc_loop29<Cv>(start, end, total, chunk, sorted_key[start], sorted_val, sorted_key,
+                 reinterpret_cast<const uint32_t*>(pts), acc29, nb, gridDim.x * blockDim.x);
 }
 
 // A bucket cut into k + 1 pieces (its last piece in chunk c0, first pieces of chunks c0+1..c1,
@@ -1196,11 +1017,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
 // bits in the top one: 2^17 terms in ~116 buckets, k ~ 18), so for k > 3 the join is two-level:
 // k_fixup_groups sums groups of G = ceil(sqrt k) consecutive first pieces into the group's first
 // slot, k_fixup adds the ceil(k / G) group sums -- G - 1 + ceil(k / G) dependent additions.
-#if defined(KZ_NO_FIX_GROUPS)  // A/B reference: one serial chain per bucket
-constexpr bool kFixGroups = false;
-#else
-constexpr bool kFixGroups = true;
-#endif
 KZ_DEV uint32_t fix_group(uint32_t k) {
   if (k <= 3) return 1;
   uint32_t g = (uint32_t)sqrtf((float)k);
@@ -1229,8 +1045,7 @@ __global__ void __launch_bounds__(256) k_fixup_groups(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ sorted_key,
                                                       const uint32_t* __restrict__ off,
                                                       const uint32_t* __restrict__ cnt,
-                                                      Xyzz<Cv>* __restrict__ part_first, uint32_t* __restrict__ acc29,
-                                                      uint32_t nb) {
+                                                      uint32_t* __restrict__ acc29, uint32_t nb) {
   KZ_TAIL_PRIO();
   const uint32_t total = *total_p;
   const uint32_t len = acc_chunk_len(total, gridDim.x * blockDim.x);
@@ -1240,31 +1055,22 @@ __global__ void __launch_bounds__(256) k_fixup_groups(const uint32_t* __restrict
   const uint32_t g = fix_group(c1 - c0);
   if (g == 1 || (c - c0 - 1) % g) return;
   const uint32_t last = c + g - 1 < c1 ? c + g - 1 : c1;
-  if constexpr (kAcc29<Cv>) {
-    using Q = Fp29Of<Cv>;
-    X29<Q> acc = load_x29<Q>(acc29, nb + c);
-    for (uint32_t cc = c + 1; cc <= last; ++cc) acc = x29_add<Cv, Q>(acc, load_x29<Q>(acc29, nb + cc));
-    store_x29<Q>(acc29, nb + c, acc);
-  } else {
-    Xyzz<Cv> acc = load_xyzz(&part_first[c]);
-    for (uint32_t cc = c + 1; cc <= last; ++cc) acc = xyzz_add(acc, load_xyzz(&part_first[cc]));
-    store_xyzz(&part_first[c], acc);
-  }
+  using Q = Fp29Of<Cv>;
+  X29<Q> acc = load_x29<Q>(acc29, nb + c);
+  for (uint32_t cc = c + 1; cc <= last; ++cc) acc = x29_add<Cv, Q>(acc, load_x29<Q>(acc29, nb + cc));
+  store_x29<Q>(acc29, nb + c, acc);
 }
 
 // joins the pieces of buckets that cross chunk boundaries (launched with the same grid as
 // k_accumulate, so acc_chunk_len agrees), after k_fixup_groups
-// BLS12-381 (kAcc29): the pieces and the bucket are radix-29 records of acc29 = [nb buckets |
+// The pieces and the bucket are radix-29 records of acc29 = [nb buckets |
 // nthreads first pieces | nthreads last pieces], joined with the radix-29 XYZZ addition and
 // written back as the record k_reduce_segments reads.
 template <class Cv>
 __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ total_p,
                                                const uint32_t* __restrict__ sorted_key,
                                                const uint32_t* __restrict__ off,
-                                               const uint32_t* __restrict__ cnt,
-                                               const Xyzz<Cv>* __restrict__ part_first,
-                                               const Xyzz<Cv>* __restrict__ part_last,
-                                               Xyzz<Cv>* __restrict__ buckets, uint32_t* __restrict__ acc29,
+                                               const uint32_t* __restrict__ cnt, uint32_t* __restrict__ acc29,
                                                uint32_t nb) {
   KZ_TAIL_PRIO();
   const uint32_t total = *total_p;
@@ -1273,18 +1079,12 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
   uint32_t key, c0, c1;
   if (!fix_range(c, len, total, sorted_key, off, cnt, key, c0, c1)) return;
   if (c0 != c - 1) return;                // a later continuation chunk: handled by c0+1
-  const uint32_t g = kFixGroups ? fix_group(c1 - c0) : 1;  // group sums at c, c + g, ...
-  if constexpr (kAcc29<Cv>) {
-    const size_t nthreads = (size_t)gridDim.x * blockDim.x;
-    using Q = Fp29Of<Cv>;
-    X29<Q> acc = load_x29<Q>(acc29, nb + nthreads + c0);
-    for (uint32_t cc = c; cc <= c1; cc += g) acc = x29_add<Cv, Q>(acc, load_x29<Q>(acc29, nb + cc));
-    store_x29<Q>(acc29, key, acc);
-  } else {
-    Xyzz<Cv> acc = load_xyzz(&part_last[c0]);
-    for (uint32_t cc = c; cc <= c1; cc += g) acc = xyzz_add(acc, load_xyzz(&part_first[cc]));
-    store_xyzz(&buckets[key], acc);
-  }
+  const uint32_t g = fix_group(c1 - c0);  // group sums at c, c + g, ...
+  const size_t nthreads = (size_t)gridDim.x * blockDim.x;
+  using Q = Fp29Of<Cv>;
+  X29<Q> acc = load_x29<Q>(acc29, nb + nthreads + c0);
+  for (uint32_t cc = c; cc <= c1; cc += g) acc = x29_add<Cv, Q>(acc, load_x29<Q>(acc29, nb + cc));
+  store_x29<Q>(acc29, key, acc);
 }
 
 // ------------------------------------------------------------------------------ reduction
@@ -1298,72 +1098,32 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
 // wave instead of ~16; the kernel is latency-bound at 1.5 waves per SIMD.)
 template <class Cv>
 __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const uint32_t* __restrict__ cnt,
-                                                         const Xyzz<Cv>* __restrict__ buckets,
                                                          const uint32_t* __restrict__ acc29,
                                                          Xyzz<Cv>* __restrict__ R, Xyzz<Cv>* __restrict__ U) {
   static_assert(SEG == 16, "two 8-bucket halves per segment");
   KZ_TAIL_PRIO();
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t g = t >> 1, h = t & 1;
-  if constexpr (kAcc29<Cv>) {  // BLS12-381: radix 2^29 on the records; R, U written as records
-    using Q = Fp29Of<Cv>;
-    const X29<Q> O{F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), true};
-    X29<Q> run = O, acc = O;
-    if (g < nseg) {
-      const uint32_t base = g * SEG + 8 * h;
-      for (int i = 7; i >= 1; --i) {
-        if (cnt[base + i]) run = x29_add<Cv, Q>(run, load_x29<Q>(acc29, base + i));
-        acc = x29_add<Cv, Q>(acc, run);
-      }
-      if (cnt[base]) run = x29_add<Cv, Q>(run, load_x29<Q>(acc29, base));
-      if (!kSegV && h == 1) acc = x29_add<Cv, Q>(acc, x29_dbl<Q>(x29_dbl<Q>(x29_dbl<Q>(run))));  // R_1 + 8 U_1
+  using Q = Fp29Of<Cv>;  // radix 2^29 on the records; R, U written as records
+  const X29<Q> O{F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), true};
+  X29<Q> run = O, acc = O;
+  if (g < nseg) {
+    const uint32_t base = g * SEG + 8 * h;
+    for (int i = 7; i >= 1; --i) {
+      if (cnt[base + i]) run = x29_add<Cv, Q>(run, load_x29<Q>(acc29, base + i));
+      acc = x29_add<Cv, Q>(acc, run);
     }
-    // h = 0 needs the partner's R_1, h = 1 the partner's U_0 (adjacent lanes, whole wave)
-    const X29<Q> other = x29_swap_pair<Q>(h ? acc : run);
-    if (g >= nseg) return;
-    if (h == 0) {
-      store_x29<Q>(reinterpret_cast<uint32_t*>(R), g, x29_add<Cv, Q>(acc, other));
-    } else {
-      store_x29<Q>(reinterpret_cast<uint32_t*>(U), g, x29_add<Cv, Q>(run, other));
-      if (kSegV) store_x29<Q>(reinterpret_cast<uint32_t*>(U), (size_t)nseg + g, run);  // V_g = U_1
-    }
+    if (cnt[base]) run = x29_add<Cv, Q>(run, load_x29<Q>(acc29, base));
+  }
+  // h = 0 needs the partner's R_1, h = 1 the partner's U_0 (adjacent lanes, whole wave)
+  const X29<Q> other = x29_swap_pair<Q>(h ? acc : run);
+  if (g >= nseg) return;
+  if (h == 0) {
+    store_x29<Q>(reinterpret_cast<uint32_t*>(R), g, x29_add<Cv, Q>(acc, other));
   } else {
-    __shared__ __attribute__((aligned(16))) Xyzz<Cv> xch[256];
-    Xyzz<Cv> run = Xyzz<Cv>::inf(), acc = Xyzz<Cv>::inf();
-    if (g < nseg) {
-      const uint32_t base = g * SEG + 8 * h;
-      for (int i = 7; i >= 1; --i) {  // inline additions: no call frames in scratch
-        if (cnt[base + i]) run = xyzz_add(run, load_xyzz(&buckets[base + i]));
-        acc = xyzz_add(acc, run);
-      }
-      if (cnt[base]) run = xyzz_add(run, load_xyzz(&buckets[base]));
-      if (!kSegV && h == 1) acc = xyzz_add(acc, xyzz_dbl(xyzz_dbl(xyzz_dbl(run))));  // R_1 + 8 U_1
-    }
-    // h = 0 needs the partner's R_1 + 8 U_1, h = 1 the partner's U_0
-    store_xyzz(&xch[threadIdx.x], h ? acc : run);
-    __syncthreads();
-    if (g >= nseg) return;
-    const Xyzz<Cv> other = load_xyzz(&xch[threadIdx.x ^ 1]);
-    if (h == 0) {
-      store_xyzz(&R[g], xyzz_add(acc, other));
-    } else {
-      store_xyzz(&U[g], xyzz_add(run, other));
-      if (kSegV) store_xyzz(&U[nseg + g], run);  // V_g = U_1
-    }
+    store_x29<Q>(reinterpret_cast<uint32_t*>(U), g, x29_add<Cv, Q>(run, other));
+    store_x29<Q>(reinterpret_cast<uint32_t*>(U), (size_t)nseg + g, run);  // V_g = U_1
   }
-}
-
-// LDS tree sum over a 256-thread block (all threads must call).
-template <class Cv>
-KZ_DEV Xyzz<Cv> block_sum256(Xyzz<Cv> v, Xyzz<Cv>* lds) {
-  const int t = threadIdx.x;
-  for (int s = 128; s >= 1; s >>= 1) {
-    if (t >= s && t < 2 * s) store_xyzz(&lds[t - s], v);
-    __syncthreads();
-    if (t < s) v = xyzz_add(v, load_xyzz(&lds[t]));
-    __syncthreads();
-  }
-  return v;  // valid in thread 0
 }
 
 // Window sums with a short dependency chain (~40 point operations per set; the earlier one
@@ -1386,7 +1146,7 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
   const uint32_t t = threadIdx.x;
   // the segment index of the q-th g (q < NSEG / 2) whose bit j is set
   auto bit_g = [j](uint32_t q) { return ((q >> j) << (j + 1)) | (1u << j) | (q & ((1u << j) - 1)); };
-  if constexpr (kAcc29<Cv>) {  // radix 2^29 on the R/U/V records, inline additions
+  {  // radix 2^29 on the R/U/V records, inline additions
     using Q = Fp29Of<Cv>;
     constexpr int N = Q::N, W29 = kW29<Q>;
     __shared__ uint32_t lds29[W29 + 1][128];
@@ -1395,7 +1155,7 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
     const uint32_t nsets = gridDim.x / RBP;  // V records follow the nsets * NSEG U records
     const uint32_t* V29 = reinterpret_cast<const uint32_t*>(U) + ((size_t)nsets + set) * NSEG * W29;
     X29<Q> v{F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), true};
-    if (j >= SB + 4) {  // kSegV: half sums of V_g
+    if (j >= SB + 4) {  // half sums of V_g
 #pragma unroll 1
       for (uint32_t q = t; q < NSEG / 2; q += 256) v = x29_add<Cv, Q>(v, load_x29<Q>(V29, (j - SB - 4) * (NSEG / 2) + q));
     } else if (j < SB) {
@@ -1436,29 +1196,7 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
       __syncthreads();
     }
     if (t == 0) store_xyzz(&parts[(size_t)set * RBP + j], x29_to32<Cv, Q>(v));
-    return;
   }
-  __shared__ __attribute__((aligned(16))) Xyzz<Cv> lds[128];
-  const Xyzz<Cv>* Rs = R + (size_t)set * NSEG;
-  const Xyzz<Cv>* Us = U + (size_t)set * NSEG;
-  const Xyzz<Cv>* Vs = U + ((size_t)gridDim.x / RBP + set) * NSEG;
-  Xyzz<Cv> s = Xyzz<Cv>::inf();
-  if (j >= SB + 4) {  // kSegV: half sums of V_g
-#pragma unroll 1
-    for (uint32_t q = t; q < NSEG / 2; q += 256) s = xyzz_add(s, load_xyzz(&Vs[(j - SB - 4) * (NSEG / 2) + q]));
-  } else if (j < SB) {
-#pragma unroll 1
-    for (uint32_t q = t; q < NSEG / 2; q += 256) s = xyzz_add(s, load_xyzz(&Us[bit_g(q)]));
-  } else {
-    const uint32_t base = (j - SB) * (NSEG / 4);
-#pragma unroll 1
-    for (uint32_t q = t; q < NSEG / 4; q += 256) {
-      s = xyzz_add(s, load_xyzz(&Rs[base + q]));
-      s = xyzz_add(s, load_xyzz(&Us[base + q]));
-    }
-  }
-  const Xyzz<Cv> v = block_sum256(s, lds);
-  if (t == 0) store_xyzz(&parts[(size_t)set * RBP + j], v);
 }
 
 // One wave per set, lane-parallel arithmetic (lpfield.hpp): Horner over the bit sums (c = 16:
@@ -1478,14 +1216,10 @@ __global__ void __launch_bounds__(64) k_reduce_bits_finish(const Xyzz<Cv>* __res
   for (int j = SB - 2; j >= 0; --j) V = lp_xyzz_add(c, lp_xyzz_dbl(c, V), lp_load_xyzz(c, &P[j]));
   LpXyzz<Cv> W = lp_xyzz_add(c, lp_xyzz_add(c, lp_load_xyzz(c, &P[SB]), lp_load_xyzz(c, &P[SB + 1])),
                              lp_xyzz_add(c, lp_load_xyzz(c, &P[SB + 2]), lp_load_xyzz(c, &P[SB + 3])));
-  if constexpr (kSegV) {  // 16 H + 8 sum V = 8 (2 H + sum V)
-    V = lp_xyzz_add(c, lp_xyzz_dbl(c, V), lp_xyzz_add(c, lp_load_xyzz(c, &P[SB + 4]), lp_load_xyzz(c, &P[SB + 5])));
+  // 16 H + 8 sum V = 8 (2 H + sum V)
+  V = lp_xyzz_add(c, lp_xyzz_dbl(c, V), lp_xyzz_add(c, lp_load_xyzz(c, &P[SB + 4]), lp_load_xyzz(c, &P[SB + 5])));
 #pragma unroll 1
-    for (int i = 0; i < 3; ++i) V = lp_xyzz_dbl(c, V);
-  } else {
-#pragma unroll 1
-    for (int i = 0; i < 4; ++i) V = lp_xyzz_dbl(c, V);
-  }
+  for (int i = 0; i < 3; ++i) V = lp_xyzz_dbl(c, V);
   lp_store_xyzz(c, &winsum[set], lp_xyzz_add(c, W, V));
 }
 

@@ -22,13 +22,13 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # KZGMI_LIB selects an alternative build (timing experiments); default: the in-tree library
 LIB_PATH = os.environ.get("KZGMI_LIB") or os.path.join(_HERE, "libkzgmi.so")
 
-ABI_VERSION = 4  # include/kzgmi.h KZGMI_ABI_VERSION
+ABI_VERSION = 5  # include/kzgmi.h KZGMI_ABI_VERSION
 CURVES = {"bls12_381": 0, "bn254": 1}
 FP_BYTES = {"bls12_381": 48, "bn254": 32}
 PHASES = ["convert", "scalars", "sort", "accumulate", "reduce", "combine", "pairing", "h2d"]
 
 ERR_NAMES = {-1: "ARG", -2: "ENCODING", -3: "NOT_ON_CURVE", -4: "SCALAR", -5: "DEVICE", -6: "OOM",
-             -7: "NOT_IN_SUBGROUP"}
+             -7: "NOT_IN_SUBGROUP", -8: "SHARD"}
 
 
 class KzgmiError(RuntimeError):
@@ -66,6 +66,7 @@ def lib():
         "kzgmi_ctx_destroy": ([vp], None),
         "kzgmi_srs_load": ([vp, c.c_int, u8p, u8p, u8p, c.POINTER(vp)], c.c_int),
         "kzgmi_ctx_num_devices": ([vp], c.c_int),
+        "kzgmi_slot_device": ([vp, c.c_int], c.c_int),
         "kzgmi_abi_version": ([], c.c_int),
         "kzgmi_ctx_reserve": ([vp, c.c_int, sz, c.c_uint32], c.c_int),
         "kzgmi_alloc_count": ([], c.c_uint64),
@@ -148,7 +149,7 @@ def exported_symbols():
         "kzgmi_batch_combine_device_async", "kzgmi_msm_partial_device",
         "kzgmi_msm_combine_device", "kzgmi_pairing", "kzgmi_gen_g1", "kzgmi_gen_tuples",
         "kzgmi_g2_mul", "kzgmi_probe_fpmul", "kzgmi_set_profiling", "kzgmi_get_phase_ms",
-        "kzgmi_ctx_num_devices", "kzgmi_stream_wait", "kzgmi_slot_signal", "kzgmi_partial_encode_device",
+        "kzgmi_ctx_num_devices", "kzgmi_slot_device", "kzgmi_stream_wait", "kzgmi_slot_signal", "kzgmi_partial_encode_device",
         "kzgmi_batch_verify_multi_device", "kzgmi_msm_g1_multi_device",
         "kzgmi_abi_version", "kzgmi_ctx_reserve", "kzgmi_alloc_count", "kzgmi_batch_verify_ex_async",
         "kzgmi_host_alloc", "kzgmi_host_free", "kzgmi_host_register", "kzgmi_host_unregister",
@@ -219,6 +220,8 @@ def _host_ptr(x):
     """(address, nbytes, keepalive) of a host buffer, without copying it: bytes, bytearray,
     memoryview, numpy arrays (C-contiguous) and CPU torch tensors.  The keepalive object must
     outlive every use of the address."""
+    if x is None:
+        return 0, 0, None
     if isinstance(x, bytes):
         cp = ctypes.c_char_p(x)  # points into the bytes object itself
         return ctypes.cast(cp, ctypes.c_void_p).value or 0, len(x), (x, cp)
@@ -232,11 +235,14 @@ def _host_ptr(x):
         return t.data_ptr(), t.numel() * t.element_size(), t
     if isinstance(x, (bytearray, memoryview)):
         x = np.frombuffer(x, dtype=np.uint8)
-    if isinstance(x, np.ndarray):
-        if not x.flags["C_CONTIGUOUS"]:
-            x = np.ascontiguousarray(x)
-        return x.ctypes.data, x.nbytes, x
-    raise TypeError("unsupported buffer type %r" % type(x))
+    if not isinstance(x, np.ndarray):
+        try:  # any other buffer-protocol object (array.array, mmap, ...)
+            x = np.frombuffer(memoryview(x).cast("B"), dtype=np.uint8)
+        except TypeError:
+            raise TypeError("unsupported buffer type %r" % type(x)) from None
+    if not x.flags["C_CONTIGUOUS"]:
+        x = np.ascontiguousarray(x)
+    return x.ctypes.data, x.nbytes, x
 
 
 class HostBuffer:
@@ -250,13 +256,17 @@ class HostBuffer:
         p = ctypes.c_void_p()
         _check(lib().kzgmi_host_alloc(int(nbytes), ctypes.byref(p)))
         self.ptr, self.nbytes = p.value, int(nbytes)
-        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr))
+        raw = (ctypes.c_uint8 * self.nbytes).from_address(self.ptr)
+        raw._kzgmi_owner = self  # every numpy view's base chain ends here: the block outlives its views
+        self.array = np.ctypeslib.as_array(raw)
 
     def view(self, offset: int, nbytes: int):
         """numpy view of [offset, offset + nbytes) (also accepted by the host entry points)."""
         return self.array[offset:offset + nbytes]
 
     def free(self):
+        """Release the block now (the caller guarantees no view is used afterwards and no job
+        reading it is in flight); otherwise it is released when the last view goes away."""
         if getattr(self, "ptr", None):
             self.array = None
             lib().kzgmi_host_free(self.ptr)
@@ -327,8 +337,10 @@ class CommitKey:
 
 class Context:
     """One GPU (device_id) with `slots` independent workspaces/streams; or, with
-    devices=[d0, d1, ...], one context over several GPUs (kzgmi_ctx_create's device list: host-buffer
-    batch_verify / msm_g1 are sharded over them; d0 is the primary device).
+    devices=[d0, d1, ...], one context over several GPUs (kzgmi_ctx_create's device list: the
+    synchronous host-buffer batch_verify / msm_g1 are sharded over them, d0 being the primary
+    device; the async entry points run whole batches per device -- slot s on device
+    slot_device(s) = devices[s % len(devices)], device tensors passed to it must live there).
 
     Device-tensor arguments are read on the library's own streams: every call first orders
     the slot's stream after torch's current stream (kzgmi_stream_wait), so tensors written by
@@ -343,9 +355,17 @@ class Context:
         self.handle = h
         self.device = device
         self.slots = slots
+        self.ndev = len(devs)
 
     def num_devices(self) -> int:
         return int(lib().kzgmi_ctx_num_devices(self.handle))
+
+    def slot_device(self, slot: int) -> int:
+        """The device id slot `slot` runs on (kzgmi_slot_device)."""
+        d = int(lib().kzgmi_slot_device(self.handle, int(slot)))
+        if d < 0:
+            _check(d)
+        return d
 
     def reserve(self, curve: str, n: int, compressed: bool = False, subgroup_check: bool = False,
                 fiat_shamir: bool = False, powers: bool = False, trusted_g1: bool = False):
@@ -355,13 +375,16 @@ class Context:
         _check(lib().kzgmi_ctx_reserve(self.handle, CURVES[curve], int(n), fl))
 
     def _order(self, slot: int = 0):
-        """Order `slot`'s stream after torch's current stream (device inputs written by torch)."""
-        _check(lib().kzgmi_stream_wait(self.handle, int(slot), _current_stream(self.device)))
+        """Order `slot`'s next job after torch's current stream on the slot's device (device
+        inputs written by torch)."""
+        dev = self.device if self.ndev == 1 else self.slot_device(slot)
+        _check(lib().kzgmi_stream_wait(self.handle, int(slot), _current_stream(dev)))
 
     def signal(self, slot: int, stream=None):
         """kzgmi_slot_signal: order later work on `stream` (a torch.cuda.Stream; default torch's
         current stream) after everything enqueued so far on `slot` -- no host sync."""
-        st = stream.cuda_stream if stream is not None else _current_stream(self.device)
+        dev = self.device if self.ndev == 1 else self.slot_device(slot)
+        st = stream.cuda_stream if stream is not None else _current_stream(dev)
         _check(lib().kzgmi_slot_signal(self.handle, int(slot), st))
 
     def close(self):
@@ -435,12 +458,14 @@ class Context:
         the slot's pinned ring before this returns."""
         g1b = (1 if compressed else 2) * FP_BYTES[srs.curve]
         ptrs, keep = self._host_inputs(commitments, zs, ys, proofs, n, g1b)
-        self._host_keep = getattr(self, "_host_keep", {})
-        self._host_keep[slot] = keep  # the DMA may read the arrays until wait(slot)
         _check(lib().kzgmi_batch_verify_ex_async(self.handle, srs.handle, int(slot), *ptrs,
                                                  _challenge_seed(seed, challenge),
                                                  _flags(compressed, subgroup_check, fiat_shamir, challenge,
                                                         trusted_g1)))
+        # the DMA may read the arrays until wait(slot); a failed call (e.g. slot busy) keeps the
+        # pending job's keepalive
+        self._host_keep = getattr(self, "_host_keep", {})
+        self._host_keep[slot] = keep
 
     def batch_verify_async(self, srs: Srs, slot: int, commitments, zs, ys, proofs, n: int,
                            seed: Optional[bytes] = None, compressed: bool = False, subgroup_check: bool = False,

@@ -68,6 +68,25 @@ def main():
             out += pipe.submit(Cs, zs, ybad if b % 2 else ys, Ps, n, off, seed)
         out += pipe.drain()
         assert out == [True, False, True, False, True], (rank, eager, out)
+    # batch 1 has an off-curve commitment on rank 1's shard only.  Rank 1
+    # raises its own error, rank 0 the marked-record error; neither returns a verdict for it,
+    # and the pipelines stay in step for the batches after it
+    Cbad = Cs.clone()
+    if rank == 1:
+        Cbad[g1b * (n - 1) + g1b - 1] ^= 1
+    for lanes, eager in ((1, False), (0, True)):
+        pipe = ShardedPipeline(ctx, srs, slots=2, lanes=lanes, eager=eager)
+        out = []
+
+        def take(call):
+            try:
+                out.extend(call())
+            except kzgmi.KzgmiError as e:
+                out.extend(e.code if r is None else r for r in e.results)
+        for b in range(4):
+            take(lambda: pipe.submit(Cbad if b == 1 else Cs, zs, ybad if b == 2 else ys, Ps, n, off, seed))
+        take(pipe.drain)
+        assert out == [True, -3, False, True], (rank, eager, out)
     dist.barrier()
     dist.destroy_process_group()
     print("RANK OK", rank, flush=True)

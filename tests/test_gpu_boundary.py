@@ -348,3 +348,121 @@ def test_reserve_argument_checks(ctx):
     with pytest.raises(kzgmi.KzgmiError):
         ctx.reserve("bls12_381", 16, fiat_shamir=True, powers=True)  # exclusive modes
     assert kzgmi.lib().kzgmi_abi_version() == kzgmi.ABI_VERSION
+
+
+@pytest.mark.parametrize("curve", ["bls12_381", "bn254"])
+def test_failed_shard_partial_is_marked(curve):
+    """a shard partial whose inputs fail validation is written MARKED, and
+    every combine that reads it fails -- with the shard's own code (device-marked record) or
+    KZGMI_ERR_SHARD (record the caller filled with 0xFF) -- so no rank of a multi-GPU batch can
+    accept it.  Also the chained combine on the failing slot and the MSM partials."""
+    import torch
+    import kzgmi
+    c = kzgmi.Context(0, 3)
+    try:
+        tau, n = 0x7777, 64
+        srs = c.load_srs(curve, kzgmi.G2_GENERATOR[curve], c.g2_mul(curve, kzgmi.G2_GENERATOR[curve], tau))
+        Cm, z, y, P = _gen_batch(c, curve, 2 * n, tau, hashlib.sha256(b"mark").digest())
+        g1b = 2 * pc.CURVES[curve].fp_bytes
+        seed = hashlib.sha256(b"mark-seed").digest()
+        pb = c.partial_bytes(curve)
+        good = torch.empty(2 * pb, dtype=torch.uint8, device="cuda")
+        bad = torch.empty(2 * pb, dtype=torch.uint8, device="cuda")
+        c.batch_partial(srs, Cm[: n * g1b], z[: 32 * n], y[: 32 * n], P[: n * g1b], n, 0, seed, good)
+        Cbad = Cm[n * g1b:].clone()
+        Cbad[5 * g1b + g1b - 1] ^= 1  # off the curve
+        with pytest.raises(kzgmi.KzgmiError) as e:
+            c.batch_partial(srs, Cbad, z[32 * n:], y[32 * n:], P[n * g1b:], n, n, seed, bad)
+        assert e.value.code == -3
+        both = torch.cat([good, bad])
+        with pytest.raises(kzgmi.KzgmiError) as e:  # a remote rank's view: the shard's own code
+            c.batch_combine(srs, both, 2)
+        assert e.value.code == -3
+        # chained on the failing slot (the eager schedule): its wait reports the shard's error
+        c.batch_partial_async(srs, 1, Cbad, z[32 * n:], y[32 * n:], P[n * g1b:], n, n, seed, bad)
+        c.batch_combine_async(srs, 1, torch.cat([good, bad]), 2)
+        with pytest.raises(kzgmi.KzgmiError) as e:
+            c.wait(1)
+        assert e.value.code == -3
+        # caller-marked record (rejected before anything ran): KZGMI_ERR_SHARD on every rank
+        bad.fill_(0xFF)
+        with pytest.raises(kzgmi.KzgmiError) as e:
+            c.batch_combine(srs, torch.cat([good, bad]), 2)
+        assert e.value.code == -8
+        # the good shards alone still combine to the valid unsharded verdict
+        ok_part = torch.empty(2 * pb, dtype=torch.uint8, device="cuda")
+        c.batch_partial(srs, Cm[n * g1b:], z[32 * n:], y[32 * n:], P[n * g1b:], n, n, seed, ok_part)
+        assert c.batch_combine(srs, torch.cat([good, ok_part]), 2) is True
+        # MSM partials
+        mg = torch.empty(pb, dtype=torch.uint8, device="cuda")
+        mb = torch.empty(pb, dtype=torch.uint8, device="cuda")
+        c.msm_partial(curve, Cm[: n * g1b], z[: 32 * n], n, mg)
+        with pytest.raises(kzgmi.KzgmiError):
+            c.msm_partial(curve, Cbad, z[32 * n:], n, mb)
+        with pytest.raises(kzgmi.KzgmiError) as e:
+            c.msm_combine(curve, torch.cat([mg, mb]), 2)
+        assert e.value.code == -3
+        assert c.msm_combine(curve, mg, 1) == c.msm_g1(curve, Cm[: n * g1b], z[: 32 * n], n=n)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("curve,n_gold", [("bls12_381", 256), ("bn254", 64)])
+def test_multi_device_async_pipeline(curve, n_gold, golden):
+    """a device-list context pipelines WHOLE batches per device through the
+    async entry points -- caller slot s runs on device s % D (kzgmi_slot_device) with its own
+    lane pipeline there, no collective.  On the box's one GPU the list is [0, 0] (two device
+    contexts).  Golden batches (valid / flipped y / swapped proofs) from host buffers on every
+    slot, verdicts as the fixtures'; A, B of a routed slot's partial bit-exact vs the golden; a
+    2^20 batch and its corrupted copy in flight on the two devices at once."""
+    import kzgmi
+    import torch
+    g = golden("%s_batch_n%d.json" % (curve, n_gold))
+    mc = kzgmi.Context(slots=4, devices=[0, 0])
+    try:
+        assert mc.num_devices() == 2 and mc.slots == 4
+        assert [mc.slot_device(s) for s in range(4)] == [0, 0, 0, 0]
+        srs = mc.load_srs(curve, h(g["g2"]), h(g["tau_g2"]))
+        seed = h(g["seed"])
+        cases = ["valid", "neg_flip_y", "neg_swap_proofs", "valid", "neg_flip_y", "valid", "neg_swap_proofs", "valid"]
+        pend = {}
+        got = []
+        for k, key in enumerate(cases):
+            s = k % 4
+            if s in pend:
+                got.append((pend.pop(s), mc.wait(s)))
+            src = g if key == "valid" else g[key]
+            mc.batch_verify_host_async(srs, s, h(src["commitments"]), h(src["zs"]), h(src["ys"]), h(src["proofs"]),
+                                       seed=seed)
+            pend[s] = key
+        for s in sorted(pend):
+            got.append((pend[s], mc.wait(s)))
+        assert sorted(got) == sorted((key, g[key]["ok"]) for key in cases)
+        # A, B through a slot on the second device (caller slot 1): partial of the whole batch
+        pb = mc.partial_bytes(curve)
+        rec = torch.empty(2 * pb, dtype=torch.uint8, device="cuda")
+        dev = [_dev(h(g[k])) for k in ("commitments", "zs", "ys", "proofs")]
+        mc.batch_partial_async(srs, 1, *dev, n_gold, 0, seed, rec)
+        assert mc.wait(1) is True
+        A, B = mc.partial_encode(curve, rec, 2)
+        assert (A.hex(), B.hex()) == (g["valid"]["A"], g["valid"]["B"])
+        # full size: one valid 2^20 batch on device 0 (slot 2), its corrupted copy on device 1 (slot 3)
+        sc = kzgmi.Context(0, 1)
+        try:
+            n, tau = 1 << 20, 0x1F2E3D4C
+            Cm, z, y, P = _gen_batch(sc, curve, n, tau, hashlib.sha256(b"multi-async").digest())
+            g2 = kzgmi.G2_GENERATOR[curve]
+            srs2 = mc.load_srs(curve, g2, mc.g2_mul(curve, g2, tau))
+            ybad = y.clone()
+            ybad[32 * 777 + 31] ^= 1
+            torch.cuda.synchronize()
+            mc.batch_verify_async(srs2, 2, Cm, z, y, P, n, seed=seed)
+            mc.batch_verify_async(srs2, 3, Cm, z, ybad, P, n, seed=seed)
+            assert mc.wait(2) is True
+            assert mc.wait(3) is False
+        finally:
+            sc.close()
+        with pytest.raises(kzgmi.KzgmiError):
+            mc.wait(5)
+    finally:
+        mc.close()

@@ -125,8 +125,17 @@ def test_host_async_errors(ctx, golden):
     mc = kzgmi.Context(slots=1, devices=[0, 0])
     try:
         msrs = mc.load_srs("bls12_381", h(g["g2"]), h(g["tau_g2"]))
-        with pytest.raises(kzgmi.KzgmiError) as e:  # multi-device contexts shard in batch_verify instead
+        # ABI 5: a multi-device context runs a whole host-buffer batch on the slot's device
+        mc.batch_verify_host_async(msrs, 0, *args, seed=h(g["seed"]))
+        with pytest.raises(kzgmi.KzgmiError) as e:  # slot busy, on the routed device too
             mc.batch_verify_host_async(msrs, 0, *args, seed=h(g["seed"]))
+        assert e.value.code == -1
+        with pytest.raises(kzgmi.KzgmiError) as e:  # the synchronous split needs every first slot idle
+            mc.batch_verify(msrs, *args, seed=h(g["seed"]))
+        assert e.value.code == -1
+        assert mc.wait(0) is True
+        with pytest.raises(kzgmi.KzgmiError) as e:  # slot 1 does not exist (slots=1)
+            mc.batch_verify_host_async(msrs, 1, *args, seed=h(g["seed"]))
         assert e.value.code == -1
         assert mc.batch_verify(msrs, *args, seed=h(g["seed"])) is True
         del msrs
