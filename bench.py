@@ -48,12 +48,13 @@ if __name__ == "__main__":
     if _rc is not None:
         sys.exit(_rc)
 
-# HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default).  The slot
-# pipeline needs about one queue per batch in flight -- batches whose streams share a queue
-# serialise (measured: 12 slots on 4 queues 77/s, on 12-16 queues 106/s; after the latency-tail
-# work 12 slots x 16 queues 139-140/s, 16 x 24 142-145/s, 24 x 32 134/s: profiles/r01/
-# prio_sweep.txt).  Read by the HIP
-# runtime when it initialises, so set before torch touches the GPU.
+# HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues per stream priority (4 by
+# default).  The slot pipeline needs about one queue per batch in flight -- batches whose streams
+# share a queue serialise.  At HIP's default the library spreads its slot streams over the stream
+# priorities (csrc/api.hip kzgmi_ctx_create_device) and reaches 0.96 of the 24-queue rate at 2^20
+# (profiles/r05/ab_stream_prio.txt); the headline sets 24 queues, and secondary.default_hw_queues
+# reports the same measurement at the default (a child process: the queue count is read when the
+# HIP runtime initialises, so it is set here before torch touches the GPU).
 os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("KZGMI_HW_QUEUES", "24")
 
 import torch  # noqa: E402
@@ -330,6 +331,11 @@ def main():
     ap.add_argument("--shard17-steps", type=int, default=240,
                     help="secondary.sharded_2e17_world1: 2^17-tuple batches (configs[2]'s 8-way per-rank share) "
                          "through ShardedPipeline + RCCL at world 1, and unsharded (0 = skip)")
+    ap.add_argument("--default-queues-steps", type=int, default=20,
+                    help="secondary.default_hw_queues: the configs[2] timed region again in a child process at HIP's "
+                         "default GPU_MAX_HW_QUEUES = 4 (0 = skip)")
+    ap.add_argument("--detail-file", default="gpurun_out/bench_detail.json",
+                    help="where the full record goes (the printed line is the compact form; '' = nowhere)")
     ap.add_argument("--strong-steps", type=int, default=0,
                     help="sharded runs: batches of the strong-scaled leg (one --n batch split over the ranks; "
                          "default = --steps)")
@@ -1086,6 +1092,22 @@ def main():
             cpu["host"] = host_info()
         except Exception as e:  # the baseline must not kill the GPU measurement
             cpu = {"error": repr(e)}
+    # ---- the same timed region at HIP's default hardware-queue count (child process)
+    dq = None
+    if world == 1 and not sharded and args.default_queues_steps > 0:
+        env = dict(os.environ, KZGMI_HW_QUEUES="4")
+        cmd = [sys.executable, os.path.abspath(__file__), "--steps", str(args.default_queues_steps),
+               "--warmup", str(min(args.warmup, 5)), "--n", str(n), "--curve", curve, "--slots", str(slots),
+               "--detail-file", "", "--no-cpu", "--repeats", "1", "--default-queues-steps", "0", "--msm-steps", "0",
+               "--trusted-steps", "0", "--fs-steps", "0", "--commit-steps", "0", "--compressed-steps", "0",
+               "--cfg4-msms", "0", "--h2d-steps", "0", "--bn254-steps", "0", "--shard17-steps", "0"]
+        try:
+            p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+            line = json.loads(p.stdout.strip().splitlines()[-1])
+            dq = {"hw_queues": 4, "batch_verifies_per_s": line["value"], "ms_per_step": line["ms_per_step"],
+                  "steps": args.default_queues_steps, "frac_of_value": line["value"] / value}
+        except Exception as e:  # the child's failure must not kill the headline measurement
+            dq = {"error": repr(e)[:300]}
     cfg0_cpu_ms = (cpu or {}).get("cfg0_cpu_n256_ms")
     if cfg0 is not None and cfg0_cpu_ms is not None:
         cfg0["cpu_ms"] = cfg0_cpu_ms
@@ -1121,15 +1143,16 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
-        "lanes": os.environ.get("KZGMI_LANES", "1"),
+        "default_hw_queues": dq,
     }
     # The printed line stays short enough (< ~5 kB) for the driver's stdout tail to hold all of
     # it; the full record (per-run arrays, phase dicts, methods) goes to a side file.
-    detail_path = os.path.join(ROOT, "gpurun_out", "bench_detail.json")
+    detail_path = os.path.join(ROOT, args.detail_file) if args.detail_file else None
     try:
-        os.makedirs(os.path.dirname(detail_path), exist_ok=True)
-        with open(detail_path, "w") as f:
-            json.dump(detail, f, indent=1)
+        if detail_path:
+            os.makedirs(os.path.dirname(detail_path), exist_ok=True)
+            with open(detail_path, "w") as f:
+                json.dump(detail, f, indent=1)
     except OSError:
         detail_path = None
 
@@ -1196,6 +1219,8 @@ def main():
         "gpu_vs_cpu": r4(value / cpu["value"]) if comp_cpu else None,
         "gpu_vs_cpu_full_host_extrapolated": r4(value / cpu["full_host_extrapolated"]["value"]) if comp_cpu else None,
         "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+        "default_hw_queues_batch_verifies_per_s": g(dq, "batch_verifies_per_s"),
+        "default_hw_queues_frac": g(dq, "frac_of_value"),
         "detail_file": os.path.relpath(detail_path, ROOT) if detail_path else None,
     }
     out = {

@@ -20,14 +20,15 @@
  *   - Return value 0 = OK, negative = error (see KZGMI_ERR_*).  Invalid input is an error,
  *     never "ok = 0".  kzgmi_last_error() gives a thread-local message.
  *   - Threading: one ctx per host thread; calls on one ctx are serialised by the caller.
- *   - Device-memory ordering: the library runs on its own non-blocking HIP streams: three
- *     shared "lanes" per context (front end / bucket accumulation / tail), which every slot's
- *     jobs hop between in order, so the pipeline needs 3 hardware queues (+1 for host-buffer
- *     copies) whatever the slot count -- HIP's default GPU_MAX_HW_QUEUES = 4 suffices
- *     (KZGMI_LANES=0 in the environment selects rounds 1-4's stream per slot instead).  A caller
- *     that produced device inputs on another stream (e.g. a torch stream) must order the slot's
- *     next job after it -- kzgmi_stream_wait(ctx, slot, stream) (no host sync), or synchronise
- *     that stream -- before the call that reads them.  Device outputs
+ *   - Device-memory ordering: the library runs on its own non-blocking HIP streams, one per
+ *     pipeline slot (+ one for host-buffer copies).  HIP gives streams GPU_MAX_HW_QUEUES hardware
+ *     queues per stream priority (4 by default) and streams sharing a queue run one after
+ *     another: when the slots outnumber the queues the slot streams cycle through the device's
+ *     stream priorities (KZGMI_STREAM_PRIO=0/1 forces it off/on), which keeps 16 slots at 0.96
+ *     of their 24-queue rate at the default 4 queues.  A caller that produced device inputs on
+ *     another stream (e.g. a torch stream) must order the slot's next job after it --
+ *     kzgmi_stream_wait(ctx, slot, stream) (no host sync), or synchronise that stream -- before
+ *     the call that reads them.  Device outputs
  *     (partials, digests, generated points) are complete when the call, or the
  *     kzgmi_slot_wait / kzgmi_msm_wait that completes it, returns.  Device buffers passed to
  *     an async call must stay allocated until its wait returns.

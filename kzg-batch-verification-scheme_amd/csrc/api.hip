@@ -92,22 +92,8 @@ enum Phase { PH_CONVERT = 0, PH_SCALARS, PH_SORT, PH_ACCUM, PH_REDUCE, PH_COMBIN
 constexpr int EV_H2D0 = kNumBatchPhases + 1, EV_H2D1 = kNumBatchPhases + 2;  // Slot::ev indices
 constexpr size_t kRingBytes = size_t(16) << 20;  // pinned staging ring of pageable host inputs (x 2 per slot)
 
-// Lanes: the streams a job's phases are issued on.  In lane mode (the default) the context owns
-// ONE accumulation stream and NJ "job" streams; a job on slot s runs its front end (decode,
-// randomisers, sort) and its tail (reduce, window combination, pairing / partial out) on job
-// stream s % NJ and hops to the accumulation stream in between, ordered by events.  So the front
-// end of batch k+1 and the tails of earlier batches run beside the accumulation of batch k, and
-// the pipeline needs NJ + 1 hardware queues (+1 for host-buffer copies) whatever the slot count:
-// NJ = GPU_MAX_HW_QUEUES - 2 (at least 2, at most 8) reaches its rate at HIP's default of 4
-// queues.  KZGMI_LANES=<NJ> sets NJ; KZGMI_LANES=0 selects slot mode: each slot has a stream of
-// its own and a job stays on it (rounds 1-4; needs a hardware queue per slot in flight).
-enum Lane { LANE_FRONT = 0, LANE_ACC = 1, LANE_TAIL = 2, kNumLanes = 3 };
-
 struct Slot {
-  int idx = 0;                   // index in the context's slots (lane mode: job stream idx % NJ)
-  hipStream_t own = nullptr;     // slot mode: this slot's stream
-  hipStream_t stream = nullptr;  // the stream the slot's current job issues on (begin_job / hop)
-  hipEvent_t hop_ev[kNumLanes] = {};  // a job's hand-over into lane l (recorded on the lane it leaves)
+  hipStream_t stream = nullptr;       // the slot's stream: every job on the slot is issued here
   hipEvent_t done_ev = nullptr;       // the slot's last job issued so far has completed
   bool done_rec = false;
   std::vector<hipEvent_t> dep_pool;   // entry dependencies of the slot's next job (kzgmi_stream_wait, the
@@ -140,9 +126,7 @@ struct kzgmi_ctx {
   int device = 0;
   std::vector<Slot> slots;
   int user_slots = 0;                   // slots in the caller's numbering (multi-device: over all devices)
-  bool lanes = true;                    // lane mode (KZGMI_LANES; see Lane)
-  std::vector<hipStream_t> acc_lanes;   // lane mode: the NA accumulation streams
-  std::vector<hipStream_t> job_lanes;   // lane mode: the NJ front-end + tail streams
+  int prio_levels = 1;                  // stream priorities the slot streams cycle through
   bool profiling = false;
   // GLV split of full Fr scalars.  phi(P) = [lambda] P holds only on
   // G1, so BLS12-381 (cofactor > 1) uses it only for points known to be in G1: batch calls
@@ -205,32 +189,12 @@ int set_dev(kzgmi_ctx* c) {
 
 inline unsigned grid(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
-hipStream_t lane_stream(const kzgmi_ctx* c, const Slot& s, int l) {
-  if (!c->lanes) return s.own;
-  return l == LANE_ACC ? c->acc_lanes[(size_t)s.idx % c->acc_lanes.size()]
-                       : c->job_lanes[(size_t)s.idx % c->job_lanes.size()];
-}
-
-// Start a job on slot s in lane l: after the slot's previous job (its workspace is reused) and
-// the entry dependencies recorded since (kzgmi_stream_wait, the H2D copy of host inputs).  Every
-// entry point that issues work on a slot calls this first; the work then goes on s.stream.
-int begin_job(kzgmi_ctx* c, Slot& s, int l) {
-  hipStream_t st = lane_stream(c, s, l);
-  if (s.done_rec && st != s.stream) HIPCHK(hipStreamWaitEvent(st, s.done_ev, 0));
-  for (int k = 0; k < s.ndep; ++k) HIPCHK(hipStreamWaitEvent(st, s.dep_pool[k], 0));
+// Start a job on slot s: its work goes on s.stream after the entry dependencies recorded since
+// the slot's previous job (kzgmi_stream_wait, the H2D copy of host inputs).  Every entry point
+// that issues work on a slot calls this first.
+int begin_job(Slot& s) {
+  for (int k = 0; k < s.ndep; ++k) HIPCHK(hipStreamWaitEvent(s.stream, s.dep_pool[k], 0));
   s.ndep = 0;
-  s.stream = st;
-  return 0;
-}
-
-// Move the slot's current job to lane l (no-op in slot mode): l's later work waits for
-// everything the job issued so far
-int hop(kzgmi_ctx* c, Slot& s, int l) {
-  hipStream_t st = lane_stream(c, s, l);
-  if (st == s.stream) return 0;
-  HIPCHK(hipEventRecord(s.hop_ev[l], s.stream));
-  HIPCHK(hipStreamWaitEvent(st, s.hop_ev[l], 0));
-  s.stream = st;
   return 0;
 }
 
@@ -242,8 +206,8 @@ int end_job(Slot& s) {
   return 0;
 }
 
-// Host wait for the slot's last job (an event: the lanes are shared, so a stream sync would
-// also wait for other slots' later work)
+// Host wait for the slot's last job (an event, not a stream sync: an entry dependency recorded
+// for the slot's next job must not be waited for here)
 int sync_slot(Slot& s) {
   if (s.done_rec) HIPCHK(hipEventSynchronize(s.done_ev));
   return 0;
@@ -403,14 +367,10 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
           s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.total.template as<uint32_t>(),
           s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(), wbits);
   mark(c, s, PH_SORT + 1);
-  CHK(hop(c, s, LANE_ACC));
-  st = s.stream;
   L::accumulate(st, nchunks, s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
                 s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts, s.acc29.template as<uint32_t>(), NB,
                 acc_threads, acc_threads ? s.accq.template as<uint32_t>() : nullptr);
   mark(c, s, PH_ACCUM + 1);
-  CHK(hop(c, s, LANE_TAIL));
-  st = s.stream;
   L::reduce(st, nsets, s.cnt.template as<uint32_t>(), s.acc29.template as<uint32_t>(), s.R.template as<XY>(),
             s.U.template as<XY>(), s.scratch.template as<XY>(), s.winsum.template as<XY>(), wbits);
   mark(c, s, PH_REDUCE + 1);
@@ -525,7 +485,7 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
     if (flags & KZGMI_FLAG_FIAT_SHAMIR) CHK(reserve_fs<Cv>(s, n));
     else if (flags & KZGMI_FLAG_POWERS) CHK(s.pow.ensure(FS_POW_BITS * sizeof(FrF)));
   }
-  hipStream_t st = nullptr;  // set by begin_job in front()
+  hipStream_t st = s.stream;
   uint32_t* err = s.flags.template as<uint32_t>() + 1;
   Affine<Cv>* pts = s.pts.template as<Affine<Cv>>();
   uint8_t* inf = s.inf.template as<uint8_t>();
@@ -540,8 +500,7 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   // decode + validate the points, derive the randomisers and the MSM scalars
   auto front = [&]() -> int {
     Roctx rx("kzgmi.batch.convert+scalars");
-    CHK(begin_job(c, s, LANE_FRONT));
-    st = s.stream;
+    CHK(begin_job(s));
     mark(c, s, 0);
     HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
     if (flags & KZGMI_FLAG_COMPRESSED) {
@@ -636,7 +595,6 @@ int enqueue_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const void* dC, c
   }
   if (dry) return 0;
   Roctx rx("kzgmi.batch.pairing");
-  st = s.stream;  // the tail lane (run_msm_core hopped there)
   if (d_partial_out) {
     L::partial_out(st, s.res.template as<XY>(), 2, err, (XY*)d_partial_out);  // marked if this shard failed
   } else {
@@ -901,54 +859,43 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
   if (const char* e = getenv("KZGMI_ACC_QUEUE_FROM")) c->acc_queue_from = strtoull(e, nullptr, 10);
   if (const char* e = getenv("KZGMI_SORT_SPLIT")) c->sort_split = atoi(e) != 0;
   if (const char* e = getenv("KZGMI_WBITS")) c->wbits_env = atoi(e);
+  // HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 unless set before the runtime
+  // starts) and serialises the streams of one queue, so every slot in flight needs a queue of its
+  // own (16 slots on 24 queues pipeline; 24 on 24 ran 3.6x slower).  The runtime keeps that many
+  // queues PER STREAM PRIORITY: when the slots (+ the copy stream) outnumber the queues, the slot
+  // streams cycle through the device's priority levels, which multiplies the queues they get --
+  // at the default 4 queues, 2^20 batches run 173 vs 161/s (0.96 of the 179.5/s on 24 queues)
+  // and 2^17 batches 814 vs 577/s (profiles/r05/ab_stream_prio*.txt).  KZGMI_STREAM_PRIO=0/1
+  // forces it off / on.
   const char* qenv = getenv("GPU_MAX_HW_QUEUES");
-  const int queues = qenv ? atoi(qenv) : 4;
-  int nj = 0;  // (A/B) slot mode unless KZGMI_LANES sets the job-lane count
-  if (const char* e = getenv("KZGMI_LANES")) nj = std::min(64, atoi(e));
-  c->lanes = nj > 0;
-  if (!c->lanes) {
-    // slot mode: HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 unless set before the
-    // runtime starts) and serialises the streams of one queue, so slots + the copy stream need
-    // queues of their own (16 slots on 24 queues pipeline; 24 on 24 ran 3.6x slower)
+  const int queues = qenv ? std::max(1, atoi(qenv)) : 4;
+  int prio_least = 0, prio_greatest = 0;
+  bool spread = pipeline_slots + 1 > queues;
+  if (const char* e = getenv("KZGMI_STREAM_PRIO")) spread = atoi(e) != 0;
+  spread = spread && hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) == hipSuccess &&
+           prio_least != prio_greatest;
+  c->prio_levels = spread ? std::abs(prio_least - prio_greatest) + 1 : 1;
+  {
     static std::atomic<bool> warned{false};
-    if (pipeline_slots > 1 && pipeline_slots + 1 > queues && !getenv("KZGMI_QUIET") && !warned.exchange(true))
-      fprintf(stderr, "kzgmi: %d pipeline slots on %d hardware queues (GPU_MAX_HW_QUEUES) in slot mode "
-                      "(KZGMI_LANES=0): slots sharing a queue run one after another\n",
-              pipeline_slots, queues);
+    if (pipeline_slots > 1 && pipeline_slots + 1 > queues * c->prio_levels && !getenv("KZGMI_QUIET") &&
+        !warned.exchange(true))
+      fprintf(stderr, "kzgmi: %d pipeline slots on %d hardware queues (GPU_MAX_HW_QUEUES x %d stream priorities): "
+                      "slots sharing a queue run one after another\n",
+              pipeline_slots, queues * c->prio_levels, c->prio_levels);
   }
-  bool okc = true;
-  // lane streams first (the runtime hands hardware queues to streams in creation order), then the
-  // copy stream of host-buffer inputs
-  if (c->lanes) {
-    int na = 1;
-    if (const char* e = getenv("KZGMI_ACC_LANES")) na = std::max(1, std::min(64, atoi(e)));
-    c->acc_lanes.assign(na, nullptr);
-    c->job_lanes.assign(nj, nullptr);
-    for (auto& st : c->acc_lanes) okc = okc && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
-    for (auto& st : c->job_lanes) okc = okc && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
-  }
-  // KZGMI_STREAM_PRIO=1 (A/B): the slot streams cycle through the device's stream priorities
-  int prio_lo = 0, prio_hi = 0;
-  const bool spread = getenv("KZGMI_STREAM_PRIO") && atoi(getenv("KZGMI_STREAM_PRIO")) != 0 &&
-                      hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) == hipSuccess;
-  okc = okc && hipStreamCreateWithFlags(&c->h2d_stream, hipStreamNonBlocking) == hipSuccess;
+  bool okc = hipStreamCreateWithFlags(&c->h2d_stream, hipStreamNonBlocking) == hipSuccess;
   c->slots.resize(pipeline_slots);
   c->user_slots = pipeline_slots;
-  for (size_t k = 0; k < c->slots.size(); ++k) c->slots[k].idx = (int)k;
-  for (auto& s : c->slots) {
-    if (!c->lanes) {
-      const int nlev = std::abs(prio_lo - prio_hi) + 1;
-      const int pr = prio_hi < prio_lo ? prio_hi + s.idx % nlev : prio_hi - s.idx % nlev;
-      okc = okc && (spread ? hipStreamCreateWithPriority(&s.own, hipStreamNonBlocking, pr)
-                           : hipStreamCreateWithFlags(&s.own, hipStreamNonBlocking)) == hipSuccess;
-    }
-    for (auto& e : s.hop_ev) okc = okc && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  for (size_t k = 0; k < c->slots.size() && okc; ++k) {
+    Slot& s = c->slots[k];
+    const int step = prio_least > prio_greatest ? 1 : -1;  // from the greatest priority towards the least
+    okc = (spread ? hipStreamCreateWithPriority(&s.stream, hipStreamNonBlocking,
+                                                prio_greatest + step * (int)(k % c->prio_levels))
+                  : hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) == hipSuccess;
     okc = okc && hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming) == hipSuccess &&
           hipEventCreateWithFlags(&s.signal_ev, hipEventDisableTiming) == hipSuccess &&
           hipHostMalloc((void**)&s.host_flags, 16, hipHostMallocDefault) == hipSuccess &&
           hipHostMalloc((void**)&s.host_out, 128, hipHostMallocDefault) == hipSuccess;
-    s.stream = lane_stream(c, s, LANE_FRONT);
-    if (!okc) break;
   }
   if (!okc) {
     kzgmi_ctx_destroy(c);
@@ -961,13 +908,8 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
 void kzgmi_ctx_destroy(kzgmi_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  for (auto& s : c->slots) (void)sync_slot(s);
-  for (auto& st : c->acc_lanes)
-    if (st) (void)hipStreamSynchronize(st);
-  for (auto& st : c->job_lanes)
-    if (st) (void)hipStreamSynchronize(st);
   for (auto& s : c->slots) {
-    if (s.own) (void)hipStreamSynchronize(s.own);
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
     DevBuf* bufs[] = {&s.pts, &s.inf, &s.scal_r, &s.scal_s, &s.scal_t, &s.tpart, &s.cnt, &s.off, &s.coarse, &s.ent,
                       &s.total, &s.sval, &s.skey, &s.acc29, &s.accq, &s.R, &s.U, &s.scratch,
                       &s.winsum, &s.res, &s.flags, &s.stage, &s.outb, &s.fs_leaves, &s.fs_tmp,
@@ -978,20 +920,14 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
     if (s.signal_ev) (void)hipEventDestroy(s.signal_ev);
     if (s.done_ev) (void)hipEventDestroy(s.done_ev);
     for (auto& e : s.dep_pool) (void)hipEventDestroy(e);
-    for (auto& e : s.hop_ev)
-      if (e) (void)hipEventDestroy(e);
     for (int b = 0; b < 2; ++b) {
       if (s.ring_ev[b]) (void)hipEventDestroy(s.ring_ev[b]);
       if (s.ring[b]) (void)hipHostFree(s.ring[b]);
     }
     if (s.host_flags) (void)hipHostFree(s.host_flags);
     if (s.host_out) (void)hipHostFree(s.host_out);
-    if (s.own) (void)hipStreamDestroy(s.own);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
   }
-  for (auto& st : c->acc_lanes)
-    if (st) (void)hipStreamDestroy(st);
-  for (auto& st : c->job_lanes)
-    if (st) (void)hipStreamDestroy(st);
   for (int k = 0; k < 2; ++k) { c->table[k].release(); c->table_base[k].release(); }
   if (c->h2d_stream) {
     (void)hipStreamSynchronize(c->h2d_stream);
@@ -1067,7 +1003,7 @@ int kzgmi_srs_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uin
     memcpy(h.data(), tau_g2, gb);
     memcpy(h.data() + gb, g2, gb);
     if (g1) memcpy(h.data() + 2 * gb, g1, g1b);
-    if (int rb = begin_job(c, s, LANE_FRONT)) {
+    if (int rb = begin_job(s)) {
       kzgmi_srs_free(srs);
       return rb;
     }
@@ -1305,7 +1241,7 @@ int kzgmi_last_combination(kzgmi_ctx* c, uint8_t* a_out, uint8_t* b_out) {
     using Cv = decltype(cv);
     const size_t gb = g1_bytes(Cv::ID);
     CHK(s.outb.ensure(2 * gb));
-    CHK(begin_job(c, s, LANE_TAIL));
+    CHK(begin_job(s));
     Launch<Cv>::encode_points(s.stream, s.res.template as<Xyzz<Cv>>(), 2, s.outb.template as<uint8_t>());
     HIPCHK(hipGetLastError());
     std::vector<uint8_t> h(2 * gb);
@@ -1328,7 +1264,7 @@ int enqueue_msm(kzgmi_ctx* c, Slot& s, const void* dpts, const void* dsc, size_t
   CHK(s.scal_s.ensure(n * 32));
   if (glv) CHK(s.glv_s.ensure(n * 32));
   CHK(s.flags.ensure(16));
-  CHK(begin_job(c, s, LANE_FRONT));
+  CHK(begin_job(s));
   hipStream_t st = s.stream;
   mark(c, s, 0);
   HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
@@ -1399,7 +1335,7 @@ int kzgmi_ck_load(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1_powers, siz
       delete ck;
       return r;
     }
-    if (int rb = begin_job(c, s, LANE_FRONT)) {
+    if (int rb = begin_job(s)) {
       delete ck;
       return rb;
     }
@@ -1458,7 +1394,7 @@ int kzgmi_commit_device_async(kzgmi_ctx* c, const kzgmi_ck* ck, int slot, const 
     CHK(s.flags.ensure(16));
     CHK(s.outb.ensure(gb));
     CHK(s.res.ensure(2 * sizeof(Xyzz<Cv>)));
-    CHK(begin_job(c, s, LANE_FRONT));
+    CHK(begin_job(s));
     hipStream_t st = s.stream;
     HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
     if (m == 0) {
@@ -1480,7 +1416,6 @@ int kzgmi_commit_device_async(kzgmi_ctx* c, const kzgmi_ck* ck, int slot, const 
       MsmWindows mw{1, {0, 0}, {1, 0}};
       CHK(run_msm_core<Cv>(c, s, tl, 1, (size_t)CK_ROWS * m + 16, mw, ck->pts.template as<Affine<Cv>>(),
                            ck->inf.template as<uint8_t>()));
-      st = s.stream;  // the tail lane
     }
     Launch<Cv>::encode_points(st, s.res.template as<Xyzz<Cv>>(), 1, s.outb.template as<uint8_t>());
     HIPCHK(hipGetLastError());
@@ -1509,7 +1444,7 @@ int kzgmi_commit(kzgmi_ctx* c, const kzgmi_ck* ck, const uint8_t* coeffs, size_t
   CHK(slot0_idle(c));
   Slot& s = c->slots[0];
   CHK(s.stage.ensure(m * 32));
-  CHK(begin_job(c, s, LANE_FRONT));  // the commit's job starts in the same lane, behind this copy
+  CHK(begin_job(s));  // the commit's job starts in the same lane, behind this copy
   HIPCHK(hipMemcpyAsync(s.stage.p, coeffs, m * 32, hipMemcpyHostToDevice, s.stream));
   return kzgmi_commit_device(c, ck, s.stage.p, m, out);
 }
@@ -1598,7 +1533,7 @@ int kzgmi_msm_g1(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* points, const u
   CHK(s.stage.ensure(n * (gb + 32)));
   uint8_t* dp = s.stage.template as<uint8_t>();
   uint8_t* ds = dp + n * gb;
-  CHK(begin_job(c, s, LANE_FRONT));  // the MSM's job starts in the same lane, behind these copies
+  CHK(begin_job(s));  // the MSM's job starts in the same lane, behind these copies
   HIPCHK(hipMemcpyAsync(dp, points, n * gb, hipMemcpyHostToDevice, s.stream));
   HIPCHK(hipMemcpyAsync(ds, scalars, n * 32, hipMemcpyHostToDevice, s.stream));
   return kzgmi_msm_g1_device(c, curve, dp, ds, n, out);
@@ -1634,7 +1569,7 @@ int kzgmi_batch_partial_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slo
     using Cv = decltype(cv);
     if (n == 0) {  // empty shard: both partials are the point at infinity (zz = 0)
       CHK(s.flags.ensure(16));
-      CHK(begin_job(c, s, LANE_TAIL));
+      CHK(begin_job(s));
       HIPCHK(hipMemsetAsync(d_partial_out, 0, 2 * sizeof(Xyzz<Cv>), s.stream));
       HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));  // a chained combine keeps the error word
       CHK(sync_job(s));
@@ -1674,7 +1609,7 @@ int kzgmi_batch_combine_device_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slo
     using XY = Xyzz<Cv>;
     CHK(s.res.ensure(2 * sizeof(XY)));
     CHK(s.flags.ensure(16));
-    CHK(begin_job(c, s, LANE_TAIL));  // chained: the lane the partial ended in
+    CHK(begin_job(s));  // chained: the lane the partial ended in
     hipStream_t st = s.stream;
     if (!chain) {
       HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
@@ -1717,7 +1652,7 @@ int kzgmi_g1_validate_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_poin
     CHK(s.pts.ensure(n * sizeof(Affine<Cv>)));
     CHK(s.inf.ensure(n));
     CHK(s.flags.ensure(16));
-    CHK(begin_job(c, s, LANE_FRONT));
+    CHK(begin_job(s));
     hipStream_t st = s.stream;
     HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
     uint32_t* err = s.flags.template as<uint32_t>() + 1;
@@ -1751,7 +1686,7 @@ static int fs_chunk_digests_enqueue(kzgmi_ctx* c, kzgmi_curve curve, const void*
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     const uint32_t* dg = nullptr;
-    CHK(begin_job(c, s, LANE_FRONT));
+    CHK(begin_job(s));
     CHK(enqueue_fs_digests<Cv>(s, dC, dpi, dz, dy, n, index_offset, (flags & KZGMI_FLAG_COMPRESSED) != 0, &dg));
     const size_t nch = (n + FS_CHUNK - 1) / FS_CHUNK;
     HIPCHK(hipMemcpyAsync(d_out, dg, nch * 32, hipMemcpyDeviceToDevice, s.stream));
@@ -1775,7 +1710,7 @@ int kzgmi_fs_challenge_from_digests_device(kzgmi_ctx* c, kzgmi_curve curve, cons
   if (s.pending) return fail(KZGMI_ERR_ARG, "slot 0 busy: call kzgmi_slot_wait first");
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
-    CHK(begin_job(c, s, LANE_FRONT));
+    CHK(begin_job(s));
     CHK(enqueue_fs_challenge<Cv>(s, (const uint32_t*)d_digests, (uint32_t)nchunks, n_total));
     uint32_t w[8];
     HIPCHK(hipMemcpyAsync(w, s.chal.p, 32, hipMemcpyDeviceToHost, s.stream));
@@ -1797,7 +1732,7 @@ int kzgmi_fs_challenge_device(kzgmi_ctx* c, kzgmi_curve curve, const void* dC, c
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     const uint32_t* dg = nullptr;
-    CHK(begin_job(c, s, LANE_FRONT));
+    CHK(begin_job(s));
     CHK(enqueue_fs_digests<Cv>(s, dC, dpi, dz, dy, n, 0, (flags & KZGMI_FLAG_COMPRESSED) != 0, &dg));
     CHK(enqueue_fs_challenge<Cv>(s, dg, (uint32_t)((n + FS_CHUNK - 1) / FS_CHUNK), n));
     uint32_t w[8];
@@ -1817,7 +1752,7 @@ int kzgmi_g1_compress_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_poin
   CHK(slot0_idle(c));
   Slot& s = c->slots[0];
   return dispatch(curve, [&](auto cv) -> int {
-    CHK(begin_job(c, s, LANE_FRONT));
+    CHK(begin_job(s));
     Launch<decltype(cv)>::compress_points(s.stream, (const uint8_t*)d_points, (uint32_t)n, (uint8_t*)d_out);
     HIPCHK(hipGetLastError());
     CHK(sync_job(s));
@@ -1861,7 +1796,7 @@ int kzgmi_msm_partial_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, co
     if (n == 0) {
       CHK(s.flags.ensure(16));
       CHK(sync_slot(s));  // host_flags may still be a copy target
-      CHK(begin_job(c, s, LANE_TAIL));
+      CHK(begin_job(s));
       HIPCHK(hipMemsetAsync(d_partial_out, 0, sizeof(Xyzz<Cv>), s.stream));  // ZZ = 0: infinity
       HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));  // a chained combine keeps the error word
       CHK(end_job(s));
@@ -1898,7 +1833,7 @@ int kzgmi_msm_combine_device_async(kzgmi_ctx* c, kzgmi_curve curve, int slot, co
     CHK(s.res.ensure(2 * sizeof(XY)));
     CHK(s.outb.ensure(gb));
     CHK(s.flags.ensure(16));
-    CHK(begin_job(c, s, LANE_TAIL));  // chained: the lane the partial ended in
+    CHK(begin_job(s));  // chained: the lane the partial ended in
     if (!chain) HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));
     Launch<Cv>::sum_partials(s.stream, (const XY*)d_partials, (uint32_t)n_parts, 1, 1, s.res.template as<XY>(),
                              s.flags.template as<uint32_t>() + 1);
@@ -1928,7 +1863,7 @@ int kzgmi_msm_combine_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_part
     CHK(s.res.ensure(2 * sizeof(XY)));
     CHK(s.outb.ensure(gb));
     CHK(s.flags.ensure(16));
-    CHK(begin_job(c, s, LANE_TAIL));
+    CHK(begin_job(s));
     HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));
     Launch<Cv>::sum_partials(s.stream, (const XY*)d_partials, (uint32_t)n_parts, 1, 1, s.res.template as<XY>(),
                              s.flags.template as<uint32_t>() + 1);
@@ -1959,7 +1894,7 @@ int kzgmi_pairing(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uint
     CHK(s.stage.ensure(96 + 32));
     CHK(s.outb.ensure(96));
     uint8_t* dp = s.stage.template as<uint8_t>();
-    CHK(begin_job(c, s, LANE_FRONT));  // the MSM's job starts in the same lane, behind these copies
+    CHK(begin_job(s));  // the MSM's job starts in the same lane, behind these copies
     HIPCHK(hipMemcpyAsync(dp, g1, 96, hipMemcpyHostToDevice, s.stream));
     HIPCHK(hipMemcpyAsync(dp + 96, kInv3, 32, hipMemcpyHostToDevice, s.stream));
     CHK(enqueue_msm<Cv>(c, s, dp, dp + 96, 1, /*allow_glv=*/false));
@@ -1984,7 +1919,7 @@ int kzgmi_pairing(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g1, const uint
     memcpy(h.data(), g1, gb1);
     memcpy(h.data() + gb1, g2, gb2);
     memcpy(h.data() + gb1 + gb2, g2, gb2);
-    CHK(begin_job(c, s, LANE_FRONT));
+    CHK(begin_job(s));
     hipStream_t st = s.stream;
     uint8_t* d = s.stage.template as<uint8_t>();
     Line<Cv>* lines = c->lines_tmp.template as<Line<Cv>>();
@@ -2012,7 +1947,7 @@ int kzgmi_gen_g1(kzgmi_ctx* c, kzgmi_curve curve, const void* d_scalars, size_t 
   return dispatch(curve, [&](auto cv) -> int {
     using Cv = decltype(cv);
     Slot& s = c->slots[0];
-    CHK(begin_job(c, s, LANE_FRONT));
+    CHK(begin_job(s));
     CHK(ensure_table<Cv>(c, s.stream));
     CHK(s.flags.ensure(16));
     HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, s.stream));
@@ -2033,7 +1968,7 @@ int kzgmi_gen_tuples(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* tau32, cons
     using Cv = decltype(cv);
     using FrF = Fp<typename Cv::FrP>;
     Slot& s = c->slots[0];
-    CHK(begin_job(c, s, LANE_FRONT));
+    CHK(begin_job(s));
     CHK(ensure_table<Cv>(c, s.stream));
     FrF tau;
     for (int k = 0; k < 8; ++k)
@@ -2075,7 +2010,7 @@ int kzgmi_g2_mul(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* g2, const uint8
       if (k[j] < Cv::FrP::MOD[j]) break;
       if (k[j] > Cv::FrP::MOD[j] || j == 0) return fail(KZGMI_ERR_SCALAR, "k >= r");
     }
-    CHK(begin_job(c, s, LANE_FRONT));
+    CHK(begin_job(s));
     hipStream_t st = s.stream;
     uint8_t* d = s.stage.template as<uint8_t>();
     HIPCHK(hipMemcpyAsync(d, g2, gb, hipMemcpyHostToDevice, st));
@@ -2102,7 +2037,7 @@ int kzgmi_probe_fpmul(kzgmi_ctx* c, kzgmi_curve curve, double* muls_per_s) {
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
-    CHK(begin_job(c, s, LANE_FRONT));
+    CHK(begin_job(s));
     Launch<Cv>::fpmul_probe(s.stream, blocks, 16, c->tmp.template as<uint32_t>());  // warm-up
     HIPCHK(hipEventRecord(e0, s.stream));
     Launch<Cv>::fpmul_probe(s.stream, blocks, iters, c->tmp.template as<uint32_t>());
@@ -2182,7 +2117,7 @@ int kzgmi_partial_encode_device(kzgmi_ctx* c, kzgmi_curve curve, const void* d_r
     Slot& s = c->slots[0];
     const size_t gb = g1_bytes(Cv::ID);
     CHK(s.outb.ensure(count * gb));
-    CHK(begin_job(c, s, LANE_TAIL));
+    CHK(begin_job(s));
     Launch<Cv>::encode_points(s.stream, (const Xyzz<Cv>*)d_records, (uint32_t)count, s.outb.template as<uint8_t>());
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out, s.outb.p, count * gb, hipMemcpyDeviceToHost, s.stream));
@@ -2251,7 +2186,7 @@ int wait_all(kzgmi_ctx* c, int started) {
 // runtime orders a null-stream peer copy against a non-blocking stream
 int gather_records(kzgmi_ctx* c, size_t rec) {
   CHK(set_dev(c));
-  CHK(begin_job(c, c->slots[0], LANE_TAIL));  // the combine's job starts in the same lane, behind these copies
+  CHK(begin_job(c->slots[0]));  // the combine's job starts in the same lane, behind these copies
   for (size_t d = 1; d <= c->peers.size(); ++d) {
     kzgmi_ctx* p = c->peers[d - 1];
     HIPCHK(hipMemcpyPeerAsync((uint8_t*)c->gath.p + d * rec, c->device, p->gath.p, p->device, rec, c->slots[0].stream));
@@ -2303,7 +2238,7 @@ int batch_multi(kzgmi_ctx* c, const kzgmi_srs* srs, const void* const* dC, const
       CHK(set_dev(p));
       CHK(sync_slot(p->slots[0]));
       CHK(set_dev(c));
-      CHK(begin_job(c, c->slots[0], LANE_FRONT));  // the challenge's job follows in this lane
+      CHK(begin_job(c->slots[0]));  // the challenge's job follows in this lane
       HIPCHK(hipMemcpyPeerAsync((uint8_t*)c->mdig_all.p + at * 32, c->device, p->mdig.p, p->device, nch * 32,
                                 c->slots[0].stream));
       at += nch;
@@ -2398,7 +2333,7 @@ int batch_multi_host(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commitme
     ppi[d] = base + nd[d] * gb;
     pz[d] = base + 2 * nd[d] * gb;
     py[d] = base + 2 * nd[d] * gb + 32 * nd[d];
-    CHK(begin_job(p, s, LANE_FRONT));  // the shard's job starts in the same lane, behind these copies
+    CHK(begin_job(s));  // the shard's job starts in the same lane, behind these copies
     if (nd[d]) {
       HIPCHK(hipMemcpyAsync((void*)pC[d], commitments + lo * gb, nd[d] * gb, hipMemcpyHostToDevice, s.stream));
       HIPCHK(hipMemcpyAsync((void*)ppi[d], proofs + lo * gb, nd[d] * gb, hipMemcpyHostToDevice, s.stream));
@@ -2424,7 +2359,7 @@ int msm_multi_host(kzgmi_ctx* c, kzgmi_curve curve, const uint8_t* points, const
     CHK(s.stage.ensure(nd[d] * (gb + 32)));
     pp[d] = s.stage.p;
     ps[d] = s.stage.template as<uint8_t>() + nd[d] * gb;
-    CHK(begin_job(p, s, LANE_FRONT));
+    CHK(begin_job(s));
     if (nd[d]) {
       HIPCHK(hipMemcpyAsync((void*)pp[d], points + lo * gb, nd[d] * gb, hipMemcpyHostToDevice, s.stream));
       HIPCHK(hipMemcpyAsync((void*)ps[d], scalars + lo * 32, nd[d] * 32, hipMemcpyHostToDevice, s.stream));

@@ -28,7 +28,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 QUIET = ("--no-cpu --msm-steps 0 --trusted-steps 0 --fs-steps 0 --commit-steps 0 --compressed-steps 0 "
-         "--cfg4-msms 0 --h2d-steps 0 --bn254-steps 0 --shard17-steps 0 --repeats 1")
+         "--cfg4-msms 0 --h2d-steps 0 --bn254-steps 0 --shard17-steps 0 --repeats 1 --default-queues-steps 0 --detail-file ''")
 
 
 def parse_variant(spec):
