@@ -11,14 +11,15 @@
 //     acc_j <- (acc_j >> 29) + (acc_{j+1} mod 2^29)   (divide the row's number by 2^29: DPP row_shl)
 // so a product is ~160 instructions on the critical path instead of ~650.  The 4 rows of a wave
 // compute up to 4 independent products at once (operands selected per row, results shared with
-// ds_bpermute): a Jacobian doubling is 3 product steps (8 products), an XYZZ addition 4.
+// ds_bpermute): an XYZZ doubling is 3 product steps (9 products), an XYZZ addition 4.
 //
 // Representation: limbs are SIGNED and redundant (|limb| < 2^29 + 4 after lp_norm); values are
 // integers congruent to the element, never reduced: a - b is a limb-wise subtraction, no bias.
 // Bound rule (params_lp_gen.hpp HEAD): |a|, |b| < 2^HEAD p  =>  |lp_mul(a, b)| < 1.5 p
 // (|a b + m p| / R with m < R); the formulas below keep every product input below 64 p.
-// Zero tests and outputs canonicalise in uniform scalar code (lp_canon: quotient estimate in
-// double precision from the top limbs, exact multi-limb correction).
+// Zero tests are row-local (lp_row_is_zero: reduce below p, carry passes, ballot); outputs
+// canonicalise in uniform scalar code (lp_canon: quotient estimate in double precision from the
+// top limbs, exact multi-limb correction).
 // Reference: none (LICENSE only); checked through every MSM / batch parity test (the window
 // combination of every MSM runs here) and kzgmi_selftest_lp.
 #pragma once
@@ -163,8 +164,6 @@ template <class Cv>
 KZ_DEV int32_t lp_row(const LpCtx<Cv>& c, int32_t v, int r) { return __builtin_amdgcn_ds_bpermute(c.src[r], v); }
 
 template <class Cv>
-KZ_DEV int32_t lp_step1(const LpCtx<Cv>& c, int32_t a0, int32_t b0) { return lp_mul(c, a0, b0); }
-template <class Cv>
 KZ_DEV void lp_step2(const LpCtx<Cv>& c, int32_t& r0, int32_t a0, int32_t b0, int32_t& r1, int32_t a1, int32_t b1) {
   const int32_t p = lp_mul(c, lp_sel(c, a0, a1, a0, a1), lp_sel(c, b0, b1, b0, b1));
   r0 = lp_row(c, p, 0);
@@ -238,16 +237,6 @@ KZ_DEV void lp_canon(int32_t v, int64_t (&l)[LpQ<Cv>::N]) {
   if (top >= 0) addmul(-1);
 }
 
-template <class Cv>
-KZ_DEV bool lp_is_zero(int32_t v) {
-  int64_t l[LpQ<Cv>::N];
-  lp_canon<Cv>(v, l);
-  int64_t o = 0;
-#pragma unroll
-  for (int j = 0; j < LpQ<Cv>::N; ++j) o |= l[j];
-  return o == 0;
-}
-
 // canonical limbs -> the 32-bit-limb words of field.hpp
 template <class Cv>
 KZ_DEV Fp<typename Cv::FpP> lp_pack(const int64_t (&l)[LpQ<Cv>::N]) {
@@ -292,11 +281,6 @@ KZ_DEV int32_t lp_raw_from_words(const uint32_t* w) {
 
 // ---------------------------------------------------------------------------- G1 (a = 0)
 template <class Cv>
-struct LpJac {  // Jacobian: x = X / Z^2, y = Y / Z^3
-  int32_t x, y, z;
-  bool inf;
-};
-template <class Cv>
 struct LpXyzz {  // x = X / ZZ, y = Y / ZZZ
   int32_t x, y, zz, zzz;
   bool inf;
@@ -334,28 +318,6 @@ KZ_DEV void lp_store_xyzz(const LpCtx<Cv>& c, Xyzz<Cv>* dst, const LpXyzz<Cv>& p
   if (threadIdx.x == 0) *dst = o;
 }
 
-// 2P in a = 0 Jacobian coordinates, 3 product steps:
-//   A = X^2, B = Y^2, T = Y Z | C = B^2, D0 = (X + B)^2, AA = A^2 | A3 = A AA, ED = E D
-//   D = 2 (D0 - A - C), E = 3 A, X3 = E^2 - 2 D = 9 AA - 2 D,
-//   Y3 = E (D - X3) - 8 C = 3 ED - 27 A3 - 8 C, Z3 = 2 T          (dbl-2009-l, re-associated)
-// Bounds (inputs < 64 p): products < 1.5 p, D < 9 p, E < 4.5 p, |X3| < 32 p, |Y3| < 58 p, Z3 < 3 p.
-template <class Cv>
-KZ_DEV LpJac<Cv> lp_jac_dbl(const LpCtx<Cv>& c, const LpJac<Cv>& p) {
-  int32_t A, B, T, C, D0, AA, A3, ED;
-  lp_step3(c, A, p.x, p.x, B, p.y, p.y, T, p.y, p.z);
-  const int32_t XB = lp_add(c, p.x, B);
-  lp_step3(c, C, B, B, D0, XB, XB, AA, A, A);
-  const int32_t D = lp_dbl(c, lp_sub(c, lp_sub(c, D0, A), C));
-  const int32_t E = lp_mul3(c, A);
-  lp_step2(c, A3, A, AA, ED, E, D);
-  LpJac<Cv> r;
-  r.x = lp_sub(c, lp_mul9(c, AA), lp_dbl(c, D));
-  r.y = lp_sub(c, lp_sub(c, lp_mul3(c, ED), lp_mul3(c, lp_mul9(c, A3))), lp_mul8(c, C));
-  r.z = lp_dbl(c, T);
-  r.inf = p.inf;  // no 2-torsion on these curves: 2P = O only for P = O
-  return r;
-}
-
 // 2P in XYZZ (dbl-2008-s-1), 3 product steps
 template <class Cv>
 KZ_DEV LpXyzz<Cv> lp_xyzz_dbl(const LpCtx<Cv>& c, const LpXyzz<Cv>& p) {
@@ -382,8 +344,11 @@ KZ_DEV LpXyzz<Cv> lp_xyzz_add(const LpCtx<Cv>& c, const LpXyzz<Cv>& p, const LpX
   int32_t U1, U2, S1, S2;
   lp_step4(c, U1, p.x, q.zz, U2, q.x, p.zz, S1, p.y, q.zzz, S2, q.y, p.zzz);
   const int32_t P = lp_sub(c, U2, U1), R = lp_sub(c, S2, S1);
-  if (lp_is_zero<Cv>(P)) {
-    if (lp_is_zero<Cv>(R)) return lp_xyzz_dbl(c, p);
+  // row-local zero tests (|P|, |R| < 3 p; every row holds the same value): a reduction and carry
+  // passes on the row, not a serial readlane canonicalisation (lp_canon): with the XYZZ running
+  // sum, k_window_combine 0.436 -> 0.369 ms (profiles/r05/ab_window_combine.txt)
+  if (lp_row_is_zero(c, P)) {
+    if (lp_row_is_zero(c, R)) return lp_xyzz_dbl(c, p);
     LpXyzz<Cv> o = p;
     o.inf = true;
     return o;
@@ -398,31 +363,6 @@ KZ_DEV LpXyzz<Cv> lp_xyzz_add(const LpCtx<Cv>& c, const LpXyzz<Cv>& p, const LpX
   r.zz = ZZ3;
   r.zzz = ZZZ3;
   r.inf = false;
-  return r;
-}
-
-// Jacobian -> XYZZ: ZZ = Z^2, ZZZ = Z^3 (2 steps)
-template <class Cv>
-KZ_DEV LpXyzz<Cv> lp_xyzz_from_jac(const LpCtx<Cv>& c, const LpJac<Cv>& p) {
-  LpXyzz<Cv> r;
-  r.x = p.x;
-  r.y = p.y;
-  r.zz = lp_step1(c, p.z, p.z);
-  r.zzz = lp_step1(c, r.zz, p.z);
-  r.inf = p.inf;
-  return r;
-}
-
-// XYZZ -> Jacobian: Z = ZZ ZZZ, X = X ZZ ZZZ^2, Y = Y ZZZ^4 (3 steps)
-template <class Cv>
-KZ_DEV LpJac<Cv> lp_jac_from_xyzz(const LpCtx<Cv>& c, const LpXyzz<Cv>& p) {
-  int32_t Z3sq, XZ, XYt, YZ;
-  LpJac<Cv> r;
-  lp_step3(c, Z3sq, p.zzz, p.zzz, r.z, p.zz, p.zzz, XZ, p.x, p.zz);
-  lp_step2(c, r.x, XZ, Z3sq, YZ, p.y, Z3sq);
-  r.y = lp_step1(c, YZ, Z3sq);
-  (void)XYt;
-  r.inf = p.inf;
   return r;
 }
 
