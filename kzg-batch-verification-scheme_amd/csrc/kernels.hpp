@@ -303,16 +303,36 @@ __global__ void k_pairing_one(const Affine<Cv>* __restrict__ p, const uint8_t* _
   }
 }
 
-// XYZZ -> G1 encoding (count points, one thread each)
+// XYZZ -> G1 encoding, one wave per point: the record's words are made wave-uniform
+// (readfirstlane), so the conversion's inversion compiles to scalar code instead of one lane's
+// vector code under an exec mask (the same change took the pairing's inversion round 245 K -> ~140 K
+// cycles, profiles/r05/ab_pairing_inv_uniform.txt); lane 0 stores.
 template <class Cv>
-__global__ void k_encode_points(const Xyzz<Cv>* __restrict__ res, uint32_t count, uint8_t* __restrict__ out) {
+KZ_DEV void fp_uniform(Fp<typename Cv::FpP>& a) {
+#pragma unroll
+  for (int k = 0; k < Cv::FpP::N; ++k) a.v[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.v[k]);
+}
+template <class Cv>
+__global__ void __launch_bounds__(64) k_encode_points(const Xyzz<Cv>* __restrict__ res, uint32_t count,
+                                                      uint8_t* __restrict__ out) {
   using P = typename Cv::FpP;
   constexpr int NW = 2 * P::N;
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = blockIdx.x;
   if (i >= count) return;
+  Xyzz<Cv> p = load_xyzz(&res[i]);
+  fp_uniform<Cv>(p.x);
+  fp_uniform<Cv>(p.y);
+  fp_uniform<Cv>(p.zz);
+  fp_uniform<Cv>(p.zzz);
   Affine<Cv> a;
   uint32_t w[NW];
-  if (!xyzz_to_affine(load_xyzz(&res[i]), a)) {
+  const bool finite = !p.is_inf();
+  if (finite) {  // xyzz_to_affine with the inversion inlined (its out-of-line form takes VGPR arguments)
+    const auto I = fp_inv(fp_mul(p.zz, p.zzz));
+    a.x = fp_mul(p.x, fp_mul(p.zzz, I));
+    a.y = fp_mul(p.y, fp_mul(p.zz, I));
+  }
+  if (!finite) {
 #pragma unroll
     for (int k = 0; k < NW; ++k) w[k] = 0;
     if constexpr (Cv::ID == 0) w[0] = 0x40u;
@@ -320,7 +340,7 @@ __global__ void k_encode_points(const Xyzz<Cv>* __restrict__ res, uint32_t count
     fp_to_be_words(fp_from_mont(a.x), w, 0);
     fp_to_be_words(fp_from_mont(a.y), w, P::N);
   }
-  store_words(out + (size_t)i * 4 * NW, w);
+  if (threadIdx.x == 0) store_words(out + (size_t)i * 4 * NW, w);
 }
 
 // A shard partial record that failed on its own device (or rank) is marked, not dropped: its x

@@ -120,7 +120,7 @@ void Launch<Cv>::scalar_prep_pow(hipStream_t st, const void* pow, uint64_t index
 }
 template <class Cv>
 void Launch<Cv>::encode_points(hipStream_t st, const XY* res, uint32_t count, uint8_t* out) {
-  k_encode_points<Cv><<<grid_for(count, 64), 64, 0, st>>>(res, count, out);
+  if (count) k_encode_points<Cv><<<count, 64, 0, st>>>(res, count, out);
 }
 template <class Cv>
 void Launch<Cv>::sum_partials(hipStream_t st, const XY* parts, uint32_t nparts, uint32_t stride, uint32_t nout, XY* out,
