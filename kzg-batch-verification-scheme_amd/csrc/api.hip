@@ -105,6 +105,7 @@ struct Slot {
   DevBuf fs_leaves, fs_tmp, fs_top, pow, chal;  // Fiat-Shamir / powers-of-r randomisers
   DevBuf glv_r, glv_s, glv_t;                    // GLV half scalars (glv.hpp): [h0 x n | h1 x n]
   DevBuf digits;                                 // signed window digit codes of every term (msm.hpp)
+  DevBuf small_nodes, small_flags;               // small calls' summation tree (msm_small.hpp)
   int* host_flags = nullptr;  // pinned: [ok, err]
   uint8_t* host_out = nullptr;  // pinned: encoded MSM result of an async MSM job
   uint8_t* ring[2] = {};        // pinned staging of pageable host inputs (kRingBytes each, lazily)
@@ -145,6 +146,7 @@ struct kzgmi_ctx {
   size_t acc_queue_from = ACC_QUEUE_FROM;    // KZGMI_ACC_QUEUE_FROM: calls with fewer entries keep the static grid
   bool sort_split = false;     // KZGMI_SORT_SPLIT: split coarse-pass entries at every size (tests)
   int wbits_env = 0;           // KZGMI_WBITS: 13 or 16 forces the window width (tests, A/B)
+  uint32_t small_terms = 4096;  // BLS12-381 calls of at most this many terms: msm_small.hpp (KZGMI_SMALL_TERMS; 0: never)
   double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
   // host-buffer inputs of every slot are copied on ONE stream, in submission order: each
   // batch's copy then gets the whole link and completes first-in first-out (16 concurrent
@@ -283,6 +285,59 @@ int map_device_err(uint32_t e) {
   }
 }
 
+// ------------------------------------------------------------------------------ small MSMs
+// The terms of tl (classes in order) as one wave each, MSM m's leaves in class order; the tree's
+// stored nodes and arrival counters per MSM, level after level (msm_small.hpp).
+template <class Cv>
+int run_small_msm(kzgmi_ctx* c, Slot& s, const TermList& tl, const MsmWindows& mw, const Affine<Cv>* pts,
+                  const uint8_t* inf, bool own_pts, bool dry) {
+  SmallPlan sp{};
+  sp.nclass = tl.nclass;
+  sp.nmsm = mw.nmsm;
+  uint32_t terms = 0, leaves[2] = {0, 0};
+  for (uint32_t k = 0; k < tl.nclass; ++k) {
+    const uint32_t m = mw.nmsm > 1 && tl.c[k].set_base >= mw.set_base[1] ? 1 : 0;
+    sp.term_base[k] = terms;
+    sp.msm[k] = m;
+    sp.leaf_base[k] = leaves[m];
+    terms += tl.c[k].count;
+    leaves[m] += tl.c[k].count;
+  }
+  uint32_t nodes = 0, flags = 0;
+  for (uint32_t m = 0; m < 2; ++m) {
+    sp.count[m] = leaves[m];
+    sp.node_base[m] = nodes;
+    sp.flag_base[m] = flags;
+    for (uint32_t cnt = leaves[m]; cnt > 1; cnt = (cnt + 1) >> 1) {
+      nodes += cnt;
+      flags += (cnt + 1) >> 1;
+    }
+  }
+  CHK(s.small_nodes.ensure((size_t)(nodes + 1) * SMALL_NODE_WORDS * 4));
+  CHK(s.small_flags.ensure((size_t)(flags + 1) * 4));
+  CHK(s.res.ensure(2 * sizeof(Xyzz<Cv>)));
+  if (dry) return 0;
+  Roctx rx("kzgmi.msm.small");
+  hipStream_t st = s.stream;
+  using L = Launch<Cv>;
+  if (!pts) pts = s.pts.template as<Affine<Cv>>();
+  if (!inf) inf = s.inf.template as<uint8_t>();
+  if (own_pts) {  // the slot's points into the radix-29 slots the kernel reads
+    uint32_t npts = 0;
+    for (uint32_t k = 0; k < tl.nclass; ++k)
+      if (tl.c[k].count) npts = std::max(npts, tl.c[k].pt_base + tl.c[k].count);
+    L::pts_to29(st, s.pts.template as<Affine<Cv>>(), npts);
+  }
+  mark(c, s, PH_SORT + 1);
+  L::small_msm(st, tl, sp, terms, pts, inf, s.small_nodes.template as<uint32_t>(), s.small_flags.template as<uint32_t>(),
+               flags + 1, s.res.template as<Xyzz<Cv>>());
+  mark(c, s, PH_ACCUM + 1);
+  mark(c, s, PH_REDUCE + 1);
+  mark(c, s, PH_COMBINE + 1);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 // ------------------------------------------------------------------------------ MSM core
 template <class Cv>
 int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, size_t emax, const MsmWindows& mw,
@@ -295,6 +350,12 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   // here unless convert_points stored them in it already (pts29); explicit pts (commit-key
   // rows) are stored in that format already (kzgmi_ck_load)
   const bool own_pts = pts == nullptr && !pts29;
+  // small calls: one wave per term and a summation tree (msm_small.hpp) instead of buckets
+  {
+    bool small = Cv::ID == 0 && c->small_terms && tl_in.total <= c->small_terms && mw.nmsm <= 2;
+    for (uint32_t k = 0; k < tl_in.nclass; ++k) small = small && tl_in.c[k].win_off == 0;
+    if (small) return run_small_msm<Cv>(c, s, tl_in, mw, pts, inf, own_pts, dry);
+  }
   TermList tl = tl_in;  // + each class's offset in the digit array
   size_t ndig = 0;
   for (uint32_t k = 0; k < tl.nclass; ++k) {
@@ -859,6 +920,7 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
   if (const char* e = getenv("KZGMI_ACC_QUEUE_FROM")) c->acc_queue_from = strtoull(e, nullptr, 10);
   if (const char* e = getenv("KZGMI_SORT_SPLIT")) c->sort_split = atoi(e) != 0;
   if (const char* e = getenv("KZGMI_WBITS")) c->wbits_env = atoi(e);
+  if (const char* e = getenv("KZGMI_SMALL_TERMS")) c->small_terms = (uint32_t)strtoul(e, nullptr, 10);
   // HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 unless set before the runtime
   // starts) and serialises the streams of one queue, so every slot in flight needs a queue of its
   // own (16 slots on 24 queues pipeline; 24 on 24 ran 3.6x slower).  The runtime keeps that many

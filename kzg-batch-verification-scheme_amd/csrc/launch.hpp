@@ -3,6 +3,7 @@
 // BLS12-381, 1 BN254), so the device code builds in parallel; api.hip only calls these.
 #pragma once
 #include "kernels.hpp"
+#include "msm_small.hpp"
 
 namespace kzgmi {
 
@@ -26,6 +27,10 @@ struct Launch {
   static void reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const uint32_t* acc29, XY* R, XY* U,
                      XY* scratch, XY* winsum, int wbits = WBITS);
   static void window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res, int wbits = WBITS);
+  // small calls (msm_small.hpp, BLS12-381): one wave per term + a counter tree; res (nmsm records)
+  // and flags are cleared here; nodes: small_node_words() words, flags: small_flag_words() words
+  static void small_msm(hipStream_t st, const TermList& tl, const SmallPlan& sp, uint32_t terms, const AF* pts,
+                        const uint8_t* inf, uint32_t* nodes, uint32_t* flags, uint32_t flag_words, XY* res);
   // ---- I/O and scalars (launch_io.hip)
   // to29: store in the accumulation's radix-29 format, for
   // points that go straight into run_msm_core(..., pts29 = true)

@@ -79,6 +79,18 @@ void Launch<Cv>::reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, con
 }
 
 template <class Cv>
+void Launch<Cv>::small_msm(hipStream_t st, const TermList& tl, const SmallPlan& sp, uint32_t terms, const AF* pts,
+                           const uint8_t* inf, uint32_t* nodes, uint32_t* flags, uint32_t flag_words, XY* res) {
+  (void)hipMemsetAsync(res, 0, (size_t)sp.nmsm * sizeof(XY), st);  // zz = 0: an MSM without terms is O
+  (void)hipMemsetAsync(flags, 0, (size_t)flag_words * 4, st);
+  if constexpr (Cv::ID == 0) {
+    if (terms) k_small_msm<Cv><<<terms, 64, 0, st>>>(tl, sp, pts, inf, nodes, flags, res);
+  } else {
+    (void)tl; (void)pts; (void)inf; (void)nodes; (void)terms;  // host never routes BN254 here (api.hip)
+  }
+}
+
+template <class Cv>
 void Launch<Cv>::window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res, int wbits) {
   with_wbits(wbits, [&](auto wb) {
     constexpr int WB = decltype(wb)::value;
@@ -96,5 +108,8 @@ template void Launch<KZ_CURVE_T>::reduce(hipStream_t, uint32_t, const uint32_t*,
                                          Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, int);
 template void Launch<KZ_CURVE_T>::window_combine(hipStream_t, const MsmWindows&, const Xyzz<KZ_CURVE_T>*,
                                                  Xyzz<KZ_CURVE_T>*, int);
+template void Launch<KZ_CURVE_T>::small_msm(hipStream_t, const TermList&, const SmallPlan&, uint32_t,
+                                            const Affine<KZ_CURVE_T>*, const uint8_t*, uint32_t*, uint32_t*, uint32_t,
+                                            Xyzz<KZ_CURVE_T>*);
 
 }  // namespace kzgmi

@@ -31,6 +31,39 @@ def ctx():
     c.close()
 
 
+def _context_with_env(**env):
+    """A kzgmi.Context created with the given environment overrides (read at creation)."""
+    import kzgmi
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return kzgmi.Context(0, 2)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def bctx():
+    """BLS12-381 calls of up to KZGMI_SMALL_TERMS terms take the one-wave-per-term path
+    (csrc/msm_small.hpp); this context never does, so the bucket method's small-size corner cases
+    stay covered."""
+    c = _context_with_env(KZGMI_SMALL_TERMS="0")
+    yield c
+    c.close()
+
+
+@pytest.fixture
+def pctx(request, ctx, bctx):
+    return ctx if request.param == "default" else bctx
+
+
+PATHS = pytest.mark.parametrize("pctx", ["default", "buckets"], indirect=True)
+
+
 @pytest.fixture(scope="module")
 def torch_dev():
     import torch
@@ -79,25 +112,27 @@ def test_pairing_golden(ctx, curve, golden):
         assert fp12_cube(curve, e) == h(g[key]), key
 
 
+@PATHS
 @pytest.mark.parametrize("curve", CURVES)
-def test_msm_golden(ctx, curve, golden):
+def test_msm_golden(pctx, curve, golden):
     g = golden("%s_msm.json" % curve)
     for case in g["cases"]:
-        got = ctx.msm_g1(curve, h(case["points"]), h(case["scalars"]))
+        got = pctx.msm_g1(curve, h(case["points"]), h(case["scalars"]))
         assert got.hex() == case["expected"], case["name"]
 
 
+@PATHS
 @pytest.mark.parametrize("curve", CURVES)
-def test_batch_golden(ctx, curve, golden):
+def test_batch_golden(pctx, curve, golden):
     for n in SIZES[curve]:
         g = golden("%s_batch_n%d.json" % (curve, n))
-        srs = ctx.load_srs(curve, h(g["g2"]), h(g["tau_g2"]))
+        srs = pctx.load_srs(curve, h(g["g2"]), h(g["tau_g2"]))
         for key in ["valid", "neg_flip_y", "neg_swap_proofs"]:
             src = g if key == "valid" else g[key]
             exp = g[key]
-            ok = ctx.batch_verify(srs, h(src["commitments"]), h(src["zs"]), h(src["ys"]), h(src["proofs"]),
+            ok = pctx.batch_verify(srs, h(src["commitments"]), h(src["zs"]), h(src["ys"]), h(src["proofs"]),
                                   seed=h(g["seed"]))
-            A, B = ctx.last_combination(curve)
+            A, B = pctx.last_combination(curve)
             assert A.hex() == exp["A"], (n, key)
             assert B.hex() == exp["B"], (n, key)
             assert ok == exp["ok"], (n, key)
@@ -162,19 +197,49 @@ def test_uncompressed_point_validation(ctx, curve, golden):
     assert ctx.msm_g1(curve, pts, sc) == O.msm_g1(curve, pts, sc, 5)
 
 
+@PATHS
 @pytest.mark.parametrize("curve", CURVES)
-def test_msm_random_vs_oracle(ctx, curve):
+def test_msm_random_vs_oracle(pctx, curve):
     C = pc.CURVES[curve]
     rng = random.Random(17)
     for n in [1, 2, 31, 33, 1000, 5000]:
         ks = [rng.randrange(C.r) for _ in range(n)]
         pts = O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(k) for k in ks), n)
         sc = b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(n))
-        assert ctx.msm_g1(curve, pts, sc) == O.msm_g1(curve, pts, sc, n), n
+        assert pctx.msm_g1(curve, pts, sc) == O.msm_g1(curve, pts, sc, n), n
 
 
+@PATHS
 @pytest.mark.parametrize("curve", CURVES)
-def test_msm_reduction_special_cases(ctx, curve):
+def test_msm_infinity_and_zero_terms(pctx, curve):
+    """Points at infinity, zero scalars, a point with its negation and repeated points among the
+    terms (the one-wave-per-term path's tree adds O + P, P + P and P + (-P) leaves), sizes around
+    the small path's term limit and a one-term MSM."""
+    C = pc.CURVES[curve]
+    rng = random.Random(97)
+    g1b = 2 * C.fp_bytes
+    inf_pt = (b"\x40" + b"\x00" * (g1b - 1)) if curve == "bls12_381" else b"\x00" * g1b
+    ks = [rng.randrange(1, C.r) for _ in range(8)]
+    base = O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(k) for k in ks + [C.r - ks[0]]), 9)
+    pt = lambda j: base[j * g1b:(j + 1) * g1b]  # noqa: E731
+    for n in [1, 2, 3, 7, 64, 513]:
+        terms, scal = [], []
+        for i in range(n):
+            kind = rng.randrange(6)
+            terms.append(inf_pt if kind == 0 else pt(8) if kind == 1 else pt(i % 8))
+            scal.append(0 if kind == 2 else rng.randrange(C.r))
+        pb = b"".join(terms)
+        sb = b"".join(pk.fr_to_bytes(x) for x in scal)
+        assert pctx.msm_g1(curve, pb, sb) == O.msm_g1(curve, pb, sb, n), n
+    # P and -P with equal scalars: the sum is O
+    pb = pt(0) + pt(8)
+    sb = pk.fr_to_bytes(12345) * 2
+    assert pctx.msm_g1(curve, pb, sb) == O.msm_g1(curve, pb, sb, 2)
+
+
+@PATHS
+@pytest.mark.parametrize("curve", CURVES)
+def test_msm_reduction_special_cases(pctx, curve):
     """Adjacent buckets whose sums cancel or coincide, so that the bucket-sum reduction's running
     sums hit P + (-P) = O and P + P (the doubling branch of its general addition):
     digits 8, 7, 6, 5 on P, -P, P, P (buckets 7..4 of the first segment half) = 12 P, plus the
@@ -203,7 +268,7 @@ def test_msm_reduction_special_cases(ctx, curve):
     for pts, sc in cases:
         pb = b"".join(pts)
         sb = b"".join(pk.fr_to_bytes(x) for x in sc)
-        assert ctx.msm_g1(curve, pb, sb) == O.msm_g1(curve, pb, sb, len(pts)), sc
+        assert pctx.msm_g1(curve, pb, sb) == O.msm_g1(curve, pb, sb, len(pts)), sc
 
 
 @pytest.mark.parametrize("curve", CURVES)
@@ -313,8 +378,9 @@ def test_accumulation_work_queue(curve, golden):
         c.close()
 
 
+@PATHS
 @pytest.mark.parametrize("curve", CURVES)
-def test_msm_cancelling_buckets(ctx, curve):
+def test_msm_cancelling_buckets(pctx, curve):
     """Buckets whose running sum returns to infinity mid-chunk (P + (-P)), then keeps adding
     (the accumulation's infinity flag, csrc/g1.hpp xyzz_acc_affine_lazy), doubling (P + P),
     pieces that cancel across chunk boundaries (k_fixup), and an all-cancelling MSM (result
@@ -334,15 +400,15 @@ def test_msm_cancelling_buckets(ctx, curve):
     ]
     try:
         for trusted in (False, True):  # True: points declared G1 members -> GLV split path
-            ctx.set_trusted_g1(trusted)
+            pctx.set_trusted_g1(trusted)
             for terms in cases:
                 n = len(terms)
                 pts = b"".join(terms)
                 for s in [5, C.r - 3, 0x10000]:
                     sc = b"".join(pk.fr_to_bytes(s) for _ in range(n))
-                    assert ctx.msm_g1(curve, pts, sc) == O.msm_g1(curve, pts, sc, n), (trusted, n, s)
+                    assert pctx.msm_g1(curve, pts, sc) == O.msm_g1(curve, pts, sc, n), (trusted, n, s)
     finally:
-        ctx.set_trusted_g1(False)
+        pctx.set_trusted_g1(False)
 
 
 @pytest.mark.parametrize("curve", CURVES)
