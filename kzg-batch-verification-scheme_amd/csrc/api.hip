@@ -146,7 +146,7 @@ struct kzgmi_ctx {
   size_t acc_queue_from = ACC_QUEUE_FROM;    // KZGMI_ACC_QUEUE_FROM: calls with fewer entries keep the static grid
   bool sort_split = false;     // KZGMI_SORT_SPLIT: split coarse-pass entries at every size (tests)
   int wbits_env = 0;           // KZGMI_WBITS: 13 or 16 forces the window width (tests, A/B)
-  uint32_t small_terms = 4096;  // BLS12-381 calls of at most this many terms: msm_small.hpp (KZGMI_SMALL_TERMS; 0: never)
+  uint32_t small_terms = 4096;  // calls of at most this many terms: msm_small.hpp (KZGMI_SMALL_TERMS; 0: never)
   double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
   // host-buffer inputs of every slot are copied on ONE stream, in submission order: each
   // batch's copy then gets the whole link and completes first-in first-out (16 concurrent
@@ -352,7 +352,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   const bool own_pts = pts == nullptr && !pts29;
   // small calls: one wave per term and a summation tree (msm_small.hpp) instead of buckets
   {
-    bool small = Cv::ID == 0 && c->small_terms && tl_in.total <= c->small_terms && mw.nmsm <= 2;
+    bool small = c->small_terms && tl_in.total <= c->small_terms && mw.nmsm <= 2;
     for (uint32_t k = 0; k < tl_in.nclass; ++k) small = small && tl_in.c[k].win_off == 0;
     if (small) return run_small_msm<Cv>(c, s, tl_in, mw, pts, inf, own_pts, dry);
   }

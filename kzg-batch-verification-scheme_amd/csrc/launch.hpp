@@ -27,7 +27,7 @@ struct Launch {
   static void reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const uint32_t* acc29, XY* R, XY* U,
                      XY* scratch, XY* winsum, int wbits = WBITS);
   static void window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res, int wbits = WBITS);
-  // small calls (msm_small.hpp, BLS12-381): one wave per term + a counter tree; res (nmsm records)
+  // small calls (msm_small.hpp): one wave per term + a counter tree; res (nmsm records)
   // and flags are cleared here; nodes: small_node_words() words, flags: small_flag_words() words
   static void small_msm(hipStream_t st, const TermList& tl, const SmallPlan& sp, uint32_t terms, const AF* pts,
                         const uint8_t* inf, uint32_t* nodes, uint32_t* flags, uint32_t flag_words, XY* res);

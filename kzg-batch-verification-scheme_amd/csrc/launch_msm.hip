@@ -83,11 +83,7 @@ void Launch<Cv>::small_msm(hipStream_t st, const TermList& tl, const SmallPlan& 
                            const uint8_t* inf, uint32_t* nodes, uint32_t* flags, uint32_t flag_words, XY* res) {
   (void)hipMemsetAsync(res, 0, (size_t)sp.nmsm * sizeof(XY), st);  // zz = 0: an MSM without terms is O
   (void)hipMemsetAsync(flags, 0, (size_t)flag_words * 4, st);
-  if constexpr (Cv::ID == 0) {
-    if (terms) k_small_msm<Cv><<<terms, 64, 0, st>>>(tl, sp, pts, inf, nodes, flags, res);
-  } else {
-    (void)tl; (void)pts; (void)inf; (void)nodes; (void)terms;  // host never routes BN254 here (api.hip)
-  }
+  if (terms) k_small_msm<Cv><<<terms, 64, 0, st>>>(tl, sp, pts, inf, nodes, flags, res);
 }
 
 template <class Cv>

@@ -13,7 +13,8 @@
 // two siblings to arrive adds the first's stored sum and climbs on; a node without a sibling
 // climbs alone.  No wave ever waits for another (no spinning): the grid drains in any schedule.
 // The root's wave writes res[m] (XYZZ, field.hpp form).  Points: the slot's radix-2^29 slots
-// (BLS12-381: 14 limbs of x then y, the lane-parallel limb layout with the same R = 2^406).
+// (BLS12-381: 14 limbs of x then y, the lane-parallel limb layout with the same R = 2^406;
+// BN254: x 2^261, y 2^261 packed in 32-bit words, one product each into the 2^290 form).
 // Reference: none (LICENSE only); the same sums as the bucket path (bit-exact A, B and MSM results
 // in every small-n parity test).
 #pragma once
@@ -113,8 +114,8 @@ template <class Cv>
 __global__ void __launch_bounds__(64) k_small_msm(TermList tl, SmallPlan sp, const Affine<Cv>* __restrict__ pts,
                                                   const uint8_t* __restrict__ inf, uint32_t* __restrict__ nodes,
                                                   uint32_t* __restrict__ flags, Xyzz<Cv>* __restrict__ res) {
-  static_assert(Cv::ID == 0, "radix-29 point slots are the lane-parallel limbs on BLS12-381 only");
   using Q = Fp29Of<Cv>;
+  using LQ = LpQ<Cv>;
   KZ_TAIL_PRIO();
   const LpCtx<Cv> c = lp_ctx<Cv>();
   const uint32_t t = blockIdx.x, j = threadIdx.x & 15;
@@ -126,16 +127,24 @@ __global__ void __launch_bounds__(64) k_small_msm(TermList tl, SmallPlan sp, con
   const uint32_t i = t - sp.term_base[k];
   const uint32_t m = sp.msm[k];
   uint32_t v = sp.leaf_base[k] + i;  // leaf of MSM m
-  // the term's point (radix-29 slot: x limbs 0..13, y limbs 14..27) and scalar (uniform words)
+  // the term's point in the accumulation's slot format (msm.hpp load_pt29) and scalar (uniform words)
   const uint32_t pi = C.pt_base + i;
   const uint32_t* slot = reinterpret_cast<const uint32_t*>(pts + pi);
-  LpXyzz<Cv> P;
-  P.x = j < (uint32_t)Q::N ? (int32_t)slot[j] : 0;
-  P.y = j < (uint32_t)Q::N ? (int32_t)slot[Q::N + j] : 0;
-  int32_t one = 0;  // R29 mod p (= the lane-parallel one: both R = 2^406)
+  int32_t one = 0, from29 = 0;  // per-lane limbs of R mod p and R^2 / R29 mod p
 #pragma unroll
-  for (int q = 0; q < Q::N; ++q)
-    if (j == (uint32_t)q) one = (int32_t)Q::ONE[q];
+  for (int q = 0; q < LQ::N; ++q)
+    if (j == (uint32_t)q) {
+      one = (int32_t)LQ::ONE[q];
+      from29 = (int32_t)LQ::FROM29[q];
+    }
+  LpXyzz<Cv> P;
+  if constexpr (kPackPts<Cv>) {  // BN254: x R29, y R29 as 32-bit words; R29 = 2^261, R = 2^290
+    lp_step2(c, P.x, lp_raw_from_words<Cv>(slot), from29, P.y, lp_raw_from_words<Cv>(slot + Cv::FpP::N), from29);
+  } else {  // BLS12-381: 14 radix-29 limbs of x, then of y; R29 = R = 2^406, the limbs as they are
+    static_assert(Q::N == LQ::N, "radix-29 slot limbs are the lane-parallel limbs");
+    P.x = j < (uint32_t)Q::N ? (int32_t)slot[j] : 0;
+    P.y = j < (uint32_t)Q::N ? (int32_t)slot[Q::N + j] : 0;
+  }
   P.zz = P.zzz = one;
   P.inf = inf[pi] != 0;
   const uint32_t* sw = C.scal + (size_t)C.scal_stride * i;
