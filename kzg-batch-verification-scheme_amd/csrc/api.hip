@@ -106,6 +106,7 @@ struct Slot {
   DevBuf glv_r, glv_s, glv_t;                    // GLV half scalars (glv.hpp): [h0 x n | h1 x n]
   DevBuf digits;                                 // signed window digit codes of every term (msm.hpp)
   DevBuf small_nodes, small_flags;               // small calls' summation tree (msm_small.hpp)
+  DevBuf acc29b, cntb, offb;                     // second bucket store of chunked batches (run_msm_core part)
   int* host_flags = nullptr;  // pinned: [ok, err]
   uint8_t* host_out = nullptr;  // pinned: encoded MSM result of an async MSM job
   uint8_t* ring[2] = {};        // pinned staging of pageable host inputs (kRingBytes each, lazily)
@@ -147,6 +148,8 @@ struct kzgmi_ctx {
   bool sort_split = false;     // KZGMI_SORT_SPLIT: split coarse-pass entries at every size (tests)
   int wbits_env = 0;           // KZGMI_WBITS: 13 or 16 forces the window width (tests, A/B)
   uint32_t small_terms = 4096;  // calls of at most this many terms: msm_small.hpp (KZGMI_SMALL_TERMS; 0: never)
+  int host_chunks_env = 0;       // KZGMI_HOST_CHUNKS: ranges of a synchronous host-buffer batch (batch_host_chunked)
+  int host_chunk_mode = 0;       // KZGMI_HOST_CHUNK_MODE=1: shard partials even where one bucket store applies
   double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
   // host-buffer inputs of every slot are copied on ONE stream, in submission order: each
   // batch's copy then gets the whole link and completes first-in first-out (16 concurrent
@@ -339,10 +342,14 @@ int run_small_msm(kzgmi_ctx* c, Slot& s, const TermList& tl, const MsmWindows& m
 }
 
 // ------------------------------------------------------------------------------ MSM core
+// part (chunked host-buffer batches, enqueue_batch_chunked): 0 the whole call; 1 the first point
+// range -- sort + accumulate into the slot's bucket store, no reduction; 2 a middle range -- into
+// the second store (acc29b, cntb, offb), merged into the first; 3 the last range -- as 2, then the
+// reduction and window combination of the merged store
 template <class Cv>
 int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, size_t emax, const MsmWindows& mw,
                  const Affine<Cv>* pts = nullptr, const uint8_t* inf = nullptr, bool pts29 = false,
-                 bool dry = false, int wbits = WBITS) {
+                 bool dry = false, int wbits = WBITS, int part = 0) {
   const uint32_t nbuckets = wbits == 13 ? Win<13>::NBUCKETS : Win<WBITS>::NBUCKETS;
   const uint32_t bins = wbits == 13 ? Win<13>::BINS : Win<WBITS>::BINS;
   const uint32_t rb_parts = wbits == 13 ? Win<13>::RB_PARTS : Win<WBITS>::RB_PARTS;
@@ -352,7 +359,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   const bool own_pts = pts == nullptr && !pts29;
   // small calls: one wave per term and a summation tree (msm_small.hpp) instead of buckets
   {
-    bool small = c->small_terms && tl_in.total <= c->small_terms && mw.nmsm <= 2;
+    bool small = part == 0 && c->small_terms && tl_in.total <= c->small_terms && mw.nmsm <= 2;
     for (uint32_t k = 0; k < tl_in.nclass; ++k) small = small && tl_in.c[k].win_off == 0;
     if (small) return run_small_msm<Cv>(c, s, tl_in, mw, pts, inf, own_pts, dry);
   }
@@ -399,6 +406,14 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   nchunks = (nchunks + 255) / 256 * 256;  // = the launched thread count (part arrays indexed by thread)
   CHK(s.cnt.ensure((size_t)NB * 4));
   CHK(s.off.ensure((size_t)NB * 4));
+  const bool second = part >= 2;  // this range accumulates into the second store, then merges
+  if (second) {
+    CHK(s.cntb.ensure((size_t)NB * 4));
+    CHK(s.offb.ensure((size_t)NB * 4));
+  }
+  DevBuf& CNT = second ? s.cntb : s.cnt;
+  DevBuf& OFF = second ? s.offb : s.off;
+  DevBuf& ACC = second ? s.acc29b : s.acc29;
   CHK(s.coarse.ensure((size_t)3 * nsets * bins * 4));
   CHK(s.ent.ensure(emax * 8));
   CHK(s.total.ensure(16));
@@ -408,6 +423,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   constexpr int W29 = kW29<Fp29Of<Cv>>;
   // buckets and bucket pieces are radix-29 records in acc29 (msm.hpp)
   CHK(s.acc29.ensure(((size_t)NB + 2 * nchunks) * W29 * 4));
+  if (second) CHK(s.acc29b.ensure(((size_t)NB + 2 * nchunks) * W29 * 4));
   const size_t seg_rec = (size_t)W29 * 4;  // a radix-29 record
   CHK(s.R.ensure((size_t)NB / SEG * seg_rec));
   CHK(s.U.ensure((size_t)NB / SEG * seg_rec * 2));  // U records, then the V records
@@ -425,13 +441,20 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
     L::pts_to29(st, s.pts.template as<Affine<Cv>>(), npts);
   }
   L::sort(st, tl, nsets, inf, s.digits.template as<uint32_t>(), s.coarse.template as<uint32_t>(), s.ent.template as<uint64_t>(), emax, c->sort_split,
-          s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), s.total.template as<uint32_t>(),
+          OFF.template as<uint32_t>(), CNT.template as<uint32_t>(), s.total.template as<uint32_t>(),
           s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(), wbits);
   mark(c, s, PH_SORT + 1);
   L::accumulate(st, nchunks, s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
-                s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts, s.acc29.template as<uint32_t>(), NB,
+                OFF.template as<uint32_t>(), CNT.template as<uint32_t>(), pts, ACC.template as<uint32_t>(), NB,
                 acc_threads, acc_threads ? s.accq.template as<uint32_t>() : nullptr);
+  if (second)
+    L::merge_buckets(st, NB, s.acc29.template as<uint32_t>(), s.cnt.template as<uint32_t>(),
+                     s.acc29b.template as<uint32_t>(), s.cntb.template as<uint32_t>());
   mark(c, s, PH_ACCUM + 1);
+  if (part == 1 || part == 2) {
+    HIPCHK(hipGetLastError());
+    return 0;  // more ranges follow
+  }
   L::reduce(st, nsets, s.cnt.template as<uint32_t>(), s.acc29.template as<uint32_t>(), s.R.template as<XY>(),
             s.U.template as<XY>(), s.scratch.template as<XY>(), s.winsum.template as<XY>(), wbits);
   mark(c, s, PH_REDUCE + 1);
@@ -891,6 +914,113 @@ int h2d(Slot& s, hipStream_t cs, void* dst, const void* src, size_t bytes) {
   return 0;
 }
 
+std::vector<size_t> split_units(size_t n, int D);  // below: balanced ranges in units of 4096 tuples
+
+// A synchronous host-buffer batch (no flags, BLS12-381: no GLV) as k point ranges on one slot:
+// range j's copy (the context's copy stream) overlaps the previous ranges' front end and
+// accumulation on the slot's stream, every range accumulates into the same bucket sets (a second
+// store merged into the first, run_msm_core parts 1..3), the G1 term joins the last range (its
+// scalar needs every range's r_i y_i), and one reduction, combination and pairing decide.  Same
+// r_i (global index), same sums as enqueue_batch; inputs land in the slot's stage buffer.
+template <class Cv>
+int enqueue_batch_chunked(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const uint8_t* hC, const uint8_t* hz,
+                          const uint8_t* hy, const uint8_t* hpi, size_t n, const Seed& seed, int k) {
+  using XY = Xyzz<Cv>;
+  using L = Launch<Cv>;
+  using FrF = Fp<typename Cv::FrP>;
+  const size_t gb = g1_bytes(Cv::ID);
+  CHK(s.pts.ensure((2 * n + 1) * sizeof(Affine<Cv>)));
+  CHK(s.inf.ensure(2 * n + 1));
+  CHK(s.scal_r.ensure(n * 16));
+  CHK(s.scal_s.ensure(n * 32));
+  CHK(s.scal_t.ensure(32));
+  CHK(s.tpart.ensure(L::tpart_bytes((uint32_t)n)));
+  CHK(s.flags.ensure(16));
+  CHK(s.stage.ensure(n * (2 * gb + 64)));
+  uint8_t* dC = s.stage.template as<uint8_t>();
+  uint8_t* dpi = dC + n * gb;
+  uint8_t* dz = dC + 2 * n * gb;
+  uint8_t* dy = dz + 32 * n;
+  Affine<Cv>* pts = s.pts.template as<Affine<Cv>>();
+  uint8_t* inf = s.inf.template as<uint8_t>();
+  uint32_t* sr = s.scal_r.template as<uint32_t>();
+  uint32_t* ss = s.scal_s.template as<uint32_t>();
+  uint32_t* stt = s.scal_t.template as<uint32_t>();
+  FrF* tpart = reinterpret_cast<FrF*>(s.tpart.p);
+  uint32_t* err = s.flags.template as<uint32_t>() + 1;
+  const int wb = call_wbits(c, (size_t)32 * n, size_t(1) << 22);
+  const uint32_t H = windows_half(wb), F = windows_full(wb);
+  const MsmWindows mw{2, {0, H}, {H, F}};
+  const uint32_t nn = (uint32_t)n;
+  // the first range short (its copy is the only one nothing overlaps), the others equal
+  std::vector<size_t> nk(k);
+  {
+    const size_t units = (n + FS_CHUNK - 1) / FS_CHUNK;
+    const size_t u0 = k > 1 ? std::max<size_t>(1, units / (2 * (size_t)k)) : units;
+    nk[0] = std::min(n, u0 * FS_CHUNK);
+    const std::vector<size_t> rest = split_units(n - nk[0], k - 1 > 0 ? k - 1 : 1);
+    for (int j = 1; j < k; ++j) nk[j] = rest[j - 1];
+  }
+  auto terms = [&](size_t lo, size_t nj, bool last) {
+    TermList tl{};
+    const uint32_t l = (uint32_t)lo, m = (uint32_t)nj;
+    tl.c[0] = {m, l, 4, H, 0, 4, sr + 4 * lo};       // MSM#0: r_i pi_i
+    tl.c[1] = {m, nn + l, 4, H, H, 4, sr + 4 * lo};  // MSM#1: r_i C_i
+    tl.c[2] = {m, l, 8, F, H, 8, ss + 8 * lo};       //        s_i pi_i
+    if (last) tl.c[3] = {1, 2 * nn, 8, F, H, 0, stt};  //      -t G1
+    tl.nclass = last ? 4 : 3;
+    tl.total = 3 * m + (last ? 1 : 0);
+    return tl;
+  };
+  auto emax_of = [&](size_t nj) { return (size_t)(2 * H + F) * nj + F + 16; };
+  size_t nmax = 0;
+  for (size_t v : nk) nmax = std::max(nmax, v);
+  // every workspace at its final size before the first launch (a later growth would free a buffer
+  // an earlier range's kernels are still using)
+  CHK(run_msm_core<Cv>(c, s, terms(0, nmax, true), H + F, emax_of(nmax), mw, nullptr, nullptr, true, true, wb, 3));
+  hipStream_t st = s.stream, cs = c->h2d_stream;
+  if (s.done_rec) HIPCHK(hipStreamWaitEvent(cs, s.done_ev, 0));  // the stage buffer is free
+  size_t lo = 0;
+  for (int j = 0; j < k; ++j) {
+    const size_t nj = nk[j];
+    const bool last = j == k - 1;
+    CHK(h2d(s, cs, dC + lo * gb, hC + lo * gb, nj * gb));
+    CHK(h2d(s, cs, dpi + lo * gb, hpi + lo * gb, nj * gb));
+    CHK(h2d(s, cs, dz + 32 * lo, hz + 32 * lo, nj * 32));
+    CHK(h2d(s, cs, dy + 32 * lo, hy + 32 * lo, nj * 32));
+    CHK(add_dep(s, cs));
+    CHK(begin_job(s));  // this range's kernels wait for its copy only
+    if (j == 0) {
+      mark(c, s, 0);
+      HIPCHK(hipMemsetAsync(s.flags.p, 0, 16, st));
+      HIPCHK(hipMemcpyAsync(pts + 2 * n, srs->g1_29(), sizeof(Affine<Cv>), hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpyAsync(inf + 2 * n, srs->g1.template as<uint8_t>() + sizeof(Affine<Cv>), 1,
+                            hipMemcpyDeviceToDevice, st));
+    }
+    L::convert_points(st, dpi + lo * gb, (uint32_t)nj, pts + lo, inf + lo, err, true);
+    L::convert_points(st, dC + lo * gb, (uint32_t)nj, pts + n + lo, inf + n + lo, err, true);
+    // range j's per-block r_i y_i sums land at its blocks of tpart (lo is a multiple of PREP_BLOCK)
+    L::scalar_prep(st, seed, nullptr, lo, dz + 32 * lo, dy + 32 * lo, (uint32_t)nj, sr + 4 * lo, ss + 8 * lo,
+                   tpart + lo / PREP_BLOCK, stt, err);
+    if (last) L::tsum(st, tpart, (uint32_t)((n + PREP_BLOCK - 1) / PREP_BLOCK), stt);  // -t over every range
+    const int part = k == 1 ? 0 : j == 0 ? 1 : last ? 3 : 2;
+    CHK(run_msm_core<Cv>(c, s, terms(lo, nj, last), H + F, emax_of(nj), mw, nullptr, nullptr, true, false, wb, part));
+    lo += nj;
+  }
+  L::pairing_check(st, s.res.template as<XY>(), srs->lines.template as<Line<Cv>>(), srs->q_inf.template as<uint8_t>(),
+                   s.flags.template as<int>());
+  mark(c, s, PH_PAIRING + 1);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(s.host_flags, s.flags.p, 8, hipMemcpyDeviceToHost, st));
+  CHK(end_job(s));
+  s.pending = true;
+  s.partial_job = false;
+  s.partial_of = 0;
+  s.msm_job = false;
+  s.curve = Cv::ID;
+  return 0;
+}
+
 }  // namespace
 
 // ================================================================================ C ABI
@@ -921,6 +1051,8 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
   if (const char* e = getenv("KZGMI_SORT_SPLIT")) c->sort_split = atoi(e) != 0;
   if (const char* e = getenv("KZGMI_WBITS")) c->wbits_env = atoi(e);
   if (const char* e = getenv("KZGMI_SMALL_TERMS")) c->small_terms = (uint32_t)strtoul(e, nullptr, 10);
+  if (const char* e = getenv("KZGMI_HOST_CHUNKS")) c->host_chunks_env = std::max(1, atoi(e));
+  if (const char* e = getenv("KZGMI_HOST_CHUNK_MODE")) c->host_chunk_mode = atoi(e);
   // HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 unless set before the runtime
   // starts) and serialises the streams of one queue, so every slot in flight needs a queue of its
   // own (16 slots on 24 queues pipeline; 24 on 24 ran 3.6x slower).  The runtime keeps that many
@@ -1190,38 +1322,14 @@ int kzgmi_batch_verify_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* dC
   return kzgmi_slot_wait(c, 0, ok_out);
 }
 
-int kzgmi_batch_verify(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commitments, const uint8_t* zs,
-                       const uint8_t* ys, const uint8_t* proofs, size_t n, const uint8_t* seed32, int* ok_out) {
-  return kzgmi_batch_verify_ex(c, srs, commitments, zs, ys, proofs, n, seed32, 0, ok_out);
-}
-
-int kzgmi_batch_verify_ex(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commitments, const uint8_t* zs,
-                          const uint8_t* ys, const uint8_t* proofs, size_t n, const uint8_t* seed32, uint32_t flags,
-                          int* ok_out) {
-  CHK(check_ctx(c));
-  if (!srs || !ok_out) return fail(KZGMI_ERR_ARG, "null argument");
-  if (srs->ctx != c) return fail(KZGMI_ERR_ARG, "srs does not belong to this context");
-  if (n && (!commitments || !zs || !ys || !proofs)) return fail(KZGMI_ERR_ARG, "null input");
-  CHK(slot0_idle(c));
-  if (!c->peers.empty()) return batch_multi_host(c, srs, commitments, zs, ys, proofs, n, seed32, flags, ok_out);
-  CHK(kzgmi_batch_verify_ex_async(c, srs, 0, commitments, zs, ys, proofs, n, seed32, flags));
-  return kzgmi_slot_wait(c, 0, ok_out);
-}
-
-int kzgmi_batch_verify_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const uint8_t* commitments,
-                                const uint8_t* zs, const uint8_t* ys, const uint8_t* proofs, size_t n,
-                                const uint8_t* seed32, uint32_t flags) {
-  if (!srs) return fail(KZGMI_ERR_ARG, "null argument");
-  KZ_ROUTE(c, &srs, slot);
-  CHK(check_ctx(c, slot));
-  if (srs->ctx != c) return fail(KZGMI_ERR_ARG, "srs does not belong to this context");
-  if (n && (!commitments || !zs || !ys || !proofs)) return fail(KZGMI_ERR_ARG, "null input");
-  if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "batch too large (max 2^26 tuples per call)");
-  if (flags & ~kAllFlags) return fail(KZGMI_ERR_ARG, "unknown flags");
-  Slot& s = c->slots[slot];
-  if (s.pending) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_slot_wait first");
-  if (n == 0) return kzgmi_batch_verify_device_ex_async(c, srs, slot, nullptr, nullptr, nullptr, nullptr, 0, seed32, flags);
-  Roctx rx("kzgmi_batch_verify_ex_async");
+}  // extern "C"
+namespace {
+// The host arrays of one batch into the slot's stage buffer on the context's FIFO copy stream
+// (pinned ranges DMA'd directly, pageable ones staged by the copy pool before this returns); the
+// slot's next job waits for the copy.
+int stage_host_batch(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, uint32_t flags, const uint8_t* commitments,
+                     const uint8_t* zs, const uint8_t* ys, const uint8_t* proofs, size_t n, const uint8_t** dC_out,
+                     const uint8_t** dz_out, const uint8_t** dy_out, const uint8_t** dpi_out) {
   const size_t gb = (flags & KZGMI_FLAG_COMPRESSED) ? g1_bytes(srs->curve) / 2 : g1_bytes(srs->curve);
   CHK(s.stage.ensure(n * (2 * gb + 64)));
   uint8_t* dC = s.stage.template as<uint8_t>();
@@ -1242,6 +1350,122 @@ int kzgmi_batch_verify_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, co
   CHK(h2d(s, cs, dy, ys, n * 32));
   if (c->profiling) HIPCHK(hipEventRecord(s.ev[EV_H2D1], cs));
   CHK(add_dep(s, cs));  // the batch's kernels wait for its copy only
+  *dC_out = dC;
+  *dz_out = dz;
+  *dy_out = dy;
+  *dpi_out = dpi;
+  return 0;
+}
+
+std::vector<size_t> split_units(size_t n, int D);  // below: balanced ranges in units of 4096 tuples
+
+// Synchronous host-buffer batches on one device: the PCIe copy (~5 ms per 2^20 batch) would sit
+// in front of the whole computation.  Split into k point ranges (units of 4096 tuples) on slots
+// 0..k-1: range j's shard partial starts as soon as its own copy has landed, while the next
+// range copies, and one combine + pairing on slot 0 decides (the same sums: r_i use the global
+// index; a failed range marks its partial records, so the combine reports its error).  Plain
+// BLS12-381 batches instead accumulate every range into one bucket store (enqueue_batch_chunked):
+// no per-range reduction.  From 2^17 tuples: 4 ranges with one store (2^20 pinned: 13.7 -> 11.0
+// ms, pageable 14.1 -> 11.3), 2 with partials (12.1 / 12.5 ms; profiles/r05/host_latency_*.txt).
+// KZGMI_HOST_CHUNKS overrides (1: never); not with Fiat-Shamir (the challenge needs every range
+// first) or when slots 0..k-1 are not all idle.
+int host_chunks(const kzgmi_ctx* c, size_t n, uint32_t flags, int curve) {
+  if (flags & KZGMI_FLAG_FIAT_SHAMIR) return 1;
+  const bool one_store = curve == KZGMI_BLS12_381 && flags == 0 && c->host_chunk_mode != 1;
+  int k = n >= (size_t(1) << 17) ? (one_store ? 4 : 2) : 1;
+  if (c->host_chunks_env) k = c->host_chunks_env;
+  k = std::min<int>(k, (int)c->slots.size());
+  k = std::min<int>(k, (int)((n + FS_CHUNK - 1) / FS_CHUNK));
+  for (int j = 0; j < k; ++j)
+    if (c->slots[j].pending) return 1;
+  return std::max(k, 1);
+}
+
+int batch_host_chunked(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commitments, const uint8_t* zs,
+                       const uint8_t* ys, const uint8_t* proofs, size_t n, const uint8_t* seed32, uint32_t flags,
+                       int k, int* ok_out) {
+  Roctx rx("kzgmi_batch_verify_ex.chunked");
+  uint8_t sb[32];
+  if (!seed32) {  // one verifier-private seed for every range
+    make_seed(nullptr, sb);
+    seed32 = sb;
+  }
+  if (srs->curve == KZGMI_BLS12_381 && flags == 0 && c->host_chunk_mode != 1) {
+    // one bucket store for every range (no per-range reduction)
+    Slot& s = c->slots[0];
+    uint8_t sb2[32];
+    const Seed seed = make_seed(seed32, sb2);
+    const int r = enqueue_batch_chunked<Bls12_381>(c, s, srs, commitments, zs, ys, proofs, n, seed, k);
+    if (r) {
+      const std::string msg = g_err;
+      if (s.done_rec) (void)sync_slot(s);  // whatever was enqueued drains before the error returns
+      s.pending = false;
+      return fail(r, msg);
+    }
+    return kzgmi_slot_wait(c, 0, ok_out);
+  }
+  const size_t gb = (flags & KZGMI_FLAG_COMPRESSED) ? g1_bytes(srs->curve) / 2 : g1_bytes(srs->curve);
+  const size_t rec = 2 * kzgmi_partial_bytes((kzgmi_curve)srs->curve);
+  CHK(c->gath.ensure((size_t)k * rec));
+  const std::vector<size_t> nk = split_units(n, k);
+  size_t lo = 0;
+  int started = 0, r = 0;
+  for (int j = 0; j < k && !r; ++j) {
+    const uint8_t *dC, *dz, *dy, *dpi;
+    r = stage_host_batch(c, c->slots[j], srs, flags, commitments + lo * gb, zs + lo * 32, ys + lo * 32,
+                         proofs + lo * gb, nk[j], &dC, &dz, &dy, &dpi);
+    if (!r)
+      r = kzgmi_batch_partial_device_async(c, srs, j, dC, dz, dy, dpi, nk[j], lo, seed32, flags,
+                                           (uint8_t*)c->gath.p + (size_t)j * rec);
+    if (!r) ++started;
+    lo += nk[j];
+  }
+  // every started range completes before the combine reads the records (a range's own error is
+  // carried by its marked records)
+  const std::string msg = r ? g_err : std::string();
+  for (int j = 0; j < started; ++j) (void)kzgmi_slot_wait(c, j, nullptr);
+  if (r) return fail(r, msg);
+  return kzgmi_batch_combine_device(c, srs, c->gath.p, k, ok_out);
+}
+}  // namespace
+extern "C" {
+
+int kzgmi_batch_verify(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commitments, const uint8_t* zs,
+                       const uint8_t* ys, const uint8_t* proofs, size_t n, const uint8_t* seed32, int* ok_out) {
+  return kzgmi_batch_verify_ex(c, srs, commitments, zs, ys, proofs, n, seed32, 0, ok_out);
+}
+
+int kzgmi_batch_verify_ex(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commitments, const uint8_t* zs,
+                          const uint8_t* ys, const uint8_t* proofs, size_t n, const uint8_t* seed32, uint32_t flags,
+                          int* ok_out) {
+  CHK(check_ctx(c));
+  if (!srs || !ok_out) return fail(KZGMI_ERR_ARG, "null argument");
+  if (srs->ctx != c) return fail(KZGMI_ERR_ARG, "srs does not belong to this context");
+  if (n && (!commitments || !zs || !ys || !proofs)) return fail(KZGMI_ERR_ARG, "null input");
+  CHK(slot0_idle(c));
+  if (!c->peers.empty()) return batch_multi_host(c, srs, commitments, zs, ys, proofs, n, seed32, flags, ok_out);
+  const int k = host_chunks(c, n, flags, srs->curve);
+  if (k > 1) return batch_host_chunked(c, srs, commitments, zs, ys, proofs, n, seed32, flags, k, ok_out);
+  CHK(kzgmi_batch_verify_ex_async(c, srs, 0, commitments, zs, ys, proofs, n, seed32, flags));
+  return kzgmi_slot_wait(c, 0, ok_out);
+}
+
+int kzgmi_batch_verify_ex_async(kzgmi_ctx* c, const kzgmi_srs* srs, int slot, const uint8_t* commitments,
+                                const uint8_t* zs, const uint8_t* ys, const uint8_t* proofs, size_t n,
+                                const uint8_t* seed32, uint32_t flags) {
+  if (!srs) return fail(KZGMI_ERR_ARG, "null argument");
+  KZ_ROUTE(c, &srs, slot);
+  CHK(check_ctx(c, slot));
+  if (srs->ctx != c) return fail(KZGMI_ERR_ARG, "srs does not belong to this context");
+  if (n && (!commitments || !zs || !ys || !proofs)) return fail(KZGMI_ERR_ARG, "null input");
+  if (n > (1u << 26)) return fail(KZGMI_ERR_ARG, "batch too large (max 2^26 tuples per call)");
+  if (flags & ~kAllFlags) return fail(KZGMI_ERR_ARG, "unknown flags");
+  Slot& s = c->slots[slot];
+  if (s.pending) return fail(KZGMI_ERR_ARG, "slot busy: call kzgmi_slot_wait first");
+  if (n == 0) return kzgmi_batch_verify_device_ex_async(c, srs, slot, nullptr, nullptr, nullptr, nullptr, 0, seed32, flags);
+  Roctx rx("kzgmi_batch_verify_ex_async");
+  const uint8_t *dC, *dz, *dy, *dpi;
+  CHK(stage_host_batch(c, s, srs, flags, commitments, zs, ys, proofs, n, &dC, &dz, &dy, &dpi));
   const int r = kzgmi_batch_verify_device_ex_async(c, srs, slot, dC, dz, dy, dpi, n, seed32, flags);
   if (c->profiling) s.ev_used[EV_H2D0] = s.ev_used[EV_H2D1] = (r == 0);
   return r;

@@ -24,6 +24,9 @@ struct Launch {
                          const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts,
                          uint32_t* acc29, uint32_t nb, size_t acc_threads = 0, uint32_t* next_chunk = nullptr);
   static void pts_to29(hipStream_t st, AF* pts, uint32_t n);  // in place
+  // acc29[b] += acc29b[b] for the buckets with cntb[b] != 0, cnt[b] += cntb[b] (chunked batches)
+  static void merge_buckets(hipStream_t st, uint32_t nb, uint32_t* acc29, uint32_t* cnt, const uint32_t* acc29b,
+                            const uint32_t* cntb);
   static void reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const uint32_t* acc29, XY* R, XY* U,
                      XY* scratch, XY* winsum, int wbits = WBITS);
   static void window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res, int wbits = WBITS);
@@ -49,6 +52,7 @@ struct Launch {
                           bool in29 = false);
   static void convert_g2(hipStream_t st, const uint8_t* bytes, uint32_t n, G2Aff<Cv>* out, uint8_t* inf,
                          uint32_t* err);
+  static void tsum(hipStream_t st, const void* tpart, uint32_t nblocks, uint32_t* negt);  // negt = -(sum) mod r
   static void scalar_prep(hipStream_t st, const Seed& seed, const uint32_t* seed_dev, uint64_t index_offset,
                           const uint8_t* zs,
                           const uint8_t* ys, uint32_t n, uint32_t* r_out, uint32_t* s_out, void* tpart,

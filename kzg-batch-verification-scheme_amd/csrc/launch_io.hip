@@ -63,6 +63,10 @@ size_t Launch<Cv>::tpart_bytes(uint32_t n) {
   return (size_t)grid_for(n, PREP_BLOCK) * sizeof(Fp<typename Cv::FrP>);
 }
 template <class Cv>
+void Launch<Cv>::tsum(hipStream_t st, const void* tpart, uint32_t nblocks, uint32_t* negt) {
+  k_tsum<Cv><<<1, 256, 0, st>>>((const Fp<typename Cv::FrP>*)tpart, nblocks, negt);
+}
+template <class Cv>
 void Launch<Cv>::scalar_prep(hipStream_t st, const Seed& seed, const uint32_t* seed_dev, uint64_t index_offset,
                              const uint8_t* zs,
                              const uint8_t* ys, uint32_t n, uint32_t* r_out, uint32_t* s_out, void* tpart,
@@ -142,6 +146,7 @@ template void Launch<C_>::subgroup_check(hipStream_t, const Affine<C_>*, const u
 template void Launch<C_>::convert_scalars(hipStream_t, const uint8_t*, uint32_t, uint32_t*, uint32_t*);
 template void Launch<C_>::convert_g2(hipStream_t, const uint8_t*, uint32_t, G2Aff<C_>*, uint8_t*, uint32_t*);
 template size_t Launch<C_>::tpart_bytes(uint32_t);
+template void Launch<C_>::tsum(hipStream_t, const void*, uint32_t, uint32_t*);
 template void Launch<C_>::scalar_prep(hipStream_t, const Seed&, const uint32_t*, uint64_t, const uint8_t*, const uint8_t*, uint32_t,
                                       uint32_t*, uint32_t*, void*, uint32_t*, uint32_t*, uint32_t*, uint32_t*);
 template void Launch<C_>::fs_leaves(hipStream_t, const uint8_t*, const uint8_t*, const uint8_t*, const uint8_t*,

@@ -79,6 +79,12 @@ void Launch<Cv>::reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, con
 }
 
 template <class Cv>
+void Launch<Cv>::merge_buckets(hipStream_t st, uint32_t nb, uint32_t* acc29, uint32_t* cnt, const uint32_t* acc29b,
+                               const uint32_t* cntb) {
+  if (nb) k_merge_buckets<Cv><<<(nb + 255) / 256, 256, 0, st>>>(nb, acc29, cnt, acc29b, cntb);
+}
+
+template <class Cv>
 void Launch<Cv>::small_msm(hipStream_t st, const TermList& tl, const SmallPlan& sp, uint32_t terms, const AF* pts,
                            const uint8_t* inf, uint32_t* nodes, uint32_t* flags, uint32_t flag_words, XY* res) {
   (void)hipMemsetAsync(res, 0, (size_t)sp.nmsm * sizeof(XY), st);  // zz = 0: an MSM without terms is O
@@ -104,6 +110,8 @@ template void Launch<KZ_CURVE_T>::reduce(hipStream_t, uint32_t, const uint32_t*,
                                          Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, int);
 template void Launch<KZ_CURVE_T>::window_combine(hipStream_t, const MsmWindows&, const Xyzz<KZ_CURVE_T>*,
                                                  Xyzz<KZ_CURVE_T>*, int);
+template void Launch<KZ_CURVE_T>::merge_buckets(hipStream_t, uint32_t, uint32_t*, uint32_t*, const uint32_t*,
+                                                const uint32_t*);
 template void Launch<KZ_CURVE_T>::small_msm(hipStream_t, const TermList&, const SmallPlan&, uint32_t,
                                             const Affine<KZ_CURVE_T>*, const uint8_t*, uint32_t*, uint32_t*, uint32_t,
                                             Xyzz<KZ_CURVE_T>*);

@@ -1087,6 +1087,25 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
   store_x29<Q>(acc29, key, acc);
 }
 
+// Bucket stores of two accumulations over the same sets (the point ranges of a chunked
+// host-buffer batch, api.hip enqueue_batch_chunked): A[b] += B[b] where B's bucket is non-empty,
+// counts added (the reduction only tests them for zero); empty buckets' records are never read.
+template <class Cv>
+__global__ void __launch_bounds__(256) k_merge_buckets(uint32_t nb, uint32_t* __restrict__ acc29,
+                                                       uint32_t* __restrict__ cnt,
+                                                       const uint32_t* __restrict__ acc29b,
+                                                       const uint32_t* __restrict__ cntb) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  const uint32_t kb = cntb[b];
+  if (!kb) return;
+  using Q = Fp29Of<Cv>;
+  const uint32_t ka = cnt[b];
+  const X29<Q> y = load_x29<Q>(acc29b, b);
+  store_x29<Q>(acc29, b, ka ? x29_add<Cv, Q>(load_x29<Q>(acc29, b), y) : y);
+  cnt[b] = ka + kb;
+}
+
 // ------------------------------------------------------------------------------ reduction
 // Segment g covers buckets [g*SEG, (g+1)*SEG) of one set (SEG divides NBUCKETS).  Two threads
 // per segment (adjacent lanes): half h runs the running sums over buckets [8h, 8h + 8) of the

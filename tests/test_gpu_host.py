@@ -180,3 +180,69 @@ def test_host_async_full_size_vs_oracle(ctx):
     assert ctx.batch_verify(srs, *host, seed=vseed) is False
     del srs
     pinned.free()
+
+
+def _context_env(**env):
+    import os
+    import kzgmi
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return kzgmi.Context(0, 4)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.slow
+def test_sync_host_chunked_matches_unsplit(ctx):
+    """The synchronous host-buffer call splits a large batch into point ranges whose work starts
+    while the next range copies (csrc/api.hip batch_host_chunked): one bucket store for every
+    range (the default for plain BLS12-381 batches) and shard partials per range
+    (KZGMI_HOST_CHUNK_MODE=1, the form for flags and BN254) both give the verdict and A, B of a
+    context that never splits (KZGMI_HOST_CHUNKS=1) and of the oracle; a corrupted y in the last
+    range rejects; a non-canonical z in an inner range reports the unsplit call's error."""
+    import kzgmi
+    import torch
+    curve = "bls12_381"
+    C = pc.CURVES[curve]
+    n, tau = (1 << 19) + 5000, 0xC0FFEE + 12  # 4 ranges
+    g1b = 2 * C.fp_bytes
+    d = [torch.empty(n * w, dtype=torch.uint8, device="cuda") for w in (g1b, 32, 32, g1b)]
+    ctx.gen_tuples(curve, tau, hashlib.sha256(b"host-chunked").digest(), n, *d)
+    host = [t.cpu().numpy() for t in d]
+    del d
+    g2 = pk.g2_to_bytes(C.g2, C)
+    tg2 = O.g2_mul(curve, g2, tau)
+    seed = hashlib.sha256(b"host-chunked-verify").digest()
+    c1 = _context_env(KZGMI_HOST_CHUNKS="1")
+    c2 = _context_env(KZGMI_HOST_CHUNK_MODE="1")
+    try:
+        s1 = c1.load_srs(curve, g2, tg2)
+        assert c1.batch_verify(s1, *host, seed=seed) is True
+        want = c1.last_combination(curve)
+        ok, Ao, Bo = O.batch_verify(curve, *(a.tobytes() for a in host), n, g2, tg2, seed, want_ab=True)
+        assert ok is True and want == (Ao, Bo)
+        bad_y = [a.copy() for a in host]
+        bad_y[2][32 * (n - 1) + 31] ^= 1  # y of the last tuple
+        bad_z = [a.copy() for a in host]
+        bad_z[1][32 * 1000:32 * 1001] = np.frombuffer(C.r.to_bytes(32, "big"), dtype=np.uint8)  # z = r
+        with pytest.raises(kzgmi.KzgmiError) as e1:
+            c1.batch_verify(s1, *bad_z, seed=seed)
+        for c in (ctx, c2):
+            srs = c.load_srs(curve, g2, tg2)
+            assert c.batch_verify(srs, *host, seed=seed) is True
+            assert c.last_combination(curve) == want
+            assert c.batch_verify(srs, *bad_y, seed=seed) is False
+            with pytest.raises(kzgmi.KzgmiError) as e:
+                c.batch_verify(srs, *bad_z, seed=seed)
+            assert e.value.code == e1.value.code == -4
+            assert c.batch_verify(srs, *host, seed=seed) is True  # the context recovers
+            del srs
+        del s1
+    finally:
+        c1.close()
+        c2.close()
