@@ -916,24 +916,31 @@ int h2d(Slot& s, hipStream_t cs, void* dst, const void* src, size_t bytes) {
 
 std::vector<size_t> split_units(size_t n, int D);  // below: balanced ranges in units of 4096 tuples
 
-// A synchronous host-buffer batch (no flags, BLS12-381: no GLV) as k point ranges on one slot:
-// range j's copy (the context's copy stream) overlaps the previous ranges' front end and
-// accumulation on the slot's stream, every range accumulates into the same bucket sets (a second
-// store merged into the first, run_msm_core parts 1..3), the G1 term joins the last range (its
-// scalar needs every range's r_i y_i), and one reduction, combination and pairing decide.  Same
-// r_i (global index), same sums as enqueue_batch; inputs land in the slot's stage buffer.
+// A synchronous host-buffer batch (plain flags, or TRUSTED_G1; BN254 and declared-G1 points take
+// the GLV form) as k point ranges on one slot: range j's copy (the context's copy stream) overlaps
+// the previous ranges' front end and accumulation on the slot's stream, every range accumulates
+// into the same bucket sets (a second store merged into the first, run_msm_core parts 1..3), the
+// G1 term joins the last range (its scalar needs every range's r_i y_i), and one reduction,
+// combination and pairing decide.  Same r_i (global index), same sums as enqueue_batch; the
+// inputs land in the slot's stage buffer.
 template <class Cv>
 int enqueue_batch_chunked(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const uint8_t* hC, const uint8_t* hz,
-                          const uint8_t* hy, const uint8_t* hpi, size_t n, const Seed& seed, int k) {
+                          const uint8_t* hy, const uint8_t* hpi, size_t n, const Seed& seed, uint32_t flags, int k) {
   using XY = Xyzz<Cv>;
   using L = Launch<Cv>;
   using FrF = Fp<typename Cv::FrP>;
+  const bool glv = c->glv_batch && (Cv::ID == 1 || (flags & KZGMI_FLAG_TRUSTED_G1) != 0);
   const size_t gb = g1_bytes(Cv::ID);
-  CHK(s.pts.ensure((2 * n + 1) * sizeof(Affine<Cv>)));
-  CHK(s.inf.ensure(2 * n + 1));
+  const size_t PH = 2 * n + 1;  // GLV: phi(pts[j]) at pts[PH + j]
+  CHK(s.pts.ensure((glv ? 2 * PH : PH) * sizeof(Affine<Cv>)));
+  CHK(s.inf.ensure(glv ? 2 * PH : PH));
   CHK(s.scal_r.ensure(n * 16));
   CHK(s.scal_s.ensure(n * 32));
   CHK(s.scal_t.ensure(32));
+  if (glv) {
+    CHK(s.glv_s.ensure(n * 32));
+    CHK(s.glv_t.ensure(32));
+  }
   CHK(s.tpart.ensure(L::tpart_bytes((uint32_t)n)));
   CHK(s.flags.ensure(16));
   CHK(s.stage.ensure(n * (2 * gb + 64)));
@@ -946,12 +953,15 @@ int enqueue_batch_chunked(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const uin
   uint32_t* sr = s.scal_r.template as<uint32_t>();
   uint32_t* ss = s.scal_s.template as<uint32_t>();
   uint32_t* stt = s.scal_t.template as<uint32_t>();
+  uint32_t* gs = s.glv_s.template as<uint32_t>();  // [h0 x n | h1 x n]
+  uint32_t* gt = s.glv_t.template as<uint32_t>();
   FrF* tpart = reinterpret_cast<FrF*>(s.tpart.p);
   uint32_t* err = s.flags.template as<uint32_t>() + 1;
   const int wb = call_wbits(c, (size_t)32 * n, size_t(1) << 22);
   const uint32_t H = windows_half(wb), F = windows_full(wb);
-  const MsmWindows mw{2, {0, H}, {H, F}};
-  const uint32_t nn = (uint32_t)n;
+  const MsmWindows mw = glv ? MsmWindows{2, {0, H}, {H, H}} : MsmWindows{2, {0, H}, {H, F}};
+  const uint32_t nsets = glv ? 2 * H : H + F;
+  const uint32_t nn = (uint32_t)n, ph = (uint32_t)PH;
   // the first range short (its copy is the only one nothing overlaps), the others equal
   std::vector<size_t> nk(k);
   {
@@ -964,20 +974,33 @@ int enqueue_batch_chunked(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const uin
   auto terms = [&](size_t lo, size_t nj, bool last) {
     TermList tl{};
     const uint32_t l = (uint32_t)lo, m = (uint32_t)nj;
-    tl.c[0] = {m, l, 4, H, 0, 4, sr + 4 * lo};       // MSM#0: r_i pi_i
-    tl.c[1] = {m, nn + l, 4, H, H, 4, sr + 4 * lo};  // MSM#1: r_i C_i
-    tl.c[2] = {m, l, 8, F, H, 8, ss + 8 * lo};       //        s_i pi_i
-    if (last) tl.c[3] = {1, 2 * nn, 8, F, H, 0, stt};  //      -t G1
-    tl.nclass = last ? 4 : 3;
-    tl.total = 3 * m + (last ? 1 : 0);
+    uint32_t q = 0;
+    tl.c[q++] = {m, l, 4, H, 0, 4, sr + 4 * lo};           // MSM#0: r_i pi_i
+    tl.c[q++] = {m, nn + l, 4, H, H, 4, sr + 4 * lo};      // MSM#1: r_i C_i
+    if (glv) {
+      tl.c[q++] = {m, l, 4, H, H, 4, gs + 4 * lo};         //        s_i pi_i = h0 pi + h1 phi(pi)
+      tl.c[q++] = {m, ph + l, 4, H, H, 4, gs + 4 * (n + lo)};
+      if (last) {
+        tl.c[q++] = {1, 2 * nn, 4, H, H, 0, gt};           //        -t G1
+        tl.c[q++] = {1, ph + 2 * nn, 4, H, H, 0, gt + 4};
+      }
+    } else {
+      tl.c[q++] = {m, l, 8, F, H, 8, ss + 8 * lo};         //        s_i pi_i
+      if (last) tl.c[q++] = {1, 2 * nn, 8, F, H, 0, stt};  //        -t G1
+    }
+    tl.nclass = q;
+    tl.total = 0;
+    for (uint32_t j = 0; j < q; ++j) tl.total += tl.c[j].count;
     return tl;
   };
-  auto emax_of = [&](size_t nj) { return (size_t)(2 * H + F) * nj + F + 16; };
+  auto emax_of = [&](size_t nj) {
+    return glv ? (size_t)4 * H * nj + 2 * H + 16 : (size_t)(2 * H + F) * nj + F + 16;
+  };
   size_t nmax = 0;
   for (size_t v : nk) nmax = std::max(nmax, v);
   // every workspace at its final size before the first launch (a later growth would free a buffer
   // an earlier range's kernels are still using)
-  CHK(run_msm_core<Cv>(c, s, terms(0, nmax, true), H + F, emax_of(nmax), mw, nullptr, nullptr, true, true, wb, 3));
+  CHK(run_msm_core<Cv>(c, s, terms(0, nmax, true), nsets, emax_of(nmax), mw, nullptr, nullptr, true, true, wb, 3));
   hipStream_t st = s.stream, cs = c->h2d_stream;
   if (s.done_rec) HIPCHK(hipStreamWaitEvent(cs, s.done_ev, 0));  // the stage buffer is free
   size_t lo = 0;
@@ -996,15 +1019,25 @@ int enqueue_batch_chunked(kzgmi_ctx* c, Slot& s, const kzgmi_srs* srs, const uin
       HIPCHK(hipMemcpyAsync(pts + 2 * n, srs->g1_29(), sizeof(Affine<Cv>), hipMemcpyDeviceToDevice, st));
       HIPCHK(hipMemcpyAsync(inf + 2 * n, srs->g1.template as<uint8_t>() + sizeof(Affine<Cv>), 1,
                             hipMemcpyDeviceToDevice, st));
+      if (glv) L::endo_points(st, pts + 2 * n, inf + 2 * n, 1, pts + PH + 2 * n, inf + PH + 2 * n, true);
     }
-    L::convert_points(st, dpi + lo * gb, (uint32_t)nj, pts + lo, inf + lo, err, true);
-    L::convert_points(st, dC + lo * gb, (uint32_t)nj, pts + n + lo, inf + n + lo, err, true);
+    if (glv) {  // phi(P) stored by the same pass
+      L::convert_points(st, dpi + lo * gb, (uint32_t)nj, pts + lo, inf + lo, err, true, pts + PH + lo, inf + PH + lo);
+      L::convert_points(st, dC + lo * gb, (uint32_t)nj, pts + n + lo, inf + n + lo, err, true, pts + PH + n + lo,
+                        inf + PH + n + lo);
+    } else {
+      L::convert_points(st, dpi + lo * gb, (uint32_t)nj, pts + lo, inf + lo, err, true);
+      L::convert_points(st, dC + lo * gb, (uint32_t)nj, pts + n + lo, inf + n + lo, err, true);
+    }
     // range j's per-block r_i y_i sums land at its blocks of tpart (lo is a multiple of PREP_BLOCK)
     L::scalar_prep(st, seed, nullptr, lo, dz + 32 * lo, dy + 32 * lo, (uint32_t)nj, sr + 4 * lo, ss + 8 * lo,
-                   tpart + lo / PREP_BLOCK, stt, err);
-    if (last) L::tsum(st, tpart, (uint32_t)((n + PREP_BLOCK - 1) / PREP_BLOCK), stt);  // -t over every range
+                   tpart + lo / PREP_BLOCK, stt, err, glv ? gs + 4 * lo : nullptr, glv ? gs + 4 * (n + lo) : nullptr);
+    if (last) {  // -t over every range (then its GLV halves)
+      L::tsum(st, tpart, (uint32_t)((n + PREP_BLOCK - 1) / PREP_BLOCK), stt);
+      if (glv) L::glv_split(st, stt, 8, 1, gt, gt + 4);
+    }
     const int part = k == 1 ? 0 : j == 0 ? 1 : last ? 3 : 2;
-    CHK(run_msm_core<Cv>(c, s, terms(lo, nj, last), H + F, emax_of(nj), mw, nullptr, nullptr, true, false, wb, part));
+    CHK(run_msm_core<Cv>(c, s, terms(lo, nj, last), nsets, emax_of(nj), mw, nullptr, nullptr, true, false, wb, part));
     lo += nj;
   }
   L::pairing_check(st, s.res.template as<XY>(), srs->lines.template as<Line<Cv>>(), srs->q_inf.template as<uint8_t>(),
@@ -1363,15 +1396,17 @@ std::vector<size_t> split_units(size_t n, int D);  // below: balanced ranges in 
 // in front of the whole computation.  Split into k point ranges (units of 4096 tuples) on slots
 // 0..k-1: range j's shard partial starts as soon as its own copy has landed, while the next
 // range copies, and one combine + pairing on slot 0 decides (the same sums: r_i use the global
-// index; a failed range marks its partial records, so the combine reports its error).  Plain
-// BLS12-381 batches instead accumulate every range into one bucket store (enqueue_batch_chunked):
-// no per-range reduction.  From 2^17 tuples: 4 ranges with one store (2^20 pinned: 13.7 -> 11.0
+// index; a failed range marks its partial records, so the combine reports its error).  Batches
+// without flags (or with TRUSTED_G1) instead accumulate every range into one bucket store
+// (enqueue_batch_chunked): no per-range reduction.  From 2^17 tuples: 4 ranges with one store (2^20 pinned: 13.7 -> 11.0
 // ms, pageable 14.1 -> 11.3), 2 with partials (12.1 / 12.5 ms; profiles/r05/host_latency_*.txt).
 // KZGMI_HOST_CHUNKS overrides (1: never); not with Fiat-Shamir (the challenge needs every range
 // first) or when slots 0..k-1 are not all idle.
+bool one_store_flags(uint32_t flags) { return (flags & ~KZGMI_FLAG_TRUSTED_G1) == 0; }
 int host_chunks(const kzgmi_ctx* c, size_t n, uint32_t flags, int curve) {
+  (void)curve;
   if (flags & KZGMI_FLAG_FIAT_SHAMIR) return 1;
-  const bool one_store = curve == KZGMI_BLS12_381 && flags == 0 && c->host_chunk_mode != 1;
+  const bool one_store = one_store_flags(flags) && c->host_chunk_mode != 1;
   int k = n >= (size_t(1) << 17) ? (one_store ? 4 : 2) : 1;
   if (c->host_chunks_env) k = c->host_chunks_env;
   k = std::min<int>(k, (int)c->slots.size());
@@ -1390,12 +1425,14 @@ int batch_host_chunked(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commit
     make_seed(nullptr, sb);
     seed32 = sb;
   }
-  if (srs->curve == KZGMI_BLS12_381 && flags == 0 && c->host_chunk_mode != 1) {
+  if (one_store_flags(flags) && c->host_chunk_mode != 1) {
     // one bucket store for every range (no per-range reduction)
     Slot& s = c->slots[0];
     uint8_t sb2[32];
     const Seed seed = make_seed(seed32, sb2);
-    const int r = enqueue_batch_chunked<Bls12_381>(c, s, srs, commitments, zs, ys, proofs, n, seed, k);
+    const int r = dispatch(srs->curve, [&](auto cv) -> int {
+      return enqueue_batch_chunked<decltype(cv)>(c, s, srs, commitments, zs, ys, proofs, n, seed, flags, k);
+    });
     if (r) {
       const std::string msg = g_err;
       if (s.done_rec) (void)sync_slot(s);  // whatever was enqueued drains before the error returns

@@ -198,16 +198,17 @@ def _context_env(**env):
 
 
 @pytest.mark.slow
-def test_sync_host_chunked_matches_unsplit(ctx):
+@pytest.mark.parametrize("curve,trusted", [("bls12_381", False), ("bls12_381", True), ("bn254", False)])
+def test_sync_host_chunked_matches_unsplit(ctx, curve, trusted):
     """The synchronous host-buffer call splits a large batch into point ranges whose work starts
     while the next range copies (csrc/api.hip batch_host_chunked): one bucket store for every
-    range (the default for plain BLS12-381 batches) and shard partials per range
-    (KZGMI_HOST_CHUNK_MODE=1, the form for flags and BN254) both give the verdict and A, B of a
+    range (the default without flags or with trusted_g1; BN254 and trusted points take the GLV
+    form) and shard partials per range (KZGMI_HOST_CHUNK_MODE=1, the form for the other flags)
+    both give the verdict and A, B of a
     context that never splits (KZGMI_HOST_CHUNKS=1) and of the oracle; a corrupted y in the last
     range rejects; a non-canonical z in an inner range reports the unsplit call's error."""
     import kzgmi
     import torch
-    curve = "bls12_381"
     C = pc.CURVES[curve]
     n, tau = (1 << 19) + 5000, 0xC0FFEE + 12  # 4 ranges
     g1b = 2 * C.fp_bytes
@@ -222,7 +223,8 @@ def test_sync_host_chunked_matches_unsplit(ctx):
     c2 = _context_env(KZGMI_HOST_CHUNK_MODE="1")
     try:
         s1 = c1.load_srs(curve, g2, tg2)
-        assert c1.batch_verify(s1, *host, seed=seed) is True
+        kw = {"trusted_g1": trusted}
+        assert c1.batch_verify(s1, *host, seed=seed, **kw) is True
         want = c1.last_combination(curve)
         ok, Ao, Bo = O.batch_verify(curve, *(a.tobytes() for a in host), n, g2, tg2, seed, want_ab=True)
         assert ok is True and want == (Ao, Bo)
@@ -231,16 +233,16 @@ def test_sync_host_chunked_matches_unsplit(ctx):
         bad_z = [a.copy() for a in host]
         bad_z[1][32 * 1000:32 * 1001] = np.frombuffer(C.r.to_bytes(32, "big"), dtype=np.uint8)  # z = r
         with pytest.raises(kzgmi.KzgmiError) as e1:
-            c1.batch_verify(s1, *bad_z, seed=seed)
+            c1.batch_verify(s1, *bad_z, seed=seed, **kw)
         for c in (ctx, c2):
             srs = c.load_srs(curve, g2, tg2)
-            assert c.batch_verify(srs, *host, seed=seed) is True
+            assert c.batch_verify(srs, *host, seed=seed, **kw) is True
             assert c.last_combination(curve) == want
-            assert c.batch_verify(srs, *bad_y, seed=seed) is False
+            assert c.batch_verify(srs, *bad_y, seed=seed, **kw) is False
             with pytest.raises(kzgmi.KzgmiError) as e:
-                c.batch_verify(srs, *bad_z, seed=seed)
+                c.batch_verify(srs, *bad_z, seed=seed, **kw)
             assert e.value.code == e1.value.code == -4
-            assert c.batch_verify(srs, *host, seed=seed) is True  # the context recovers
+            assert c.batch_verify(srs, *host, seed=seed, **kw) is True  # the context recovers
             del srs
         del s1
     finally:
