@@ -179,7 +179,12 @@ void kzgmi_srs_free(kzgmi_srs* srs);
 
 /* BASELINE.json:5 batch_verify(commitments, zs, ys, proofs, srs) -- host buffers (copied to
  * HBM, i.e. the PCIe-inclusive path; see kzgmi_batch_verify_ex_async for how).  *ok_out = 1
- * accept, 0 reject. */
+ * accept, 0 reject.  From 2^17 tuples the copy overlaps the computation: the batch is copied in
+ * point ranges and each range's work starts when its copy lands (slot 0; slots 0-1 for
+ * compressed, subgroup-checked and powers-of-r batches, which must then be idle too; not with
+ * Fiat-Shamir).  KZGMI_HOST_CHUNKS=1 in the environment before kzgmi_ctx_create turns it off.
+ * Calls of at most 4096 MSM terms (a batch has 3n + 1; with GLV 2 (2n + 1)) take a one-wave-
+ * per-term path instead of the bucket method (KZGMI_SMALL_TERMS=<terms> moves the limit). */
 int kzgmi_batch_verify(kzgmi_ctx* ctx, const kzgmi_srs* srs, const uint8_t* commitments,
                        const uint8_t* zs, const uint8_t* ys, const uint8_t* proofs, size_t n,
                        const uint8_t* seed32, int* ok_out);
