@@ -150,6 +150,20 @@ struct kzgmi_ctx {
   uint32_t small_terms = 4096;  // calls of at most this many terms: msm_small.hpp (KZGMI_SMALL_TERMS; 0: never)
   int host_chunks_env = 0;       // KZGMI_HOST_CHUNKS: ranges of a synchronous host-buffer batch (batch_host_chunked)
   int host_chunk_mode = 0;       // KZGMI_HOST_CHUNK_MODE=1: shard partials even where one bucket store applies
+  // accumulation order: a slot's k_accumulate waits for the accumulation D launches before it
+  // (any slot), so at most D run at once and they start in submission order.  Without it 16
+  // slots in flight ran their accumulations in bursts and their tails (pairing: one CU) together,
+  // with no accumulation beside them, and the oldest batch -- the one the caller waits on to
+  // reuse its slot -- finished last (tools/trace_gaps.py).  D = acc_order for calls of at least
+  // ACC_ORDER_WIDE entries, acc_order_small below (a 2^17 batch's accumulation does not fill
+  // the chip): pipelined 2^20 batches 184.7 vs 183.5/s (BN254 361 vs 347), 2^17 batches 1074 vs
+  // 1028/s with D = 4 (925 with 2) -- profiles/r05/ab_acc_order*.txt.
+  // KZGMI_ACC_ORDER, KZGMI_ACC_ORDER_SMALL (0: off)
+  static constexpr int kAccOrderMax = 8;
+  static constexpr size_t ACC_ORDER_WIDE = size_t(1) << 23;
+  int acc_order = 2, acc_order_small = 4;
+  hipEvent_t acc_ring[kAccOrderMax] = {};  // launch i's event at i % kAccOrderMax
+  uint64_t acc_launches = 0;
   double phase_ms[kNumPhases] = {};  // running sums since profiling was (re)enabled
   // host-buffer inputs of every slot are copied on ONE stream, in submission order: each
   // batch's copy then gets the whole link and completes first-in first-out (16 concurrent
@@ -444,9 +458,20 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
           OFF.template as<uint32_t>(), CNT.template as<uint32_t>(), s.total.template as<uint32_t>(),
           s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(), wbits);
   mark(c, s, PH_SORT + 1);
+  hipEvent_t* order_ev = nullptr;  // accumulation order (kzgmi_ctx::acc_order)
+  const int order = emax >= kzgmi_ctx::ACC_ORDER_WIDE ? c->acc_order : c->acc_order_small;
+  if (order > 0 && c->slots.size() > 1) {
+    constexpr uint64_t M = kzgmi_ctx::kAccOrderMax;
+    const uint64_t i = c->acc_launches++;
+    if (i >= (uint64_t)order && c->acc_ring[(i - order) % M])  // the accumulation `order` launches back
+      HIPCHK(hipStreamWaitEvent(st, c->acc_ring[(i - order) % M], 0));
+    order_ev = &c->acc_ring[i % M];  // (launch i - M's event: no later launch waits for it)
+    if (!*order_ev) HIPCHK(hipEventCreateWithFlags(order_ev, hipEventDisableTiming));
+  }
   L::accumulate(st, nchunks, s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
                 OFF.template as<uint32_t>(), CNT.template as<uint32_t>(), pts, ACC.template as<uint32_t>(), NB,
                 acc_threads, acc_threads ? s.accq.template as<uint32_t>() : nullptr);
+  if (order_ev) HIPCHK(hipEventRecord(*order_ev, st));
   if (second)
     L::merge_buckets(st, NB, s.acc29.template as<uint32_t>(), s.cnt.template as<uint32_t>(),
                      s.acc29b.template as<uint32_t>(), s.cntb.template as<uint32_t>());
@@ -1086,6 +1111,9 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
   if (const char* e = getenv("KZGMI_SMALL_TERMS")) c->small_terms = (uint32_t)strtoul(e, nullptr, 10);
   if (const char* e = getenv("KZGMI_HOST_CHUNKS")) c->host_chunks_env = std::max(1, atoi(e));
   if (const char* e = getenv("KZGMI_HOST_CHUNK_MODE")) c->host_chunk_mode = atoi(e);
+  if (const char* e = getenv("KZGMI_ACC_ORDER")) c->acc_order = std::min(std::max(0, atoi(e)), kzgmi_ctx::kAccOrderMax);
+  if (const char* e = getenv("KZGMI_ACC_ORDER_SMALL"))
+    c->acc_order_small = std::min(std::max(0, atoi(e)), kzgmi_ctx::kAccOrderMax);
   // HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 unless set before the runtime
   // starts) and serialises the streams of one queue, so every slot in flight needs a queue of its
   // own (16 slots on 24 queues pipeline; 24 on 24 ran 3.6x slower).  The runtime keeps that many
@@ -1155,6 +1183,8 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
     if (s.host_out) (void)hipHostFree(s.host_out);
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
+  for (hipEvent_t e : c->acc_ring)
+    if (e) (void)hipEventDestroy(e);
   for (int k = 0; k < 2; ++k) { c->table[k].release(); c->table_base[k].release(); }
   if (c->h2d_stream) {
     (void)hipStreamSynchronize(c->h2d_stream);
