@@ -331,7 +331,7 @@ def main():
     ap.add_argument("--shard17-steps", type=int, default=240,
                     help="secondary.sharded_2e17_world1: 2^17-tuple batches (configs[2]'s 8-way per-rank share) "
                          "through ShardedPipeline + RCCL at world 1, and unsharded (0 = skip)")
-    ap.add_argument("--default-queues-steps", type=int, default=20,
+    ap.add_argument("--default-queues-steps", type=int, default=60,
                     help="secondary.default_hw_queues: the configs[2] timed region again in a child process at HIP's "
                          "default GPU_MAX_HW_QUEUES = 4 (0 = skip)")
     ap.add_argument("--detail-file", default="gpurun_out/bench_detail.json",

@@ -157,8 +157,10 @@ struct kzgmi_ctx {
   // reuse its slot -- finished last (tools/trace_gaps.py).  D = acc_order for calls of at least
   // ACC_ORDER_WIDE entries, acc_order_small below (a 2^17 batch's accumulation does not fill
   // the chip): pipelined 2^20 batches 184.7 vs 183.5/s (BN254 361 vs 347), 2^17 batches 1074 vs
-  // 1028/s with D = 4 (925 with 2) -- profiles/r05/ab_acc_order*.txt.
-  // KZGMI_ACC_ORDER, KZGMI_ACC_ORDER_SMALL (0: off)
+  // 1028/s with D = 4 (925 with 2) -- profiles/r05/ab_acc_order*.txt.  Only where every slot has
+  // a hardware queue of its own: a stream waiting for the event holds up the other slots of its
+  // queue (at the default 4 queues 2^20 batches ran 160 vs 173/s with the order).
+  // KZGMI_ACC_ORDER, KZGMI_ACC_ORDER_SMALL (0: off; set: also on shared queues)
   static constexpr int kAccOrderMax = 8;
   static constexpr size_t ACC_ORDER_WIDE = size_t(1) << 23;
   int acc_order = 2, acc_order_small = 4;
@@ -1111,9 +1113,6 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
   if (const char* e = getenv("KZGMI_SMALL_TERMS")) c->small_terms = (uint32_t)strtoul(e, nullptr, 10);
   if (const char* e = getenv("KZGMI_HOST_CHUNKS")) c->host_chunks_env = std::max(1, atoi(e));
   if (const char* e = getenv("KZGMI_HOST_CHUNK_MODE")) c->host_chunk_mode = atoi(e);
-  if (const char* e = getenv("KZGMI_ACC_ORDER")) c->acc_order = std::min(std::max(0, atoi(e)), kzgmi_ctx::kAccOrderMax);
-  if (const char* e = getenv("KZGMI_ACC_ORDER_SMALL"))
-    c->acc_order_small = std::min(std::max(0, atoi(e)), kzgmi_ctx::kAccOrderMax);
   // HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 unless set before the runtime
   // starts) and serialises the streams of one queue, so every slot in flight needs a queue of its
   // own (16 slots on 24 queues pipeline; 24 on 24 ran 3.6x slower).  The runtime keeps that many
@@ -1138,6 +1137,10 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
                       "slots sharing a queue run one after another\n",
               pipeline_slots, queues * c->prio_levels, c->prio_levels);
   }
+  if (pipeline_slots + 1 > queues * c->prio_levels) c->acc_order = c->acc_order_small = 0;  // shared queues
+  if (const char* e = getenv("KZGMI_ACC_ORDER")) c->acc_order = std::min(std::max(0, atoi(e)), kzgmi_ctx::kAccOrderMax);
+  if (const char* e = getenv("KZGMI_ACC_ORDER_SMALL"))
+    c->acc_order_small = std::min(std::max(0, atoi(e)), kzgmi_ctx::kAccOrderMax);
   bool okc = hipStreamCreateWithFlags(&c->h2d_stream, hipStreamNonBlocking) == hipSuccess;
   c->slots.resize(pipeline_slots);
   c->user_slots = pipeline_slots;
