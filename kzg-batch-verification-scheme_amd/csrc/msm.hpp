@@ -1150,8 +1150,9 @@ __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const
 //   W = sum_g (R'_g + U_g) + 8 sum_g V_g + SEG * sum_g g U_g,   sum_g g U_g = sum_j 2^j B_j,
 //   B_j = sum of the NSEG / 2 U_g whose index g has bit j set (j < SEG_BITS: 11 for c = 16).
 // k_reduce_bits: RB_PARTS workgroups per set -- SEG_BITS compute B_j, 4 compute quarter sums of
-// R'_g + U_g, 2 compute half sums of V_g -- each a few points per thread (c = 16: 4) + an
-// 8-level LDS tree.  k_reduce_bits_finish: one wave per set, Horner over the bit sums, then
+// R'_g + U_g, 2 compute half sums of V_g -- each a few points per thread (c = 16: 4), two levels
+// of a thread-serial LDS tree, then 6 levels in lane-parallel arithmetic (single-batch reduce
+// phase 0.853 -> 0.759 ms at 2^20, 0.55 -> 0.42 ms at 2^17: profiles/r05/ab_reduce_bits_lp.txt).  k_reduce_bits_finish: one wave per set, Horner over the bit sums, then
 // 2 H + sum V, 3 doublings: 16 H + 8 sum V.
 constexpr int RB_PARTS = Win<WBITS>::RB_PARTS;  // c = 16 (the most parts per set)
 
@@ -1188,7 +1189,8 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
         v = x29_add<Cv, Q>(v, load_x29<Q>(U29, base + q));
       }
     }
-    for (int st = 128; st >= 1; st >>= 1) {  // LDS tree, one coordinate word per row
+    // two levels of the thread-serial LDS tree (256 -> 64 sums), one coordinate word per row
+    for (int st = 128; st >= 64; st >>= 1) {
       if (t >= (uint32_t)st && t < 2u * st) {
 #pragma unroll
         for (int k = 0; k < N; ++k) {
@@ -1214,7 +1216,66 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
       }
       __syncthreads();
     }
-    if (t == 0) store_xyzz(&parts[(size_t)set * RBP + j], x29_to32<Cv, Q>(v));
+    // the last 6 levels (64 -> 1) in lane-parallel arithmetic, one point addition per wave at a
+    // time: a thread-serial level costs one serial addition (~25 us at this occupancy), a
+    // lane-parallel addition ~1.5 us, and the upper levels have few additions to spread
+    constexpr int LPW = 4 * 16 + 1;  // a point: x, y, zz, zzz (16 lanes each), the infinity flag
+    uint32_t(*lpn)[LPW] = reinterpret_cast<uint32_t(*)[LPW]>(&lds29[0][0]);
+    static_assert(sizeof(lds29) >= sizeof(uint32_t) * 64 * LPW, "LDS for 64 lane-parallel points");
+    if (t < 64) {  // radix-29 limbs as they are (zero above N)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        lpn[t][k] = k < N ? v.x.v[k < N ? k : 0] : 0u;
+        lpn[t][16 + k] = k < N ? v.y.v[k < N ? k : 0] : 0u;
+        lpn[t][32 + k] = k < N ? v.zz.v[k < N ? k : 0] : 0u;
+        lpn[t][48 + k] = k < N ? v.zzz.v[k < N ? k : 0] : 0u;
+      }
+      lpn[t][64] = v.inf ? 1u : 0u;
+    }
+    __syncthreads();
+    const LpCtx<Cv> c = lp_ctx<Cv>();
+    const uint32_t wave = t >> 6, lane16 = t & 15;
+    auto lp_get = [&](uint32_t k) {
+      LpXyzz<Cv> P;
+      P.x = (int32_t)lpn[k][lane16];
+      P.y = (int32_t)lpn[k][16 + lane16];
+      P.zz = (int32_t)lpn[k][32 + lane16];
+      P.zzz = (int32_t)lpn[k][48 + lane16];
+      P.inf = __builtin_amdgcn_readfirstlane((int)lpn[k][64]) != 0;
+      return P;
+    };
+    auto lp_put = [&](uint32_t k, const LpXyzz<Cv>& P) {
+      if ((t & 63) < 16) {
+        lpn[k][lane16] = (uint32_t)P.x;
+        lpn[k][16 + lane16] = (uint32_t)P.y;
+        lpn[k][32 + lane16] = (uint32_t)P.zz;
+        lpn[k][48 + lane16] = (uint32_t)P.zzz;
+      }
+      if ((t & 63) == 0) lpn[k][64] = P.inf ? 1u : 0u;
+    };
+    if constexpr (LpQ<Cv>::N != N) {  // BN254: x R29 (R29 = 2^261) -> x R (2^290), one product step per point
+      int32_t from29 = 0;
+#pragma unroll
+      for (int q = 0; q < LpQ<Cv>::N; ++q)
+        if (lane16 == (uint32_t)q) from29 = (int32_t)LpQ<Cv>::FROM29[q];
+#pragma unroll 1
+      for (uint32_t k = wave; k < 64; k += 4) {
+        LpXyzz<Cv> P = lp_get(k);
+        lp_step4(c, P.x, P.x, from29, P.y, P.y, from29, P.zz, P.zz, from29, P.zzz, P.zzz, from29);
+        lp_put(k, P);
+      }
+      __syncthreads();
+    } else {
+      static_assert(LpQ<Cv>::N == N, "BLS12-381: radix-29 record limbs are the lane-parallel limbs (R29 = R)");
+    }
+#pragma unroll 1
+    for (uint32_t half = 32; half >= 1; half >>= 1) {
+      // each sum q < half read and written by one wave; the sums >= half only read
+#pragma unroll 1
+      for (uint32_t q = wave; q < half; q += 4) lp_put(q, lp_xyzz_add(c, lp_get(q), lp_get(q + half)));
+      __syncthreads();
+    }
+    if (wave == 0) lp_store_xyzz(c, &parts[(size_t)set * RBP + j], lp_get(0));
   }
 }
 

@@ -6,11 +6,11 @@ time covered by at least one k_accumulate, the time covered by two or more, the 
 kernel at all, and -- over the time with no k_accumulate -- each kernel's share of the covered
 time (a kernel's wall time there divided by the number of kernels running alongside it).
 
-python tools/trace_gaps.py <run_kernel_trace.csv> [LO:HI]
+python tools/trace_gaps.py <run_kernel_trace.csv> [LO:HI | sI-J]
 
 LO:HI restricts the window to the k_accumulate launches inside [LO, HI] ms from the first one
 (e.g. the timed region, which follows the warm-up's drain; the segment list printed first shows
-where the drains are).
+where the drains are); sI-J restricts it to segments I..J of that list (0-based).
 """
 import collections
 import csv
@@ -38,7 +38,11 @@ def main(path):
     print("k_accumulate segments (launches, then the gap to the next in ms): " +
           ", ".join("%d (%.2f)" % (len(s), g / 1e6) for s, g in segs))
     t0, t1 = acc[0][0], acc[-1][1]
-    if len(sys.argv) > 2:  # a time window in ms from the first k_accumulate
+    if len(sys.argv) > 2 and sys.argv[2].startswith("s"):  # segments I..J (0-based) of the list
+        i, _, j = sys.argv[2][1:].partition("-")
+        acc = [a for s, _ in segs[int(i):int(j or i) + 1] for a in s]
+        t0, t1 = acc[0][0], acc[-1][1]
+    elif len(sys.argv) > 2:  # a time window in ms from the first k_accumulate
         lo, hi = (float(x) for x in sys.argv[2].split(":"))
         acc = [a for a in acc if a[0] >= t0 + lo * 1e6 and a[1] <= t0 + hi * 1e6]
         t0, t1 = acc[0][0], acc[-1][1]
