@@ -25,7 +25,10 @@
  *     queues per stream priority (4 by default) and streams sharing a queue run one after
  *     another: when the slots outnumber the queues the slot streams cycle through the device's
  *     stream priorities (KZGMI_STREAM_PRIO=0/1 forces it off/on), which keeps 16 slots at 0.96
- *     of their 24-queue rate at the default 4 queues.  A caller that produced device inputs on
+ *     of their 24-queue rate at the default 4 queues.  With a queue per slot, the batches'
+ *     bucket accumulations also start in submission order (at most 2 -- 4 for small batches --
+ *     at once; KZGMI_ACC_ORDER / KZGMI_ACC_ORDER_SMALL), so slots complete in the order they were
+ *     submitted.  A caller that produced device inputs on
  *     another stream (e.g. a torch stream) must order the slot's next job after it --
  *     kzgmi_stream_wait(ctx, slot, stream) (no host sync), or synchronise that stream -- before
  *     the call that reads them.  Device outputs
