@@ -333,6 +333,9 @@ __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t
 }
 
 // one workgroup per coarse bin g: LDS counting sort of its entries by the low 7 key bits.
+// Packed entries of a staged bin (the common case: 2^20 BLS12-381 batches average ~4 K entries per
+// bin) are read once, into registers, and the histogram atomics return each entry's rank in its
+// bucket (sort phase 0.368 -> 0.329 ms, profiles/r05/ab_fine_sort_one_read.txt); the rest:
 // Both passes over the bin's entries issue FINE_ILP independent loads per thread before
 // using them (the loops are latency-bound otherwise).  Bins of up to FINE_STAGE entries are
 // sorted into an LDS staging array and then written out contiguously (coalesced stores; the
@@ -422,6 +425,52 @@ __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ 
   const bool staged = count <= (uint32_t)FINE_STAGE;
   if (t < FINE) fine[t] = 0;
   __syncthreads();
+  using R = typename E::R;
+  if constexpr (sizeof(R) == 4) {
+    if (staged) {  // packed entries of a staged bin: ONE read, the histogram atomics return the ranks
+      constexpr int PER = FINE_STAGE / 256;
+      R v[PER];
+      uint32_t rank[PER];
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const uint32_t e = j * 256 + t;
+        v[j] = e < count ? tmp.load(start + e) : kNoEnt<R>;
+      }
+#pragma unroll
+      for (int j = 0; j < PER; ++j) rank[j] = v[j] != kNoEnt<R> ? atomicAdd(&fine[E::fine(v[j])], 1u) : 0u;
+      __syncthreads();
+      const uint32_t tot = t < FINE ? fine[t] : 0u;
+      if (t < FINE) scan[t] = tot;
+      __syncthreads();
+      for (int d = 1; d < FINE; d <<= 1) {  // Hillis-Steele, threads 0..127
+        const uint32_t x = (t < FINE && t >= (uint32_t)d) ? scan[t - d] : 0u;
+        __syncthreads();
+        if (t < FINE) scan[t] += x;
+        __syncthreads();
+      }
+      if (t < FINE) {
+        const uint32_t key = g * FINE + t;
+        off[key] = start + scan[t] - tot;
+        cnt[key] = tot;
+      }
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        if (v[j] == kNoEnt<R>) continue;
+        const uint32_t f = E::fine(v[j]);
+        stage[scan[f] - fine[f] + rank[j]] = E::val(v[j]) | (rank[j] == 0 ? SV_FIRST : 0u);
+      }
+      __syncthreads();
+      for (uint32_t p = t; p < count; p += 256) {
+        uint32_t b = 0;  // smallest b with scan[b] > p
+#pragma unroll
+        for (int step = FINE / 2; step >= 1; step >>= 1)
+          if (scan[b + step - 1] <= p) b += step;
+        sorted_val[start + p] = stage[p];
+        sorted_key[start + p] = g * FINE + b;
+      }
+      return;
+    }
+  }
   for (uint32_t e0 = t; e0 < count; e0 += 256 * FINE_ILP) {
     uint32_t k[FINE_ILP];  // fine index, FINE = none
 #pragma unroll
