@@ -31,13 +31,13 @@ def ctx():
     c.close()
 
 
-def _context_with_env(**env):
+def _context_with_env(slots=2, **env):
     """A kzgmi.Context created with the given environment overrides (read at creation)."""
     import kzgmi
     saved = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
-        return kzgmi.Context(0, 2)
+        return kzgmi.Context(0, slots)
     finally:
         for k, v in saved.items():
             if v is None:
@@ -503,6 +503,62 @@ def test_async_slots(ctx, curve, torch_dev):
     ctx.batch_verify_async(srs, 1, Cm, z, y_bad, P, n, seed=seed)
     assert ctx.wait(0) is True
     assert ctx.wait(1) is False
+
+
+def test_async_accumulation_order(torch_dev):
+    """The accumulation order across slots (api.hip kzgmi_ctx::acc_order, forced on here although 8
+    slots may share hardware queues): 20 batches of four sizes (both order depths: 2^18 is above
+    ACC_ORDER_WIDE) and pipelined MSMs on 8 slots, verdicts and MSM results as submitted, the
+    last slots collected out of submission order."""
+    torch = torch_dev
+    curve = "bls12_381"
+    C = pc.CURVES[curve]
+    c8 = _context_with_env(8, KZGMI_ACC_ORDER="2", KZGMI_ACC_ORDER_SMALL="3")
+    try:
+        tau = 0x5EED
+        g2 = pk.g2_to_bytes(C.g2, C)
+        srs = c8.load_srs(curve, g2, O.g2_mul(curve, g2, tau))
+        seed = hashlib.sha256(b"order").digest()
+        batches = {}
+        sizes = (3000, 20000, 1 << 17, 1 << 18)  # 2^18: 10.5 M window entries, the large-call order depth
+        for n in sizes:
+            Cm, z, y, P = _gen_batch(c8, torch, curve, n, tau, seed)
+            y_bad = y.clone()
+            y_bad[32 * (n // 2) + 31] ^= 1
+            batches[n] = (Cm, z, y, P, y_bad)
+        rng = random.Random(5)
+        m = 2048
+        pts = O.g1_mul_gen(curve, b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(m)), m)
+        sc = b"".join(pk.fr_to_bytes(rng.randrange(C.r)) for _ in range(m))
+        dp = torch.frombuffer(bytearray(pts), dtype=torch.uint8).cuda()
+        ds = torch.frombuffer(bytearray(sc), dtype=torch.uint8).cuda()
+        want_msm = O.msm_g1(curve, pts, sc, m)
+        pending = {}  # slot -> expected outcome ("msm" or a verdict)
+
+        def collect(s):
+            exp = pending.pop(s)
+            if exp == "msm":
+                assert c8.msm_wait(s) == want_msm, s
+            else:
+                assert c8.wait(s) is exp, s
+
+        for k in range(20):
+            s = (5 * k) % 8
+            if s in pending:
+                collect(s)
+            if k % 7 == 3:
+                c8.msm_g1_async(curve, s, dp, ds, m)
+                pending[s] = "msm"
+                continue
+            n = sizes[k % 4]
+            Cm, z, y, P, y_bad = batches[n]
+            bad = k % 5 == 1
+            c8.batch_verify_async(srs, s, Cm, z, y_bad if bad else y, P, n, seed=seed)
+            pending[s] = not bad
+        for s in sorted(pending, reverse=True):  # newest-first is not submission order
+            collect(s)
+    finally:
+        c8.close()
 
 
 @pytest.mark.parametrize("curve", CURVES)
