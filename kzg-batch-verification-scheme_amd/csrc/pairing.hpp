@@ -27,15 +27,19 @@ struct G2Aff {
   Fp2<Cv> x, y;
 };
 
+// digit i of the Miller loop scalar: +1 (LOOP), -1 (LOOP_NEG: BN254's 6u + 2 runs in NAF, 21
+// additions of +-Q instead of 36 of Q), or 0
 template <class Cv>
-KZ_DEV int loop_bit(int i) { return (Cv::K::LOOP[i >> 5] >> (i & 31)) & 1; }
+KZ_DEV int loop_digit(int i) {
+  return (int)((Cv::K::LOOP[i >> 5] >> (i & 31)) & 1) - (int)((Cv::K::LOOP_NEG[i >> 5] >> (i & 31)) & 1);
+}
 
 template <class Cv>
 constexpr int num_lines() {
   int n = 0;
   for (int i = Cv::K::LOOP_BITS - 2; i >= 0; --i) {
     n += 1;
-    n += (Cv::K::LOOP[i >> 5] >> (i & 31)) & 1;
+    n += ((Cv::K::LOOP[i >> 5] | Cv::K::LOOP_NEG[i >> 5]) >> (i & 31)) & 1;
   }
   return Cv::M_TWIST ? n : n + 2;
 }
@@ -77,11 +81,13 @@ __global__ void k_precompute_lines(const G2Aff<Cv>* __restrict__ q_in, Line<Cv>*
   constexpr int NL = num_lines<Cv>();
   Line<Cv>* out = lines + k * NL;
   G2Aff<Cv> Q = q_in[k];
+  const G2Aff<Cv> negQ = {Q.x, f2_neg(Q.y)};
   G2Aff<Cv> T = Q;
   int idx = 0;
   for (int i = Cv::K::LOOP_BITS - 2; i >= 0; --i) {
     line_dbl(T, out[idx++]);
-    if (loop_bit<Cv>(i)) line_add(T, Q, out[idx++]);
+    const int d = loop_digit<Cv>(i);
+    if (d) line_add(T, d > 0 ? Q : negQ, out[idx++]);  // the line through T and -Q for a -1 digit
   }
   if constexpr (!Cv::M_TWIST) {
     G2Aff<Cv> Q1 = g2_frob(Q);
@@ -129,7 +135,7 @@ KZ_DEV Fp12<Cv> miller2(const Line<Cv>* lines, const Homog<Cv> (&P)[2], const bo
     for (int k = 0; k < 2; ++k)
       if (!skip[k]) f = mul_line_at(f, lines[k * NL + idx], P[k]);
     ++idx;
-    if (loop_bit<Cv>(i)) {
+    if (loop_digit<Cv>(i)) {  // the precomputed line through T and +-Q
 #pragma unroll
       for (int k = 0; k < 2; ++k)
         if (!skip[k]) f = mul_line_at(f, lines[k * NL + idx], P[k]);

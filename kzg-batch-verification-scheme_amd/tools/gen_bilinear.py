@@ -497,11 +497,27 @@ XABS = 0xD201000000010000
 BN_U = 4965661367192848881
 
 
-def num_lines(cv):
+def naf(k):
+    """Non-adjacent form of k > 0, least significant digit first."""
+    d = []
+    while k:
+        z = 2 - (k & 3) if k & 1 else 0
+        d.append(z)
+        k = (k - z) >> 1
+    return d
+
+
+def loop_digits(cv):
+    """The Miller loop's digits below the top one, most significant first (csrc/params_gen.hpp
+    LOOP / LOOP_NEG): |x| in binary for BLS12-381, the NAF of 6u + 2 for BN254."""
     lp = LOOP[cv]
-    n = 0
-    for i in range(lp.bit_length() - 2, -1, -1):
-        n += 1 + ((lp >> i) & 1)
+    d = naf(lp) if cv == "bn254" else [(lp >> i) & 1 for i in range(lp.bit_length())]
+    assert d[-1] == 1 and sum(v << i if v >= 0 else -(1 << i) for i, v in enumerate(d)) == lp
+    return d[-2::-1]
+
+
+def num_lines(cv):
+    n = sum(1 + (dg != 0) for dg in loop_digits(cv))
     return n if cv == "bls12_381" else n + 2
 
 
@@ -590,10 +606,9 @@ def op_shape(name, cv):
 def build_program(cv):
     P = Prog(cv)
     f, t, g = P.g(0), P.g(1), P.g(2)
-    lp = LOOP[cv]
     idx = 0
     first = True
-    for i in range(lp.bit_length() - 2, -1, -1):
+    for dg in loop_digits(cv):
         if first:
             P.op("LL", P.e(idx), P.e(idx) + 6, f)
             first = False
@@ -601,7 +616,7 @@ def build_program(cv):
             P.op2("SQR", f, None, t, "LL", P.e(idx), P.e(idx) + 6, g)
             P.op("MUL", t, g, f)
         idx += 1
-        if (lp >> i) & 1:
+        if dg:  # the precomputed lines through T and +-Q
             P.op("LL", P.e(idx), P.e(idx) + 6, g)
             P.op("MUL", f, g, t)
             P.copy(f, t)
@@ -633,17 +648,21 @@ def build_program(cv):
     P.op("MUL", r5, g, r6)           # r6 = gg (cyclotomic)
     gg = r6
 
-    def cyclo_pow(dst, a, tmp, e):
-        # ping-pong between dst and tmp; a copy only if the result ends in tmp
+    def cyclo_pow(dst, a, tmp, e, conj_reg=None):
+        # ping-pong between dst and tmp; a copy only if the result ends in tmp.  conj_reg: signed
+        # digits (NAF) -- a^-1 = conj(a) in the cyclotomic subgroup, one CONJ round into conj_reg
+        digits = naf(e)[-2::-1] if conj_reg is not None else [(e >> i) & 1 for i in range(e.bit_length() - 2, -1, -1)]
+        if conj_reg is not None and -1 in digits:
+            P.op("CONJ", a, None, conj_reg)
         cur, oth = None, None
-        for i in range(e.bit_length() - 2, -1, -1):
+        for dg in digits:
             src = a if cur is None else cur
             nxt = tmp if cur != tmp else dst
             P.op("CYC", src, None, nxt)
             cur = nxt
-            if (e >> i) & 1:
+            if dg:
                 nxt = dst if cur == tmp else tmp
-                P.op("MUL", cur, a, nxt)
+                P.op("MUL", cur, a if dg > 0 else conj_reg, nxt)
                 cur = nxt
         if cur != dst:
             P.copy(dst, cur)
@@ -664,9 +683,10 @@ def build_program(cv):
     else:
         U = BN_U
         fu, fu2, fu3 = P.g(8), P.g(9), P.g(10)
-        cyclo_pow(fu, gg, t, U)
-        cyclo_pow(fu2, fu, t, U)
-        cyclo_pow(fu3, fu2, t, U)
+        ca = P.g(12)  # conj of the base: free until k_a below
+        cyclo_pow(fu, gg, t, U, ca)   # u in NAF: 24 nonzero digits instead of 28 set bits
+        cyclo_pow(fu2, fu, t, U, ca)
+        cyclo_pow(fu3, fu2, t, U, ca)
         sq = lambda d, a: P.op("CYC", a, None, d)  # noqa: E731
         mul = lambda d, a, b: P.op("MUL", a, b, d)  # noqa: E731
         x1, x2, x3 = r4, r5, r7
@@ -722,16 +742,15 @@ def check_program(cv, tables, P, res):
         return from_w([a, z, b, c, z, z] if cv == "bls12_381" else [a, b, z, c, z, z])
     one = [1] + [0] * 11
     f = one
-    lp = LOOP[cv]
     idx = 0
     first = True
-    for i in range(lp.bit_length() - 2, -1, -1):
+    for dg in loop_digits(cv):
         l = from_w(wmul(to_w(line_full(R[P.R_E + 12 * idx:P.R_E + 12 * idx + 6])),
                         to_w(line_full(R[P.R_E + 12 * idx + 6:P.R_E + 12 * idx + 12])), cv))
         f = l if first else from_w(wmul(to_w(from_w(wmul(to_w(f), to_w(f), cv))), to_w(l), cv))
         first = False
         idx += 1
-        if (lp >> i) & 1:
+        if dg:
             l = from_w(wmul(to_w(line_full(R[P.R_E + 12 * idx:P.R_E + 12 * idx + 6])),
                             to_w(line_full(R[P.R_E + 12 * idx + 6:P.R_E + 12 * idx + 12])), cv))
             f = from_w(wmul(to_w(f), to_w(l), cv))

@@ -146,6 +146,23 @@ def glv_lines(p, r, g1, n, M, lam=None):
     ]
 
 
+def naf_masks(k):
+    """Non-adjacent form of k > 0 as (mask of +1 digits, mask of -1 digits)."""
+    pos = neg = 0
+    i = 0
+    while k:
+        if k & 1:
+            d = 2 - (k & 3)  # +1 or -1
+            k -= d
+            if d > 0:
+                pos |= 1 << i
+            else:
+                neg |= 1 << i
+        k >>= 1
+        i += 1
+    return pos, neg
+
+
 def window_steps(e, w=4):
     """Sliding-window (width w) left-to-right schedule for x^e: the first odd window value
     (table index), then (squarings, table index or 255 = none) pairs.  Table k = x^(2k+1)."""
@@ -239,8 +256,14 @@ def main():
             gam.append("{" + ", ".join(row) + "}")
         out.append("  static constexpr uint32_t FROB[3][6][2][%d] = {%s};" % (n, ", ".join(gam)))
         lp = c["loop"]
-        out.append("  static constexpr int LOOP_BITS = %d;" % lp.bit_length())
-        out.append("  static constexpr uint32_t LOOP[3] = %s;" % arr(lp, 3))
+        if "u" in c:  # BN254: the Miller loop over the NAF of 6u + 2 (21 additions instead of 36)
+            pos, neg = naf_masks(lp)
+            nbits = max(pos.bit_length(), neg.bit_length())
+        else:         # BLS12-381: |x| in binary (its NAF has as many nonzero digits)
+            pos, neg, nbits = lp, 0, lp.bit_length()
+        out.append("  static constexpr int LOOP_BITS = %d;  // digits of the loop scalar (top digit 1)" % nbits)
+        out.append("  static constexpr uint32_t LOOP[3] = %s;      // digits +1" % arr(pos, 3))
+        out.append("  static constexpr uint32_t LOOP_NEG[3] = %s;  // digits -1" % arr(neg, 3))
         if "u" in c:
             out.append("  static constexpr uint64_t U = 0x%016xull;" % c["u"])
         else:
