@@ -218,3 +218,28 @@ def test_ragged_msm_vs_oracle(ctx, curve, n, trusted):
     finally:
         ctx.set_trusted_g1(False)
     assert got == O.msm_g1(curve, _host(pts), sc.tobytes(), n)
+
+
+# the path switches of a batch call: the one-wave-per-term small path up to 4096 MSM terms (3n + 1
+# for BLS12-381, 4n + 2 for BN254's GLV halves), 13-bit windows from 2^15 + 1 tuples, 16-bit
+# windows and the 2^23-entry accumulation order depth above 2^17 (api.hip run_msm_core, call_wbits)
+@pytest.mark.parametrize("curve,n", [("bls12_381", 1365), ("bls12_381", 1366), ("bls12_381", 32768),
+                                     ("bls12_381", 32769), ("bls12_381", 131072), ("bls12_381", 131073),
+                                     ("bn254", 1023), ("bn254", 1024), ("bn254", 32769)])
+def test_batch_path_boundaries_vs_oracle(ctx, curve, n):
+    """A, B and the verdict bit-exact vs the oracle on both sides of every size switch, then a
+    corrupted y in the middle tuple flips the verdict."""
+    C = pc.CURVES[curve]
+    tau = 0xB0DA + n
+    Cm, z, y, P = _gen_batch(ctx, curve, n, tau, hashlib.sha256(b"boundary%d" % n).digest())
+    g2 = pk.g2_to_bytes(C.g2, C)
+    tg2 = O.g2_mul(curve, g2, tau)
+    srs = ctx.load_srs(curve, g2, tg2)
+    vseed = hashlib.sha256(b"boundary-verify%d" % n).digest()
+    assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n) is True
+    A, B = ctx.last_combination(curve)
+    hb = [_host(t) for t in (Cm, z, y, P)]
+    ok, Ao, Bo = O.batch_verify(curve, hb[0], hb[1], hb[2], hb[3], n, g2, tg2, vseed, want_ab=True)
+    assert ok is True and A == Ao and B == Bo
+    y[32 * (n // 2) + 31] ^= 1
+    assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n) is False
