@@ -17,27 +17,38 @@ void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const 
   with_wbits(wbits, [&](auto wb) {
     constexpr int WB = decltype(wb)::value;
     const uint32_t nbins = nsets * Win<WB>::BINS;
+    SetShift ss;
+    if (!set_shifts_host<WB>(tl, nsets, ss)) {
+      fprintf(stderr, "kzgmi: %u bucket sets exceed MAX_SETS\n", nsets);
+      abort();
+    }
     uint32_t* ccnt = coarse;
     uint32_t* coff = coarse + nbins;
     uint32_t* ccur = coarse + 2 * nbins;
     (void)hipMemsetAsync(ccnt, 0, (size_t)nbins * 4, st);
     const uint32_t tiles = num_tiles_host(tl);
-    if (tl.total) k_digits_count<WB><<<num_digit_groups_host(tl), 256, 0, st>>>(tl, inf, digits, ccnt);
+    bool uniform = true;
+    for (uint32_t s = 0; s < nsets; ++s) uniform &= ss.s[s] == COARSE_SHIFT;
+    if (tl.total && uniform) k_digits_count<WB, true><<<num_digit_groups_host(tl), 256, 0, st>>>(tl, ss, inf, digits, ccnt);
+    else if (tl.total) k_digits_count<WB, false><<<num_digit_groups_host(tl), 256, 0, st>>>(tl, ss, inf, digits, ccnt);
     k_bin_scan<<<1, 1024, 0, st>>>(ccnt, nbins, coff, ccur, total);
     // coarse-pass entries (msm.hpp EntPacked / EntSplit): packed 4 B when every sorted value (point
     // index << 1 | sign) fits CV_BITS, else 4 B values + 1 B fine indices (ent holds emax x 8 B)
     uint64_t npts = 0;
     for (uint32_t k = 0; k < tl.nclass; ++k)
       if (tl.c[k].count) npts = std::max<uint64_t>(npts, (uint64_t)tl.c[k].pt_base + tl.c[k].count);
-    if (!force_split && 2 * npts < (1ull << CV_BITS)) {
-      const EntPacked e{reinterpret_cast<uint32_t*>(ent)};
-      if (tiles) k_bin_scatter<EntPacked, WB><<<tiles, 256, 0, st>>>(tl, digits, ccur, e);
-      k_fine_sort<EntPacked><<<nbins, 256, 0, st>>>(coff, ccnt, e, off, cnt, sval, skey);
-    } else {
-      const EntSplit e{reinterpret_cast<uint32_t*>(ent), reinterpret_cast<uint8_t*>(ent) + 4 * emax};
-      if (tiles) k_bin_scatter<EntSplit, WB><<<tiles, 256, 0, st>>>(tl, digits, ccur, e);
-      k_fine_sort<EntSplit><<<nbins, 256, 0, st>>>(coff, ccnt, e, off, cnt, sval, skey);
-    }
+    auto scatter_and_sort = [&](auto e, auto uni) {
+      using E = decltype(e);
+      constexpr bool U = decltype(uni)::value;
+      if (tiles) k_bin_scatter<E, WB, U><<<tiles, 256, 0, st>>>(tl, ss, digits, ccur, e);
+      k_fine_sort<E, WB, U><<<nbins, 256, 0, st>>>(coff, ccnt, e, off, cnt, sval, skey, ss);
+    };
+    auto with_uniform = [&](auto e) {
+      if (uniform) scatter_and_sort(e, std::true_type{});
+      else scatter_and_sort(e, std::false_type{});
+    };
+    if (!force_split && 2 * npts < (1ull << CV_BITS)) with_uniform(EntPacked{reinterpret_cast<uint32_t*>(ent)});
+    else with_uniform(EntSplit{reinterpret_cast<uint32_t*>(ent), reinterpret_cast<uint8_t*>(ent) + 4 * emax});
   });
 }
 

@@ -57,6 +57,17 @@ struct TermList {
   uint32_t total;
 };
 
+// Coarse-bin width per bucket set: bin = (|d| - 1) >> s[set].  A full window spreads over every
+// bucket (s = COARSE_SHIFT: 128 buckets per bin); a window cut short by the top of its scalars
+// does not: 13-bit windows keep 8 bits of a 255-bit scalar in the top one, and with 128-bucket
+// bins its 2^17 terms fell into 2 bins of 64 K entries, each sorted by one workgroup in 16 chunks
+// (k_fine_sort 0.18 ms of a 2^17 batch).  Narrower bins (s = top bits - log2(bins)) spread such a
+// window over every bin; k_fine_sort writes the counts of the buckets no bin covers as 0.
+constexpr int MAX_SETS = 64;
+struct SetShift {
+  uint8_t s[MAX_SETS];
+};
+
 // ------------------------------------------------------------------------------ sort
 // Entries (one per nonzero signed window digit) are grouped by global bucket id
 // key = set * 2^15 + (|d| - 1) with a two-pass MSD partition that keeps the atomics in LDS:
@@ -90,7 +101,32 @@ struct Win {
   static constexpr int MAXW = 256 / C + 1;               // windows of a 256-bit scalar (+ carry)
   static constexpr int RB_PARTS = SEG_BITS + 6;         // k_reduce_bits parts per set
   static_assert(NSEG == (1 << SEG_BITS) && BINS <= 256 && BINS >= 1, "window width");
+  static constexpr int BINS_LOG2 = C - 1 - COARSE_SHIFT;
 };
+
+// SetShift of a call (host): per set, the widest bin any of its windows needs.  A window of a
+// class reads raw bits [w c, w c + c) of scalars below 2^127 (4-word: randomisers, GLV halves)
+// or 2^255 (8-word: Fr); a window with tb < c raw bits takes |d| <= 2^tb (its carry-in included,
+// no carry out), so bins of 2^(tb - log2 BINS) buckets cover it.
+template <int WB>
+inline bool set_shifts_host(const TermList& tl, uint32_t nsets, SetShift& ss) {
+  using W = Win<WB>;
+  if (nsets > (uint32_t)MAX_SETS) return false;
+  for (uint32_t s = 0; s < nsets; ++s) ss.s[s] = 0;
+  for (uint32_t k = 0; k < tl.nclass; ++k) {
+    const TermClass& C = tl.c[k];
+    if (!C.count) continue;
+    const int bits = C.scal_words == 4 ? 127 : 255;
+    for (uint32_t w = 0; w < C.nwin; ++w) {
+      const int tb = std::min(WB, std::max(0, bits - (int)(C.win_off + w) * WB));
+      const int need = tb >= WB - 1 ? COARSE_SHIFT : std::max(0, tb - W::BINS_LOG2);
+      const uint32_t s = C.set_base + w;
+      if (s >= nsets) return false;
+      ss.s[s] = (uint8_t)std::max<int>(ss.s[s], need);
+    }
+  }
+  return true;
+}
 // sorted value = point index << 1 | sign, | SV_FIRST on the first entry of each bucket (point
 // indices stay below 2^30: at most 16 x 2^26 commit-key points)
 constexpr uint32_t SV_FIRST = 1u << 31;
@@ -112,7 +148,7 @@ struct EntPacked {
   KZ_DEV void store(size_t i, R r) const { p[i] = r; }
   KZ_DEV static uint32_t fine(R r) { return r >> CV_BITS; }
   KZ_DEV static uint32_t val(R r) { return r & ((1u << CV_BITS) - 1); }
-  KZ_DEV static R make(uint32_t key, uint32_t v) { return ((key & (FINE - 1)) << CV_BITS) | v; }
+  KZ_DEV static R make(uint32_t fine, uint32_t v) { return ((fine & (FINE - 1)) << CV_BITS) | v; }
 };
 struct EntSplit {
   uint32_t* p;
@@ -126,7 +162,7 @@ struct EntSplit {
   }
   KZ_DEV static uint32_t fine(R r) { return (uint32_t)(r >> 32); }
   KZ_DEV static uint32_t val(R r) { return (uint32_t)r; }
-  KZ_DEV static R make(uint32_t key, uint32_t v) { return ((uint64_t)(key & (FINE - 1)) << 32) | v; }
+  KZ_DEV static R make(uint32_t fine, uint32_t v) { return ((uint64_t)(fine & (FINE - 1)) << 32) | v; }
 };
 // empty register slot (never a real entry: packed values stay below 2^CV_BITS - 1, fine < 128)
 template <class R>
@@ -199,8 +235,9 @@ inline uint32_t num_digit_groups_host(const TermList& tl) {
   for (uint32_t k = 0; k < tl.nclass; ++k) g += (tl.c[k].count + TILE_TERMS - 1) / TILE_TERMS;
   return g;
 }
-template <int WB>
-__global__ void __launch_bounds__(256) k_digits_count(TermList tl, const uint8_t* __restrict__ inf,
+// UNIFORM: every set at COARSE_SHIFT (16-bit windows: no window is cut short), the shift a constant
+template <int WB, bool UNIFORM>
+__global__ void __launch_bounds__(256) k_digits_count(TermList tl, SetShift ss, const uint8_t* __restrict__ inf,
                                                       uint32_t* __restrict__ digits,
                                                       uint32_t* __restrict__ coarse_cnt) {
   using W = Win<WB>;
@@ -214,6 +251,10 @@ __global__ void __launch_bounds__(256) k_digits_count(TermList tl, const uint8_t
   }
   const TermClass& C = tl.c[k];
   const uint32_t t = threadIdx.x;
+  uint32_t shw[W::MAXW];  // each window's coarse-bin shift, read once (uniform)
+#pragma unroll
+  for (int w = 0; w < W::MAXW; ++w)
+    shw[w] = UNIFORM ? (uint32_t)COARSE_SHIFT : ss.s[min(C.set_base + (uint32_t)w, (uint32_t)MAX_SETS - 1)];
   if (t < (uint32_t)W::BINS) {
 #pragma unroll
     for (int w = 0; w < W::MAXW; ++w) hist[w][t] = 0;
@@ -224,7 +265,7 @@ __global__ void __launch_bounds__(256) k_digits_count(TermList tl, const uint8_t
     const uint32_t i = b * TILE_TERMS + j * 256 + t;
     if (i >= C.count) break;
     term_digits<WB>(C, i, inf, [&](int w, uint32_t code) {
-      if (code) atomicAdd(&hist[w][((code & 0x7fffffffu) - 1) >> COARSE_SHIFT], 1u);
+      if (code) atomicAdd(&hist[w][((code & 0x7fffffffu) - 1) >> shw[w]], 1u);
       digits[C.dig_base + (size_t)w * C.count + i] = code;
     });
   }
@@ -271,8 +312,8 @@ static __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __rest
 // consecutive threads store consecutive addresses of a bin's run (the tile's run in each bin
 // is contiguous in `tmp`); writing each entry from the thread that ranked it scattered every
 // wavefront store over ~64 bins.
-template <class E, int WB = WBITS>
-__global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t* __restrict__ digits,
+template <class E, int WB = WBITS, bool UNIFORM = true>
+__global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, SetShift ss, const uint32_t* __restrict__ digits,
                                                      uint32_t* __restrict__ coarse_cursor, E tmp) {
   using W = Win<WB>;
   constexpr uint32_t NBIN = W::BINS;        // coarse bins per set (threads >= NBIN only rank)
@@ -284,6 +325,7 @@ __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t
   const TileRef T = tile_decode(tl, blockIdx.x);
   const TermClass& C = tl.c[T.k];
   const uint32_t set = C.set_base + T.w;
+  const uint32_t sh = UNIFORM ? (uint32_t)COARSE_SHIFT : ss.s[set];  // coarse-bin width of the set (SetShift)
   const uint32_t* dg = digits + C.dig_base + (size_t)T.w * C.count;
   const uint32_t t = threadIdx.x;
   if (t < NBIN) hist[t] = 0;
@@ -298,7 +340,7 @@ __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t
     const uint32_t mag = code & 0x7fffffffu;
     key[j] = set * W::NBUCKETS + (mag - 1);
     ent[j] = ((C.pt_base + local) << 1) | (code >> 31);
-    rank[j] = atomicAdd(&hist[(mag - 1) >> COARSE_SHIFT], 1u);
+    rank[j] = atomicAdd(&hist[(mag - 1) >> sh], 1u);
   }
   __syncthreads();
   const uint32_t h = t < NBIN ? hist[t] : 0u;
@@ -320,9 +362,10 @@ __global__ void __launch_bounds__(256) k_bin_scatter(TermList tl, const uint32_t
 #pragma unroll
   for (int j = 0; j < TILE_TERMS / 256; ++j) {
     if (key[j] == 0xffffffffu) continue;
-    const uint32_t bin = (key[j] >> COARSE_SHIFT) & (NBIN - 1);
+    const uint32_t m1 = key[j] & (W::NBUCKETS - 1);  // |d| - 1
+    const uint32_t bin = m1 >> sh;
     const uint32_t q = lstart[bin] + rank[j];
-    stage[q] = E::make(key[j], ent[j]);
+    stage[q] = E::make(m1 & ((1u << sh) - 1), ent[j]);  // the fine index within the bin
     stage_bin[q] = (uint8_t)bin;
   }
   __syncthreads();
@@ -354,7 +397,7 @@ constexpr int FINE_STAGE = 8192;
 // staging: chunks of FINE_STAGE / 2 keep the kernel within 128 VGPRs (4 workgroups per CU for
 // the staged bins, whose LDS allows 4).
 template <class E>
-KZ_DEV void fine_sort_chunks(uint32_t g, uint32_t start, uint32_t count, const E tmp,
+KZ_DEV void fine_sort_chunks(uint32_t kbase, uint32_t start, uint32_t count, const E tmp,
                              const uint32_t* bstart, uint32_t* cursor, uint32_t* stage,
                              uint32_t* __restrict__ sorted_val, uint32_t* __restrict__ sorted_key) {
   constexpr uint32_t CHUNK = FINE_STAGE / 2, PER = CHUNK / 256;  // 16 per thread: 147 -> <= 128 VGPRs
@@ -401,7 +444,7 @@ KZ_DEV void fine_sort_chunks(uint32_t g, uint32_t start, uint32_t count, const E
         if (cscan[b + step - 1] <= q) b += step;
       const uint32_t p = cursor[b] + q - (cscan[b] - ccnt[b]);  // position in the bin
       sorted_val[start + p] = stage[q] | (p == bstart[b] ? SV_FIRST : 0u);
-      sorted_key[start + p] = g * FINE + b;
+      sorted_key[start + p] = kbase + b;
     }
     __syncthreads();
     if (t < FINE) cursor[t] += ccnt[t];
@@ -409,12 +452,12 @@ KZ_DEV void fine_sort_chunks(uint32_t g, uint32_t start, uint32_t count, const E
   }
 }
 
-template <class E>
+template <class E, int WB, bool UNIFORM>
 __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ coarse_off,
                                                    const uint32_t* __restrict__ coarse_cnt, const E tmp,
                                                    uint32_t* __restrict__ off, uint32_t* __restrict__ cnt,
                                                    uint32_t* __restrict__ sorted_val,
-                                                   uint32_t* __restrict__ sorted_key) {
+                                                   uint32_t* __restrict__ sorted_key, SetShift ss) {
   __shared__ uint32_t fine[FINE];
   __shared__ uint32_t cursor[FINE];
   __shared__ uint32_t scan[FINE];  // inclusive bucket scan
@@ -423,6 +466,17 @@ __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ 
   const uint32_t start = coarse_off[g], count = coarse_cnt[g];
   const uint32_t t = threadIdx.x;
   const bool staged = count <= (uint32_t)FINE_STAGE;
+  // bin g = bin gl of set s: buckets kbase + [0, 2^sh) of the set's bins * FINE (SetShift)
+  constexpr uint32_t bins = Win<WB>::BINS;
+  const uint32_t s = g / bins, gl = g % bins, sh = UNIFORM ? (uint32_t)COARSE_SHIFT : ss.s[s];
+  const uint32_t kbase = s * bins * FINE + (gl << sh), nfine = 1u << sh;
+  if (sh < COARSE_SHIFT) {  // the set's buckets no bin covers: empty (this bin's share of them)
+    const uint32_t unc = FINE - nfine, ub = s * bins * FINE + (bins << sh) + gl * unc;
+    for (uint32_t u = t; u < unc; u += 256) {
+      off[ub + u] = start;
+      cnt[ub + u] = 0;
+    }
+  }
   if (t < FINE) fine[t] = 0;
   __syncthreads();
   using R = typename E::R;
@@ -448,8 +502,8 @@ __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ 
         if (t < FINE) scan[t] += x;
         __syncthreads();
       }
-      if (t < FINE) {
-        const uint32_t key = g * FINE + t;
+      if (t < nfine) {
+        const uint32_t key = kbase + t;
         off[key] = start + scan[t] - tot;
         cnt[key] = tot;
       }
@@ -466,7 +520,7 @@ __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ 
         for (int step = FINE / 2; step >= 1; step >>= 1)
           if (scan[b + step - 1] <= p) b += step;
         sorted_val[start + p] = stage[p];
-        sorted_key[start + p] = g * FINE + b;
+        sorted_key[start + p] = kbase + b;
       }
       return;
     }
@@ -495,15 +549,17 @@ __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ 
   if (t < FINE) {
     const uint32_t base = scan[t] - tot;
     cursor[t] = base;
-    const uint32_t key = g * FINE + t;
-    off[key] = start + base;
-    cnt[key] = tot;
+    if (t < nfine) {
+      const uint32_t key = kbase + t;
+      off[key] = start + base;
+      cnt[key] = tot;
+    }
   }
   __syncthreads();
   if (!staged) {
     if (t < FINE) scan[t] -= fine[t];  // bucket starts (exclusive scan); cursor[] is a copy
     __syncthreads();
-    fine_sort_chunks(g, start, count, tmp, scan, cursor, stage, sorted_val, sorted_key);
+    fine_sort_chunks(kbase, start, count, tmp, scan, cursor, stage, sorted_val, sorted_key);
     return;
   }
   for (uint32_t e0 = t; e0 < count; e0 += 256 * FINE_ILP) {
@@ -530,7 +586,7 @@ __global__ void __launch_bounds__(256) k_fine_sort(const uint32_t* __restrict__ 
     for (int step = FINE / 2; step >= 1; step >>= 1)
       if (scan[b + step - 1] <= p) b += step;
     sorted_val[start + p] = stage[p];
-    sorted_key[start + p] = g * FINE + b;
+    sorted_key[start + p] = kbase + b;
   }
 }
 
