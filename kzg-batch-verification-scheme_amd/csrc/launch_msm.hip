@@ -18,17 +18,15 @@ void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const 
     constexpr int WB = decltype(wb)::value;
     const uint32_t nbins = nsets * Win<WB>::BINS;
     SetShift ss;
-    if (!set_shifts_host<WB>(tl, nsets, ss)) {
-      fprintf(stderr, "kzgmi: %u bucket sets exceed MAX_SETS\n", nsets);
-      abort();
-    }
+    // more sets than the table holds: every set at the full 128-bucket bins (always correct)
+    const bool table = set_shifts_host<WB>(tl, nsets, ss);
     uint32_t* ccnt = coarse;
     uint32_t* coff = coarse + nbins;
     uint32_t* ccur = coarse + 2 * nbins;
     (void)hipMemsetAsync(ccnt, 0, (size_t)nbins * 4, st);
     const uint32_t tiles = num_tiles_host(tl);
     bool uniform = true;
-    for (uint32_t s = 0; s < nsets; ++s) uniform &= ss.s[s] == COARSE_SHIFT;
+    for (uint32_t s = 0; table && s < nsets; ++s) uniform &= ss.s[s] == COARSE_SHIFT;
     if (tl.total && uniform) k_digits_count<WB, true><<<num_digit_groups_host(tl), 256, 0, st>>>(tl, ss, inf, digits, ccnt);
     else if (tl.total) k_digits_count<WB, false><<<num_digit_groups_host(tl), 256, 0, st>>>(tl, ss, inf, digits, ccnt);
     k_bin_scan<<<1, 1024, 0, st>>>(ccnt, nbins, coff, ccur, total);
