@@ -102,6 +102,7 @@ struct Slot {
   DevBuf R, U, scratch, winsum, res, flags, stage, outb;
   DevBuf acc29;                                  // radix-29 bucket records (msm.hpp)
   DevBuf accq;                                   // k_accumulate's work-queue counter (large calls)
+  DevBuf crowd;                                  // k_fixup's list of crowded buckets (msm.hpp k_fixup_crowded)
   DevBuf fs_leaves, fs_tmp, fs_top, pow, chal;  // Fiat-Shamir / powers-of-r randomisers
   DevBuf glv_r, glv_s, glv_t;                    // GLV half scalars (glv.hpp): [h0 x n | h1 x n]
   DevBuf digits;                                 // signed window digit codes of every term (msm.hpp)
@@ -434,6 +435,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   CHK(s.ent.ensure(emax * 8));
   CHK(s.total.ensure(16));
   if (acc_threads) CHK(s.accq.ensure(16));
+  CHK(s.crowd.ensure(4 * (1 + 3 * (nchunks / FIX_LP_FROM + 2))));  // at most one per FIX_LP_FROM + 1 chunks
   CHK(s.sval.ensure(emax * 4 + 16));  // + 16: k_accumulate reads values 4 at a time, up to 3 past the end
   CHK(s.skey.ensure(emax * 4));
   constexpr int W29 = kW29<Fp29Of<Cv>>;
@@ -472,7 +474,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   }
   L::accumulate(st, nchunks, s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
                 OFF.template as<uint32_t>(), CNT.template as<uint32_t>(), pts, ACC.template as<uint32_t>(), NB,
-                acc_threads, acc_threads ? s.accq.template as<uint32_t>() : nullptr);
+                acc_threads, acc_threads ? s.accq.template as<uint32_t>() : nullptr, s.crowd.template as<uint32_t>());
   if (order_ev) HIPCHK(hipEventRecord(*order_ev, st));
   if (second)
     L::merge_buckets(st, NB, s.acc29.template as<uint32_t>(), s.cnt.template as<uint32_t>(),
@@ -1169,7 +1171,7 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
   for (auto& s : c->slots) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     DevBuf* bufs[] = {&s.pts, &s.inf, &s.scal_r, &s.scal_s, &s.scal_t, &s.tpart, &s.cnt, &s.off, &s.coarse, &s.ent,
-                      &s.total, &s.sval, &s.skey, &s.acc29, &s.accq, &s.R, &s.U, &s.scratch,
+                      &s.total, &s.sval, &s.skey, &s.acc29, &s.accq, &s.crowd, &s.R, &s.U, &s.scratch,
                       &s.winsum, &s.res, &s.flags, &s.stage, &s.outb, &s.fs_leaves, &s.fs_tmp,
                       &s.fs_top, &s.pow, &s.chal, &s.glv_r, &s.glv_s, &s.glv_t, &s.digits};
     for (DevBuf* b : bufs) b->release();

@@ -22,7 +22,7 @@ struct Launch {
   // store (k_fixup joins pieces into them; reduce reads them)
   static void accumulate(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* sval,
                          const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts,
-                         uint32_t* acc29, uint32_t nb, size_t acc_threads = 0, uint32_t* next_chunk = nullptr);
+                         uint32_t* acc29, uint32_t nb, size_t acc_threads, uint32_t* next_chunk, uint32_t* crowd);
   static void pts_to29(hipStream_t st, AF* pts, uint32_t n);  // in place
   // acc29[b] += acc29b[b] for the buckets with cntb[b] != 0, cnt[b] += cntb[b] (chunked batches)
   static void merge_buckets(hipStream_t st, uint32_t nb, uint32_t* acc29, uint32_t* cnt, const uint32_t* acc29b,

@@ -53,7 +53,8 @@ void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const 
 template <class Cv>
 void Launch<Cv>::accumulate(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* sval,
                             const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts,
-                            uint32_t* acc29, uint32_t nb, size_t acc_threads, uint32_t* next_chunk) {
+                            uint32_t* acc29, uint32_t nb, size_t acc_threads, uint32_t* next_chunk,
+                            uint32_t* crowd) {
   // nchunks threads (rounded up to whole 256-thread blocks); both kernels derive the chunk
   // length from the same grid -- except the radix-29 work-queue form: acc_threads (< nchunks,
   // whole blocks) threads take the nchunks chunks from the counter next_chunk, zeroed here
@@ -65,8 +66,10 @@ void Launch<Cv>::accumulate(hipStream_t st, size_t nchunks, const uint32_t* tota
   } else {
     k_accumulate<Cv><<<blocks, 256, 0, st>>>(total, sval, skey, off, cnt, pts, acc29, nb, 0u, nullptr);
   }
-  k_fixup_groups<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, acc29, nb);
-  k_fixup<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, acc29, nb);
+  (void)hipMemsetAsync(crowd, 0, 4, st);
+  k_fixup<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, acc29, nb, crowd);
+  // crowded buckets: at most one per FIX_LP_FROM + 1 chunks; 1024 waves stride over the list
+  k_fixup_crowded<Cv><<<256, 256, 0, st>>>(crowd, acc29, nb, blocks * 256u);
 }
 
 template <class Cv>
@@ -113,7 +116,7 @@ template void Launch<KZ_CURVE_T>::sort(hipStream_t, const TermList&, uint32_t, c
                                        uint64_t*, size_t, bool, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
 template void Launch<KZ_CURVE_T>::accumulate(hipStream_t, size_t, const uint32_t*, const uint32_t*, const uint32_t*,
                                              const uint32_t*, const uint32_t*, const Affine<KZ_CURVE_T>*, uint32_t*,
-                                             uint32_t, size_t, uint32_t*);
+                                             uint32_t, size_t, uint32_t*, uint32_t*);
 template void Launch<KZ_CURVE_T>::pts_to29(hipStream_t, Affine<KZ_CURVE_T>*, uint32_t);
 template void Launch<KZ_CURVE_T>::reduce(hipStream_t, uint32_t, const uint32_t*, const uint32_t*, Xyzz<KZ_CURVE_T>*,
                                          Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, int);

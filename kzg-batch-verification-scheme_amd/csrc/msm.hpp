@@ -1117,17 +1117,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
 }
 
 // A bucket cut into k + 1 pieces (its last piece in chunk c0, first pieces of chunks c0+1..c1,
-// k = c1 - c0) is joined by one thread with k dependent additions of ~20 us each.  Narrow top
-// windows crowd thousands of entries into a bucket (13-bit windows of a 255-bit scalar keep 8
-// bits in the top one: 2^17 terms in ~116 buckets, k ~ 18), so for k > 3 the join is two-level:
-// k_fixup_groups sums groups of G = ceil(sqrt k) consecutive first pieces into the group's first
-// slot, k_fixup adds the ceil(k / G) group sums -- G - 1 + ceil(k / G) dependent additions.
-KZ_DEV uint32_t fix_group(uint32_t k) {
-  if (k <= 3) return 1;
-  uint32_t g = (uint32_t)sqrtf((float)k);
-  while (g * g < k) ++g;
-  return g;
-}
+// k = c1 - c0) is joined with k dependent additions.  Thread-serial, one costs ~25 us at the
+// occupancy of these kernels; narrow top windows crowd hundreds of entries into a bucket (13-bit
+// windows of a 255-bit scalar keep 8 bits in the top one: 2^17 terms in 257 buckets, k ~ 8), so
+// buckets of k >= FIX_LP_FROM pieces are listed by k_fixup and joined by k_fixup_crowded, one wave
+// per bucket in lane-parallel arithmetic (lpfield.hpp: ~1.5 us per addition).  (Before: a
+// two-level thread-serial join, G - 1 + ceil(k / G) additions with G = ceil(sqrt k).)
+constexpr uint32_t FIX_LP_FROM = 4;
 
 // (bucket, continuation range) of chunk c when its first entry continues a bucket begun in an
 // earlier chunk: false otherwise.  c0 = the bucket's first chunk, c1 = its last.
@@ -1144,52 +1140,102 @@ KZ_DEV bool fix_range(uint32_t c, uint32_t len, uint32_t total, const uint32_t* 
   return true;
 }
 
-// first level of the two-level join: chunk c heads a group when (c - c0 - 1) % G == 0
-template <class Cv>
-__global__ void __launch_bounds__(256) k_fixup_groups(const uint32_t* __restrict__ total_p,
-                                                      const uint32_t* __restrict__ sorted_key,
-                                                      const uint32_t* __restrict__ off,
-                                                      const uint32_t* __restrict__ cnt,
-                                                      uint32_t* __restrict__ acc29, uint32_t nb) {
-  KZ_TAIL_PRIO();
-  const uint32_t total = *total_p;
-  const uint32_t len = acc_chunk_len(total, gridDim.x * blockDim.x);
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x + 1;
-  uint32_t key, c0, c1;
-  if (!fix_range(c, len, total, sorted_key, off, cnt, key, c0, c1)) return;
-  const uint32_t g = fix_group(c1 - c0);
-  if (g == 1 || (c - c0 - 1) % g) return;
-  const uint32_t last = c + g - 1 < c1 ? c + g - 1 : c1;
-  using Q = Fp29Of<Cv>;
-  X29<Q> acc = load_x29<Q>(acc29, nb + c);
-  for (uint32_t cc = c + 1; cc <= last; ++cc) acc = x29_add<Cv, Q>(acc, load_x29<Q>(acc29, nb + cc));
-  store_x29<Q>(acc29, nb + c, acc);
-}
-
 // joins the pieces of buckets that cross chunk boundaries (launched with the same grid as
-// k_accumulate, so acc_chunk_len agrees), after k_fixup_groups
-// The pieces and the bucket are radix-29 records of acc29 = [nb buckets |
-// nthreads first pieces | nthreads last pieces], joined with the radix-29 XYZZ addition and
-// written back as the record k_reduce_segments reads.
+// k_accumulate, so acc_chunk_len agrees).  The pieces and the bucket are radix-29 records of
+// acc29 = [nb buckets | nthreads first pieces | nthreads last pieces], joined with the radix-29
+// XYZZ addition and written back as the record k_reduce_segments reads.  Buckets of
+// FIX_LP_FROM pieces or more go to the crowded list (crowd[0] = count, then (key, c0, c1)).
 template <class Cv>
 __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ total_p,
                                                const uint32_t* __restrict__ sorted_key,
                                                const uint32_t* __restrict__ off,
                                                const uint32_t* __restrict__ cnt, uint32_t* __restrict__ acc29,
-                                               uint32_t nb) {
+                                               uint32_t nb, uint32_t* __restrict__ crowd) {
   KZ_TAIL_PRIO();
   const uint32_t total = *total_p;
   const uint32_t len = acc_chunk_len(total, gridDim.x * blockDim.x);
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x + 1;
   uint32_t key, c0, c1;
   if (!fix_range(c, len, total, sorted_key, off, cnt, key, c0, c1)) return;
-  if (c0 != c - 1) return;                // a later continuation chunk: handled by c0+1
-  const uint32_t g = fix_group(c1 - c0);  // group sums at c, c + g, ...
+  if (c0 != c - 1) return;  // a later continuation chunk: handled by c0+1
+  if (c1 - c0 >= FIX_LP_FROM) {
+    const uint32_t i = atomicAdd(&crowd[0], 1u);
+    crowd[1 + 3 * i] = key;
+    crowd[2 + 3 * i] = c0;
+    crowd[3 + 3 * i] = c1;
+    return;
+  }
   const size_t nthreads = (size_t)gridDim.x * blockDim.x;
   using Q = Fp29Of<Cv>;
   X29<Q> acc = load_x29<Q>(acc29, nb + nthreads + c0);
-  for (uint32_t cc = c; cc <= c1; cc += g) acc = x29_add<Cv, Q>(acc, load_x29<Q>(acc29, nb + cc));
+  for (uint32_t cc = c; cc <= c1; ++cc) acc = x29_add<Cv, Q>(acc, load_x29<Q>(acc29, nb + cc));
   store_x29<Q>(acc29, key, acc);
+}
+
+// a radix-29 record (load_x29 layout) <-> lane-parallel form.  BLS12-381: the record limbs are
+// the lane limbs (R29 = R); BN254: x R29 <-> x R by one row-parallel product each way
+template <class Cv>
+KZ_DEV LpXyzz<Cv> lp_load_x29(const LpCtx<Cv>& c, const uint32_t* rec) {
+  using Q = Fp29Of<Cv>;
+  using LQ = LpQ<Cv>;
+  const int j = threadIdx.x & 15;
+  LpXyzz<Cv> p;
+  p.x = j < Q::N ? (int32_t)rec[j] : 0;
+  p.y = j < Q::N ? (int32_t)rec[Q::N + j] : 0;
+  p.zz = j < Q::N ? (int32_t)rec[2 * Q::N + j] : 0;
+  p.zzz = j < Q::N ? (int32_t)rec[3 * Q::N + j] : 0;
+  p.inf = __builtin_amdgcn_ballot_w64(p.zz != 0) == 0;  // zz = 0 marks infinity (store_x29)
+  if constexpr (LQ::N != Q::N) {
+    int32_t from29 = 0;
+#pragma unroll
+    for (int q = 0; q < LQ::N; ++q)
+      if (j == q) from29 = (int32_t)LQ::FROM29[q];
+    lp_step4(c, p.x, p.x, from29, p.y, p.y, from29, p.zz, p.zz, from29, p.zzz, p.zzz, from29);
+  }
+  return p;
+}
+template <class Cv>
+KZ_DEV void lp_store_x29(const LpCtx<Cv>& c, uint32_t* rec, const LpXyzz<Cv>& p) {
+  using Q = Fp29Of<Cv>;
+  using LQ = LpQ<Cv>;
+  int32_t v[4] = {p.x, p.y, p.zz, p.zzz};
+  if constexpr (LQ::N != Q::N) {
+    const int j = threadIdx.x & 15;
+    int32_t to29 = 0;
+#pragma unroll
+    for (int q = 0; q < LQ::N; ++q)
+      if (j == q) to29 = (int32_t)LQ::TO29[q];
+    lp_step4(c, v[0], v[0], to29, v[1], v[1], to29, v[2], v[2], to29, v[3], v[3], to29);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int64_t l[LQ::N];
+    lp_canon<Cv>(v[k], l);  // canonical limbs, uniform over the wave
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+      for (int i = 0; i < Q::N; ++i) rec[k * Q::N + i] = (k == 2 && p.inf) ? 0u : (uint32_t)l[i];
+    }
+  }
+}
+
+// the crowded buckets listed by k_fixup: one wave per bucket, its pieces added in lane-parallel
+// arithmetic; any grid (waves stride over the list)
+template <class Cv>
+__global__ void __launch_bounds__(256) k_fixup_crowded(const uint32_t* __restrict__ crowd, uint32_t* __restrict__ acc29,
+                                                       uint32_t nb, uint32_t nthreads) {
+  KZ_TAIL_PRIO();
+  constexpr int W29 = kW29<Fp29Of<Cv>>;
+  const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)crowd[0]);
+  const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+  const LpCtx<Cv> c = lp_ctx<Cv>();
+  for (uint32_t i = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; i < n; i += nwaves) {
+    const uint32_t key = (uint32_t)__builtin_amdgcn_readfirstlane((int)crowd[1 + 3 * i]);
+    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)crowd[2 + 3 * i]);
+    const uint32_t c1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)crowd[3 + 3 * i]);
+    LpXyzz<Cv> acc = lp_load_x29(c, acc29 + ((size_t)nb + nthreads + c0) * W29);
+    for (uint32_t cc = c0 + 1; cc <= c1; ++cc) acc = lp_xyzz_add(c, acc, lp_load_x29(c, acc29 + ((size_t)nb + cc) * W29));
+    lp_store_x29(c, acc29 + (size_t)key * W29, acc);
+  }
 }
 
 // Bucket stores of two accumulations over the same sets (the point ranges of a chunked
