@@ -121,6 +121,16 @@ struct Slot {
   int partial_of = 0;        // ... of a batch (1) or an MSM (2): a combine of that kind may chain behind it
   bool msm_job = false;      // pending job is an MSM whose encoded result lands in host_out
   int curve = 0;
+  // every device buffer of the slot (kzgmi_ctx_destroy releases them all: a buffer added above
+  // must be listed here)
+  template <class F>
+  void for_each_buf(F&& f) {
+    DevBuf* bufs[] = {&pts, &inf, &scal_r, &scal_s, &scal_t, &tpart, &cnt, &off, &coarse, &ent, &total, &sval, &skey,
+                      &R, &U, &scratch, &winsum, &res, &flags, &stage, &outb, &acc29, &accq, &crowd, &fs_leaves,
+                      &fs_tmp, &fs_top, &pow, &chal, &glv_r, &glv_s, &glv_t, &digits, &small_nodes, &small_flags,
+                      &acc29b, &cntb, &offb};
+    for (DevBuf* b : bufs) f(*b);
+  }
 };
 
 }  // namespace
@@ -1170,11 +1180,7 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
   (void)hipSetDevice(c->device);
   for (auto& s : c->slots) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
-    DevBuf* bufs[] = {&s.pts, &s.inf, &s.scal_r, &s.scal_s, &s.scal_t, &s.tpart, &s.cnt, &s.off, &s.coarse, &s.ent,
-                      &s.total, &s.sval, &s.skey, &s.acc29, &s.accq, &s.crowd, &s.R, &s.U, &s.scratch,
-                      &s.winsum, &s.res, &s.flags, &s.stage, &s.outb, &s.fs_leaves, &s.fs_tmp,
-                      &s.fs_top, &s.pow, &s.chal, &s.glv_r, &s.glv_s, &s.glv_t, &s.digits};
-    for (DevBuf* b : bufs) b->release();
+    s.for_each_buf([](DevBuf& b) { b.release(); });
     for (auto& e : s.ev)
       if (e) (void)hipEventDestroy(e);
     if (s.signal_ev) (void)hipEventDestroy(s.signal_ev);
@@ -1210,6 +1216,8 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
     srs->ctx = nullptr;
   }
   c->gath.release();
+  c->mdig.release();
+  c->mdig_all.release();
   std::vector<kzgmi_ctx*> peers;
   peers.swap(c->peers);
   delete c;
@@ -1444,8 +1452,11 @@ int host_chunks(const kzgmi_ctx* c, size_t n, uint32_t flags, int curve) {
   const bool one_store = one_store_flags(flags) && c->host_chunk_mode != 1;
   int k = n >= (size_t(1) << 17) ? (one_store ? 4 : 2) : 1;
   if (c->host_chunks_env) k = c->host_chunks_env;
-  k = std::min<int>(k, (int)c->slots.size());
   k = std::min<int>(k, (int)((n + FS_CHUNK - 1) / FS_CHUNK));
+  // the one-store form runs every range on slot 0 (slot0_idle checked it); the shard-partial
+  // form takes slots 0..k-1, which must exist and be idle
+  if (one_store) return std::max(k, 1);
+  k = std::min<int>(k, (int)c->slots.size());
   for (int j = 0; j < k; ++j)
     if (c->slots[j].pending) return 1;
   return std::max(k, 1);
@@ -1469,8 +1480,13 @@ int batch_host_chunked(kzgmi_ctx* c, const kzgmi_srs* srs, const uint8_t* commit
       return enqueue_batch_chunked<decltype(cv)>(c, s, srs, commitments, zs, ys, proofs, n, seed, flags, k);
     });
     if (r) {
+      // whatever was enqueued drains before the error returns: the slot's kernels of this call
+      // (end_job never ran, so done_ev still marks the previous job) and the copies that may
+      // still read the caller's buffers
       const std::string msg = g_err;
-      if (s.done_rec) (void)sync_slot(s);  // whatever was enqueued drains before the error returns
+      (void)hipStreamSynchronize(s.stream);
+      (void)hipStreamSynchronize(c->h2d_stream);
+      s.ndep = 0;
       s.pending = false;
       return fail(r, msg);
     }

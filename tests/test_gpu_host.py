@@ -206,7 +206,10 @@ def test_sync_host_chunked_matches_unsplit(ctx, curve, trusted):
     form) and shard partials per range (KZGMI_HOST_CHUNK_MODE=1, the form for the other flags)
     both give the verdict and A, B of a
     context that never splits (KZGMI_HOST_CHUNKS=1) and of the oracle; a corrupted y in the last
-    range rejects; a non-canonical z in an inner range reports the unsplit call's error."""
+    range and in a middle range (second store + merge, then more accumulation) rejects; a
+    non-canonical z in an inner range reports the unsplit call's error.  With n = 2^19 + 5000 the
+    ranges are [0, 65536), then three of ~154 K (api.hip enqueue_batch_chunked): index 66536 is
+    in range 1, n / 2 in range 2."""
     import kzgmi
     import torch
     C = pc.CURVES[curve]
@@ -230,8 +233,11 @@ def test_sync_host_chunked_matches_unsplit(ctx, curve, trusted):
         assert ok is True and want == (Ao, Bo)
         bad_y = [a.copy() for a in host]
         bad_y[2][32 * (n - 1) + 31] ^= 1  # y of the last tuple
+        bad_ymid = [a.copy() for a in host]
+        bad_ymid[2][32 * (n // 2) + 31] ^= 1  # y of a tuple in range 2
+        iz = (1 << 16) + 1000  # range 1
         bad_z = [a.copy() for a in host]
-        bad_z[1][32 * 1000:32 * 1001] = np.frombuffer(C.r.to_bytes(32, "big"), dtype=np.uint8)  # z = r
+        bad_z[1][32 * iz:32 * (iz + 1)] = np.frombuffer(C.r.to_bytes(32, "big"), dtype=np.uint8)  # z = r
         with pytest.raises(kzgmi.KzgmiError) as e1:
             c1.batch_verify(s1, *bad_z, seed=seed, **kw)
         for c in (ctx, c2):
@@ -239,6 +245,7 @@ def test_sync_host_chunked_matches_unsplit(ctx, curve, trusted):
             assert c.batch_verify(srs, *host, seed=seed, **kw) is True
             assert c.last_combination(curve) == want
             assert c.batch_verify(srs, *bad_y, seed=seed, **kw) is False
+            assert c.batch_verify(srs, *bad_ymid, seed=seed, **kw) is False
             with pytest.raises(kzgmi.KzgmiError) as e:
                 c.batch_verify(srs, *bad_z, seed=seed, **kw)
             assert e.value.code == e1.value.code == -4
@@ -248,3 +255,47 @@ def test_sync_host_chunked_matches_unsplit(ctx, curve, trusted):
     finally:
         c1.close()
         c2.close()
+
+
+def test_ctx_destroy_releases_chunked_workspaces():
+    """kzgmi_ctx_destroy releases every slot buffer (the second bucket store of
+    chunked host batches -- acc29b, cntb, offb -- and the small-call tree were left allocated,
+    ~60 MB per context at 2^17 tuples).  A one-slot context also takes the one-store chunked form
+    (its ranges all run on slot 0).  Device free memory must come back after each
+    create / chunked verify / small verify / destroy cycle."""
+    import kzgmi
+    import torch
+    curve = "bls12_381"
+    C = pc.CURVES[curve]
+    n, tau = 1 << 17, 0xC0FFEE + 21
+    g1b = 2 * C.fp_bytes
+    g2 = pk.g2_to_bytes(C.g2, C)
+    tg2 = O.g2_mul(curve, g2, tau)
+    seed = hashlib.sha256(b"destroy-cycle").digest()
+    d = [torch.empty(n * w, dtype=torch.uint8, device="cuda") for w in (g1b, 32, 32, g1b)]
+    c0 = kzgmi.Context(0, 1)
+    try:
+        c0.gen_tuples(curve, tau, hashlib.sha256(b"destroy-cycle-tuples").digest(), n, *d)
+    finally:
+        c0.close()
+    host = [t.cpu().numpy() for t in d]
+    small = [a[: 64 * (len(a) // n)] for a in host]
+    del d
+    torch.cuda.synchronize()
+
+    def cycle():
+        c = kzgmi.Context(0, 1)
+        try:
+            srs = c.load_srs(curve, g2, tg2)
+            assert c.batch_verify(srs, *host, seed=seed) is True
+            assert c.batch_verify(srs, *small, seed=seed) is True
+            del srs
+        finally:
+            c.close()
+
+    cycle()  # runtime pools, code objects
+    free0 = torch.cuda.mem_get_info()[0]
+    for _ in range(3):
+        cycle()
+    free1 = torch.cuda.mem_get_info()[0]
+    assert free0 - free1 < (32 << 20), (free0 - free1) / 2**20
