@@ -815,8 +815,16 @@ def main():
             lat_b = 1e3 * (time.perf_counter() - a)
             phb = ctx.phase_ms()
             ctx.set_profiling(False)
+            # BN254's compute floor as roofline.compute.hw_floor's: 32 nn mixed
+            # additions x 10 products, 162 mads per 9-limb radix-2^29 product (9 x 9 a b + 9 x 9 m p)
+            n_simd_b = 4 * torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+            floor_b = 0.4596e9 * n_simd_b * 64 / 162
+            acc_b = phb.get("accumulate") or 0.0
             bn[key] = {"n": nn_, "steps": st_, "batch_verifies_per_s": rate_b, "tuples_per_s": rate_b * nn_,
-                       "single_batch_latency_ms": lat_b, "phase_ms_single_batch": phb}
+                       "single_batch_latency_ms": lat_b, "phase_ms_single_batch": phb,
+                       "accumulate_ms": acc_b, "hw_floor_fpmul_per_s": floor_b,
+                       "hw_floor_frac": (32 * nn_ * 10 / (acc_b * 1e-3)) / floor_b if acc_b > 0 else None,
+                       "pipeline_hw_floor_frac": 32 * nn_ * 10 * rate_b / floor_b}
         bn["method"] = ("BN254 toy-tau tuples generated on the GPU, kzgmi_batch_verify_device_async over %d slots "
                         "(GLV split: BN254's G1 has cofactor 1)" % slots)
         bn["projected_8gpu_whole_batch_per_s"] = bn["n2e19_per_gpu_shard"]["batch_verifies_per_s"]
@@ -1216,6 +1224,8 @@ def main():
         "shard_2e17_projected_8gpu_strong_speedup": g(shard17, "projected_8gpu_strong_speedup"),
         "cfg4_bn254_2e19_per_s": g(bn, "n2e19_per_gpu_shard", "batch_verifies_per_s"),
         "cfg4_bn254_2e22_per_s": g(bn, "n2e22_whole", "batch_verifies_per_s"),
+        "cfg4_bn254_hw_floor_frac": g(bn, "n2e22_whole", "hw_floor_frac"),
+        "cfg4_bn254_2e19_hw_floor_frac": g(bn, "n2e19_per_gpu_shard", "hw_floor_frac"),
         "gpu_vs_cpu": r4(value / cpu["value"]) if comp_cpu else None,
         "gpu_vs_cpu_full_host_extrapolated": r4(value / cpu["full_host_extrapolated"]["value"]) if comp_cpu else None,
         "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),

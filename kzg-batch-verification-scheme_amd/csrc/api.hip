@@ -108,6 +108,10 @@ struct Slot {
   DevBuf digits;                                 // signed window digit codes of every term (msm.hpp)
   DevBuf small_nodes, small_flags;               // small calls' summation tree (msm_small.hpp)
   DevBuf acc29b, cntb, offb;                     // second bucket store of chunked batches (run_msm_core part)
+  // split accumulation (run_msm_core): the second MSM's reduction and window combination run on
+  // `side` beside the first MSM's accumulation; side_ev[0] = its sets accumulated, [1] = combined
+  hipStream_t side = nullptr;
+  hipEvent_t side_ev[2] = {};
   int* host_flags = nullptr;  // pinned: [ok, err]
   uint8_t* host_out = nullptr;  // pinned: encoded MSM result of an async MSM job
   uint8_t* ring[2] = {};        // pinned staging of pageable host inputs (kRingBytes each, lazily)
@@ -157,10 +161,21 @@ struct kzgmi_ctx {
   size_t acc_queue_min = ACC_QUEUE_MIN_LEN;  // KZGMI_ACC_QUEUE_MIN: shortest queue chunk (entries)
   size_t acc_queue_from = ACC_QUEUE_FROM;    // KZGMI_ACC_QUEUE_FROM: calls with fewer entries keep the static grid
   bool sort_split = false;     // KZGMI_SORT_SPLIT: split coarse-pass entries at every size (tests)
+  bool sort_full_bins = false;  // KZGMI_SORT_FULL_BINS: the set-table-overflow fallback at every size (tests)
   int wbits_env = 0;           // KZGMI_WBITS: 13 or 16 forces the window width (tests, A/B)
   uint32_t small_terms = 4096;  // calls of at most this many terms: msm_small.hpp (KZGMI_SMALL_TERMS; 0: never)
   int host_chunks_env = 0;       // KZGMI_HOST_CHUNKS: ranges of a synchronous host-buffer batch (batch_host_chunked)
   int host_chunk_mode = 0;       // KZGMI_HOST_CHUNK_MODE=1: shard partials even where one bucket store applies
+  // Split accumulation of two-MSM calls (run_msm_core): -1 calls of at least SPLIT_FROM entries
+  // with no other slot in flight (latency-bound), 0 never, 1 always (KZGMI_SPLIT_ACC).  Single
+  // 2^20 BLS12-381 batches 8.47 -> 8.37 ms; 2^17 ones lose (3.46 -> 3.69 ms: the side work
+  // outlasts the short second launch), so smaller calls keep one launch
+  // (profiles/r06/split_accumulation.txt)
+  static constexpr size_t SPLIT_FROM = size_t(1) << 25;
+  int split_acc = -1;
+  bool split_low_prio = true;    // KZGMI_SPLIT_LOWPRIO: the side stream's kernels without the tail's raised issue priority
+  bool split_side_fix = true;    // KZGMI_SPLIT_SIDEFIX: the first launch's piece joins on the side stream
+  bool split_side_prio = true;   // KZGMI_SPLIT_SIDEPRIO: the side stream at the device's greatest priority
   // accumulation order: a slot's k_accumulate waits for the accumulation D launches before it
   // (any slot), so at most D run at once and they start in submission order.  Without it 16
   // slots in flight ran their accumulations in bursts and their tails (pairing: one CU) together,
@@ -431,6 +446,18 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
     if (nchunks <= cap) acc_threads = 0;
   }
   nchunks = (nchunks + 255) / 256 * 256;  // = the launched thread count (part arrays indexed by thread)
+  // Split accumulation (latency): the second MSM's sets (a suffix of the sets: MSM#1 of a batch)
+  // accumulate first, then the first MSM's; the second MSM's reduction and window combination run
+  // on the slot's side stream beside the first MSM's accumulation, so only the first MSM's
+  // (fewer windows: 8 of a 127-bit randomiser against 16) stay on the critical path.
+  const uint32_t split_set = mw.nmsm == 2 ? mw.set_base[1] : 0;
+  const bool can_split = part == 0 && mw.set_base[0] == 0 && split_set > 0 && split_set + mw.nwin[1] == nsets &&
+                         mw.nwin[0] == split_set && c->split_acc != 0;
+  const bool split = can_split && (c->split_acc > 0 || (alone && emax >= kzgmi_ctx::SPLIT_FROM));
+  const size_t nchunks_b = nchunks, acc_threads_b = acc_threads;  // the second launch's grid
+  // pieces: [A's first | A's last | B's first | B's last] when A's joins run on the side stream
+  const size_t pieces = can_split && c->split_side_fix ? nchunks + nchunks_b : std::max(nchunks, nchunks_b);
+  const size_t crowd_words = 1 + 3 * (pieces / FIX_LP_FROM + 2);  // at most one per FIX_LP_FROM + 1 chunks
   CHK(s.cnt.ensure((size_t)NB * 4));
   CHK(s.off.ensure((size_t)NB * 4));
   const bool second = part >= 2;  // this range accumulates into the second store, then merges
@@ -444,13 +471,13 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   CHK(s.coarse.ensure((size_t)3 * nsets * bins * 4));
   CHK(s.ent.ensure(emax * 8));
   CHK(s.total.ensure(16));
-  if (acc_threads) CHK(s.accq.ensure(16));
-  CHK(s.crowd.ensure(4 * (1 + 3 * (nchunks / FIX_LP_FROM + 2))));  // at most one per FIX_LP_FROM + 1 chunks
+  if (acc_threads || acc_threads_b) CHK(s.accq.ensure(16));
+  CHK(s.crowd.ensure(4 * crowd_words * (can_split ? 2 : 1)));  // a split's second list after the first
   CHK(s.sval.ensure(emax * 4 + 16));  // + 16: k_accumulate reads values 4 at a time, up to 3 past the end
   CHK(s.skey.ensure(emax * 4));
   constexpr int W29 = kW29<Fp29Of<Cv>>;
   // buckets and bucket pieces are radix-29 records in acc29 (msm.hpp)
-  CHK(s.acc29.ensure(((size_t)NB + 2 * nchunks) * W29 * 4));
+  CHK(s.acc29.ensure(((size_t)NB + 2 * pieces) * W29 * 4));
   if (second) CHK(s.acc29b.ensure(((size_t)NB + 2 * nchunks) * W29 * 4));
   const size_t seg_rec = (size_t)W29 * 4;  // a radix-29 record
   CHK(s.R.ensure((size_t)NB / SEG * seg_rec));
@@ -458,6 +485,13 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   CHK(s.scratch.ensure((size_t)nsets * rb_parts * sizeof(XY)));  // k_reduce_bits partial sums
   CHK(s.winsum.ensure((size_t)nsets * sizeof(XY)));
   CHK(s.res.ensure(2 * sizeof(XY)));
+  if (can_split && !s.side) {  // the side stream at the slot stream's priority, or the device's greatest
+    int prio = 0, least = 0, greatest = 0;
+    HIPCHK(hipStreamGetPriority(s.stream, &prio));
+    if (c->split_side_prio && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess) prio = greatest;
+    HIPCHK(hipStreamCreateWithPriority(&s.side, hipStreamNonBlocking, prio));
+    for (auto& e : s.side_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   if (dry) return 0;  // kzgmi_ctx_reserve: workspace sized, nothing enqueued
   Roctx rx("kzgmi.msm.sort+accumulate+reduce+combine");
   hipStream_t st = s.stream;
@@ -468,7 +502,8 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
       if (tl.c[k].count) npts = std::max(npts, tl.c[k].pt_base + tl.c[k].count);
     L::pts_to29(st, s.pts.template as<Affine<Cv>>(), npts);
   }
-  L::sort(st, tl, nsets, inf, s.digits.template as<uint32_t>(), s.coarse.template as<uint32_t>(), s.ent.template as<uint64_t>(), emax, c->sort_split,
+  L::sort(st, tl, nsets, inf, s.digits.template as<uint32_t>(), s.coarse.template as<uint32_t>(), s.ent.template as<uint64_t>(), emax,
+          (c->sort_split ? L::SORT_SPLIT : 0) | (c->sort_full_bins ? L::SORT_FULL_BINS : 0),
           OFF.template as<uint32_t>(), CNT.template as<uint32_t>(), s.total.template as<uint32_t>(),
           s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(), wbits);
   mark(c, s, PH_SORT + 1);
@@ -482,9 +517,56 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
     order_ev = &c->acc_ring[i % M];  // (launch i - M's event: no later launch waits for it)
     if (!*order_ev) HIPCHK(hipEventCreateWithFlags(order_ev, hipEventDisableTiming));
   }
+  if (split) {
+    // sets [split_set, nsets) are the sorted entries [coff[split_set * bins], total)
+    const uint32_t* mid = s.coarse.template as<uint32_t>() + (size_t)nsets * bins + (size_t)split_set * bins;
+    const uint32_t h = split_set, hn = nsets - split_set;
+    uint32_t* acc = s.acc29.template as<uint32_t>();
+    uint32_t* crowd_a = s.crowd.template as<uint32_t>();
+    uint32_t* crowd_b = crowd_a + crowd_words;
+    // launch A's pieces follow the buckets, launch B's follow A's: A's joins may run on the side
+    // stream while B accumulates
+    const uint32_t nb_b = c->split_side_fix ? (uint32_t)(NB + 2 * nchunks) : NB;
+    L::accumulate(st, nchunks, s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(),
+                  s.skey.template as<uint32_t>(), s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts, acc,
+                  NB, acc_threads, acc_threads ? s.accq.template as<uint32_t>() : nullptr, crowd_a, mid,
+                  c->split_side_fix ? nullptr : st);
+    HIPCHK(hipEventRecord(s.side_ev[0], st));
+    HIPCHK(hipStreamWaitEvent(s.side, s.side_ev[0], 0));
+    L::accumulate(st, nchunks_b, mid, s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
+                  s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts, acc, nb_b, acc_threads_b,
+                  acc_threads_b ? s.accq.template as<uint32_t>() : nullptr, crowd_b, nullptr, st);
+    if (order_ev) HIPCHK(hipEventRecord(*order_ev, st));
+    // side: (A's piece joins,) the second MSM's reduction and window combination -- bucket
+    // records, R / U+V records, bit sums and window sums at the offsets of its sets
+    const bool lowp = c->split_low_prio;
+    if (c->split_side_fix)
+      L::fixup(s.side, nchunks, s.total.template as<uint32_t>(), s.skey.template as<uint32_t>(),
+               s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), acc, NB, crowd_a, mid);
+    const size_t nseg = nbuckets / SEG;
+    uint32_t* R29 = s.R.template as<uint32_t>();
+    uint32_t* U29 = s.U.template as<uint32_t>();
+    L::reduce(s.side, hn, s.cnt.template as<uint32_t>() + (size_t)h * nbuckets, acc + (size_t)h * nbuckets * W29,
+              reinterpret_cast<XY*>(R29 + h * nseg * W29), reinterpret_cast<XY*>(U29 + 2 * h * nseg * W29),
+              s.scratch.template as<XY>() + (size_t)h * rb_parts, s.winsum.template as<XY>() + h, wbits, lowp);
+    L::window_combine(s.side, MsmWindows{1, {h, 0}, {mw.nwin[1], 0}}, s.winsum.template as<XY>(),
+                      s.res.template as<XY>() + 1, wbits, lowp);
+    HIPCHK(hipEventRecord(s.side_ev[1], s.side));
+    mark(c, s, PH_ACCUM + 1);
+    L::reduce(st, h, s.cnt.template as<uint32_t>(), acc, s.R.template as<XY>(), s.U.template as<XY>(),
+              s.scratch.template as<XY>(), s.winsum.template as<XY>(), wbits);
+    mark(c, s, PH_REDUCE + 1);
+    L::window_combine(st, MsmWindows{1, {0, 0}, {mw.nwin[0], 0}}, s.winsum.template as<XY>(), s.res.template as<XY>(),
+                      wbits);
+    HIPCHK(hipStreamWaitEvent(st, s.side_ev[1], 0));
+    mark(c, s, PH_COMBINE + 1);
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
   L::accumulate(st, nchunks, s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
                 OFF.template as<uint32_t>(), CNT.template as<uint32_t>(), pts, ACC.template as<uint32_t>(), NB,
-                acc_threads, acc_threads ? s.accq.template as<uint32_t>() : nullptr, s.crowd.template as<uint32_t>());
+                acc_threads, acc_threads ? s.accq.template as<uint32_t>() : nullptr, s.crowd.template as<uint32_t>(),
+                nullptr, st);
   if (order_ev) HIPCHK(hipEventRecord(*order_ev, st));
   if (second)
     L::merge_buckets(st, NB, s.acc29.template as<uint32_t>(), s.cnt.template as<uint32_t>(),
@@ -1121,10 +1203,15 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
   if (const char* e = getenv("KZGMI_ACC_QUEUE_MIN")) c->acc_queue_min = std::max<size_t>(4, strtoull(e, nullptr, 10));
   if (const char* e = getenv("KZGMI_ACC_QUEUE_FROM")) c->acc_queue_from = strtoull(e, nullptr, 10);
   if (const char* e = getenv("KZGMI_SORT_SPLIT")) c->sort_split = atoi(e) != 0;
+  if (const char* e = getenv("KZGMI_SORT_FULL_BINS")) c->sort_full_bins = atoi(e) != 0;
   if (const char* e = getenv("KZGMI_WBITS")) c->wbits_env = atoi(e);
   if (const char* e = getenv("KZGMI_SMALL_TERMS")) c->small_terms = (uint32_t)strtoul(e, nullptr, 10);
   if (const char* e = getenv("KZGMI_HOST_CHUNKS")) c->host_chunks_env = std::max(1, atoi(e));
   if (const char* e = getenv("KZGMI_HOST_CHUNK_MODE")) c->host_chunk_mode = atoi(e);
+  if (const char* e = getenv("KZGMI_SPLIT_ACC")) c->split_acc = atoi(e) < 0 ? -1 : std::min(1, atoi(e));
+  if (const char* e = getenv("KZGMI_SPLIT_LOWPRIO")) c->split_low_prio = atoi(e) != 0;
+  if (const char* e = getenv("KZGMI_SPLIT_SIDEFIX")) c->split_side_fix = atoi(e) != 0;
+  if (const char* e = getenv("KZGMI_SPLIT_SIDEPRIO")) c->split_side_prio = atoi(e) != 0;
   // HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 unless set before the runtime
   // starts) and serialises the streams of one queue, so every slot in flight needs a queue of its
   // own (16 slots on 24 queues pipeline; 24 on 24 ran 3.6x slower).  The runtime keeps that many
@@ -1190,6 +1277,12 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
       if (s.ring_ev[b]) (void)hipEventDestroy(s.ring_ev[b]);
       if (s.ring[b]) (void)hipHostFree(s.ring[b]);
     }
+    if (s.side) {
+      (void)hipStreamSynchronize(s.side);
+      (void)hipStreamDestroy(s.side);
+    }
+    for (auto& e : s.side_ev)
+      if (e) (void)hipEventDestroy(e);
     if (s.host_flags) (void)hipHostFree(s.host_flags);
     if (s.host_out) (void)hipHostFree(s.host_out);
     if (s.stream) (void)hipStreamDestroy(s.stream);

@@ -14,22 +14,35 @@ struct Launch {
   // ---- MSM (launch_msm.hip)
   // digits: sum_k count_k * nwin_k u32 (tl.c[k].dig_base set), coarse: 3 * nsets * 256 u32
   // (counts, offsets, cursors), ent: emax x 8 B (coarse-pass entries: msm.hpp EntPacked / EntSplit)
+  // sort_flags: SORT_SPLIT (split coarse-pass entries at every size), SORT_FULL_BINS (every set at
+  // full-width coarse bins, the fallback of a set table overflow) -- test knobs
+  static constexpr int SORT_SPLIT = 1, SORT_FULL_BINS = 2;
   static void sort(hipStream_t st, const TermList& tl, uint32_t nsets, const uint8_t* inf, uint32_t* digits,
-                   uint32_t* coarse, uint64_t* ent, size_t emax, bool force_split, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
+                   uint32_t* coarse, uint64_t* ent, size_t emax, int sort_flags, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
                    uint32_t* skey, int wbits = WBITS);
   // both curves accumulate in radix 2^29: pts in that format (convert_points(to29) or
   // pts_to29), acc29 = (nb + 2 x launched threads) records of W29 words that stay the bucket
-  // store (k_fixup joins pieces into them; reduce reads them)
+  // store (k_fixup joins pieces into them; reduce reads them).  The sorted entries [*lo, *total)
+  // (lo nullptr: from 0), whole buckets
   static void accumulate(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* sval,
                          const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts,
-                         uint32_t* acc29, uint32_t nb, size_t acc_threads, uint32_t* next_chunk, uint32_t* crowd);
+                         uint32_t* acc29, uint32_t nb, size_t acc_threads, uint32_t* next_chunk, uint32_t* crowd,
+                         const uint32_t* lo, hipStream_t fix_st);
+  // the piece joins of an accumulation launch (k_fixup, k_fixup_crowded: same nchunks, nb, lo);
+  // accumulate issues them itself on fix_st (nullptr: the caller does, e.g. on another stream).
+  // nb: the record index of the launch's first piece (its pieces follow the nb bucket records)
+  static void fixup(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* skey, const uint32_t* off,
+                    const uint32_t* cnt, uint32_t* acc29, uint32_t nb, uint32_t* crowd, const uint32_t* lo);
   static void pts_to29(hipStream_t st, AF* pts, uint32_t n);  // in place
   // acc29[b] += acc29b[b] for the buckets with cntb[b] != 0, cnt[b] += cntb[b] (chunked batches)
   static void merge_buckets(hipStream_t st, uint32_t nb, uint32_t* acc29, uint32_t* cnt, const uint32_t* acc29b,
                             const uint32_t* cntb);
+  // low_prio: the kernels run at normal issue priority instead of the tail's raised one (the
+  // side stream of a split accumulation)
   static void reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const uint32_t* acc29, XY* R, XY* U,
-                     XY* scratch, XY* winsum, int wbits = WBITS);
-  static void window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res, int wbits = WBITS);
+                     XY* scratch, XY* winsum, int wbits = WBITS, bool low_prio = false);
+  static void window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res, int wbits = WBITS,
+                             bool low_prio = false);
   // small calls (msm_small.hpp): one wave per term + a counter tree; res (nmsm records)
   // and flags are cleared here; nodes: small_node_words() words, flags: small_flag_words() words
   static void small_msm(hipStream_t st, const TermList& tl, const SmallPlan& sp, uint32_t terms, const AF* pts,

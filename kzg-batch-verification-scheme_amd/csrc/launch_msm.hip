@@ -12,14 +12,16 @@ void with_wbits(int wbits, F&& f) {
 
 template <class Cv>
 void Launch<Cv>::sort(hipStream_t st, const TermList& tl, uint32_t nsets, const uint8_t* inf, uint32_t* digits,
-                      uint32_t* coarse, uint64_t* ent, size_t emax, bool force_split, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
+                      uint32_t* coarse, uint64_t* ent, size_t emax, int sort_flags, uint32_t* off, uint32_t* cnt, uint32_t* total, uint32_t* sval,
                       uint32_t* skey, int wbits) {
+  const bool force_split = (sort_flags & SORT_SPLIT) != 0;
   with_wbits(wbits, [&](auto wb) {
     constexpr int WB = decltype(wb)::value;
     const uint32_t nbins = nsets * Win<WB>::BINS;
     SetShift ss;
-    // more sets than the table holds: every set at the full 128-bucket bins (always correct)
-    const bool table = set_shifts_host<WB>(tl, nsets, ss);
+    // more sets than the table holds: every set at the full 128-bucket bins (always correct;
+    // SORT_FULL_BINS forces it, tests)
+    const bool table = !(sort_flags & SORT_FULL_BINS) && set_shifts_host<WB>(tl, nsets, ss);
     uint32_t* ccnt = coarse;
     uint32_t* coff = coarse + nbins;
     uint32_t* ccur = coarse + 2 * nbins;
@@ -54,7 +56,7 @@ template <class Cv>
 void Launch<Cv>::accumulate(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* sval,
                             const uint32_t* skey, const uint32_t* off, const uint32_t* cnt, const AF* pts,
                             uint32_t* acc29, uint32_t nb, size_t acc_threads, uint32_t* next_chunk,
-                            uint32_t* crowd) {
+                            uint32_t* crowd, const uint32_t* lo, hipStream_t fix_st) {
   // nchunks threads (rounded up to whole 256-thread blocks); both kernels derive the chunk
   // length from the same grid -- except the radix-29 work-queue form: acc_threads (< nchunks,
   // whole blocks) threads take the nchunks chunks from the counter next_chunk, zeroed here
@@ -62,12 +64,19 @@ void Launch<Cv>::accumulate(hipStream_t st, size_t nchunks, const uint32_t* tota
   if (next_chunk && acc_threads && acc_threads < nchunks) {
     (void)hipMemsetAsync(next_chunk, 0, 4, st);
     k_accumulate<Cv><<<grid_for(acc_threads, 256), 256, 0, st>>>(total, sval, skey, off, cnt, pts, acc29, nb,
-                                                                  (uint32_t)(blocks * 256u), next_chunk);
+                                                                  (uint32_t)(blocks * 256u), next_chunk, lo);
   } else {
-    k_accumulate<Cv><<<blocks, 256, 0, st>>>(total, sval, skey, off, cnt, pts, acc29, nb, 0u, nullptr);
+    k_accumulate<Cv><<<blocks, 256, 0, st>>>(total, sval, skey, off, cnt, pts, acc29, nb, 0u, nullptr, lo);
   }
+  if (fix_st) fixup(fix_st, nchunks, total, skey, off, cnt, acc29, nb, crowd, lo);
+}
+
+template <class Cv>
+void Launch<Cv>::fixup(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* skey, const uint32_t* off,
+                       const uint32_t* cnt, uint32_t* acc29, uint32_t nb, uint32_t* crowd, const uint32_t* lo) {
+  const unsigned blocks = grid_for(nchunks, 256);
   (void)hipMemsetAsync(crowd, 0, 4, st);
-  k_fixup<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, acc29, nb, crowd);
+  k_fixup<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, acc29, nb, crowd, lo);
   // crowded buckets: at most one per FIX_LP_FROM + 1 chunks; 1024 waves stride over the list
   k_fixup_crowded<Cv><<<256, 256, 0, st>>>(crowd, acc29, nb, blocks * 256u);
 }
@@ -79,14 +88,19 @@ void Launch<Cv>::pts_to29(hipStream_t st, AF* pts, uint32_t n) {
 
 template <class Cv>
 void Launch<Cv>::reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const uint32_t* acc29, XY* R, XY* U,
-                        XY* scratch, XY* winsum, int wbits) {
+                        XY* scratch, XY* winsum, int wbits, bool low_prio) {
   with_wbits(wbits, [&](auto wb) {
     constexpr int WB = decltype(wb)::value;
     const uint32_t nseg = nsets * Win<WB>::NSEG;
-    k_reduce_segments<Cv><<<grid_for(2 * (size_t)nseg, 256), 256, 0, st>>>(nseg, cnt, acc29, R, U);  // 2 threads per segment
-    // scratch: nsets * RB_PARTS partial sums
-    k_reduce_bits<Cv, WB><<<nsets * Win<WB>::RB_PARTS, 256, 0, st>>>(R, U, scratch);
-    k_reduce_bits_finish<Cv, WB><<<nsets, 64, 0, st>>>(scratch, winsum);
+    auto go = [&](auto lp) {
+      constexpr bool LP = decltype(lp)::value;
+      k_reduce_segments<Cv, LP><<<grid_for(2 * (size_t)nseg, 256), 256, 0, st>>>(nseg, cnt, acc29, R, U);  // 2 threads per segment
+      // scratch: nsets * RB_PARTS partial sums
+      k_reduce_bits<Cv, WB, LP><<<nsets * Win<WB>::RB_PARTS, 256, 0, st>>>(R, U, scratch);
+      k_reduce_bits_finish<Cv, WB, LP><<<nsets, 64, 0, st>>>(scratch, winsum);
+    };
+    if (low_prio) go(std::true_type{});
+    else go(std::false_type{});
   });
 }
 
@@ -105,23 +119,27 @@ void Launch<Cv>::small_msm(hipStream_t st, const TermList& tl, const SmallPlan& 
 }
 
 template <class Cv>
-void Launch<Cv>::window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res, int wbits) {
+void Launch<Cv>::window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res, int wbits,
+                                bool low_prio) {
   with_wbits(wbits, [&](auto wb) {
     constexpr int WB = decltype(wb)::value;
-    k_window_combine<Cv, WB><<<mw.nmsm, 64, 0, st>>>(mw, winsum, res);
+    if (low_prio) k_window_combine<Cv, WB, true><<<mw.nmsm, 64, 0, st>>>(mw, winsum, res);
+    else k_window_combine<Cv, WB><<<mw.nmsm, 64, 0, st>>>(mw, winsum, res);
   });
 }
 
 template void Launch<KZ_CURVE_T>::sort(hipStream_t, const TermList&, uint32_t, const uint8_t*, uint32_t*, uint32_t*,
-                                       uint64_t*, size_t, bool, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
+                                       uint64_t*, size_t, int, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
 template void Launch<KZ_CURVE_T>::accumulate(hipStream_t, size_t, const uint32_t*, const uint32_t*, const uint32_t*,
                                              const uint32_t*, const uint32_t*, const Affine<KZ_CURVE_T>*, uint32_t*,
-                                             uint32_t, size_t, uint32_t*, uint32_t*);
+                                             uint32_t, size_t, uint32_t*, uint32_t*, const uint32_t*, hipStream_t);
+template void Launch<KZ_CURVE_T>::fixup(hipStream_t, size_t, const uint32_t*, const uint32_t*, const uint32_t*,
+                                        const uint32_t*, uint32_t*, uint32_t, uint32_t*, const uint32_t*);
 template void Launch<KZ_CURVE_T>::pts_to29(hipStream_t, Affine<KZ_CURVE_T>*, uint32_t);
 template void Launch<KZ_CURVE_T>::reduce(hipStream_t, uint32_t, const uint32_t*, const uint32_t*, Xyzz<KZ_CURVE_T>*,
-                                         Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, int);
+                                         Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, int, bool);
 template void Launch<KZ_CURVE_T>::window_combine(hipStream_t, const MsmWindows&, const Xyzz<KZ_CURVE_T>*,
-                                                 Xyzz<KZ_CURVE_T>*, int);
+                                                 Xyzz<KZ_CURVE_T>*, int, bool);
 template void Launch<KZ_CURVE_T>::merge_buckets(hipStream_t, uint32_t, uint32_t*, uint32_t*, const uint32_t*,
                                                 const uint32_t*);
 template void Launch<KZ_CURVE_T>::small_msm(hipStream_t, const TermList&, const SmallPlan&, uint32_t,

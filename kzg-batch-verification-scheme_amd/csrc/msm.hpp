@@ -1081,8 +1081,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
                                                     const uint32_t* __restrict__ cnt,
                                                     const Affine<Cv>* __restrict__ pts,
                                                     uint32_t* __restrict__ acc29, uint32_t nb,
-                                                    uint32_t nchunks, uint32_t* __restrict__ next_chunk) {
+                                                    uint32_t nchunks, uint32_t* __restrict__ next_chunk,
+                                                    const uint32_t* __restrict__ lo_p) {
+  // the entry range [lo, total) of this launch: the whole sorted list, or the sets of one MSM
+  // (api.hip run_msm_core's split accumulation; no bucket crosses a set boundary, so the range
+  // end is where the last bucket ends)
   const uint32_t total = *total_p;
+  const uint32_t lo = lo_p ? *lo_p : 0u;
   {
     if (next_chunk) {
       // Work queue (large calls, Launch::accumulate): nchunks chunks, more than the launched
@@ -1091,7 +1096,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
       // slot's accumulation -- take fewer, so the last accumulation in flight ends on every CU
       // at about the same time instead of a whole chunk duration apart.  Every wave's loop ends
       // once the counter passes nchunks (a multiple of 64).
-      const uint32_t len = acc_chunk_len(total, nchunks);
+      const uint32_t len = acc_chunk_len(total - lo, nchunks);
       const uint32_t lane = threadIdx.x & 63u;
       for (;;) {
         uint32_t base = 0;
@@ -1099,18 +1104,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
         base = __shfl(base, 0);
         if (base >= nchunks) break;
         const uint32_t chunk = base + lane;
-        const uint32_t start = chunk * len;
-        if (start < total)
+        const uint32_t start = lo + chunk * len;
+        if (chunk * len < total - lo)
           acc_loop29<Cv>(start, min(start + len, total), total, chunk, sorted_key[start], sorted_val, sorted_key,
                          reinterpret_cast<const uint32_t*>(pts), acc29, nb, nchunks);
       }
       return;
     }
   }
-  const uint32_t len = acc_chunk_len(total, gridDim.x * blockDim.x);
+  const uint32_t len = acc_chunk_len(total - lo, gridDim.x * blockDim.x);
   const uint32_t chunk = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t start = chunk * len;
-  if (start >= total) return;
+  if (chunk * len >= total - lo) return;
+  const uint32_t start = lo + chunk * len;
   const uint32_t end = min(start + len, total);
   acc_loop29<Cv>(start, end, total, chunk, sorted_key[start], sorted_val, sorted_key,
                  reinterpret_cast<const uint32_t*>(pts), acc29, nb, gridDim.x * blockDim.x);
@@ -1127,16 +1132,16 @@ constexpr uint32_t FIX_LP_FROM = 4;
 
 // (bucket, continuation range) of chunk c when its first entry continues a bucket begun in an
 // earlier chunk: false otherwise.  c0 = the bucket's first chunk, c1 = its last.
-KZ_DEV bool fix_range(uint32_t c, uint32_t len, uint32_t total, const uint32_t* __restrict__ sorted_key,
+KZ_DEV bool fix_range(uint32_t c, uint32_t len, uint32_t lo, uint32_t total, const uint32_t* __restrict__ sorted_key,
                       const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt, uint32_t& key,
                       uint32_t& c0, uint32_t& c1) {
-  const uint32_t start = c * len;
-  if (start >= total) return false;
+  if (c * len >= total - lo) return false;
+  const uint32_t start = lo + c * len;
   key = sorted_key[start];
-  const uint32_t o = off[key];
+  const uint32_t o = off[key];  // >= lo: the launch's range holds whole buckets
   if (o >= start) return false;  // bucket starts inside this chunk
-  c0 = o / len;
-  c1 = (o + cnt[key] - 1) / len;
+  c0 = (o - lo) / len;
+  c1 = (o + cnt[key] - 1 - lo) / len;
   return true;
 }
 
@@ -1150,13 +1155,15 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ tota
                                                const uint32_t* __restrict__ sorted_key,
                                                const uint32_t* __restrict__ off,
                                                const uint32_t* __restrict__ cnt, uint32_t* __restrict__ acc29,
-                                               uint32_t nb, uint32_t* __restrict__ crowd) {
+                                               uint32_t nb, uint32_t* __restrict__ crowd,
+                                               const uint32_t* __restrict__ lo_p) {
   KZ_TAIL_PRIO();
   const uint32_t total = *total_p;
-  const uint32_t len = acc_chunk_len(total, gridDim.x * blockDim.x);
+  const uint32_t lo = lo_p ? *lo_p : 0u;  // the accumulation launch's range [lo, total)
+  const uint32_t len = acc_chunk_len(total - lo, gridDim.x * blockDim.x);
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x + 1;
   uint32_t key, c0, c1;
-  if (!fix_range(c, len, total, sorted_key, off, cnt, key, c0, c1)) return;
+  if (!fix_range(c, len, lo, total, sorted_key, off, cnt, key, c0, c1)) return;
   if (c0 != c - 1) return;  // a later continuation chunk: handled by c0+1
   if (c1 - c0 >= FIX_LP_FROM) {
     const uint32_t i = atomicAdd(&crowd[0], 1u);
@@ -1266,12 +1273,14 @@ __global__ void __launch_bounds__(256) k_merge_buckets(uint32_t nb, uint32_t* __
 // k_reduce_bits and scaled once in k_reduce_bits_finish.  (Forming R_1 + 8 U_1 here put three
 // doublings on the upper half's chain while the lower half idled: ~20 point operations per
 // wave instead of ~16; the kernel is latency-bound at 1.5 waves per SIMD.)
-template <class Cv>
+// LOWP (the reduction and combination kernels): no raised issue priority -- the side stream of a
+// split accumulation runs them beside the critical-path accumulation (api.hip run_msm_core)
+template <class Cv, bool LOWP = false>
 __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const uint32_t* __restrict__ cnt,
                                                          const uint32_t* __restrict__ acc29,
                                                          Xyzz<Cv>* __restrict__ R, Xyzz<Cv>* __restrict__ U) {
   static_assert(SEG == 16, "two 8-bucket halves per segment");
-  KZ_TAIL_PRIO();
+  if constexpr (!LOWP) KZ_TAIL_PRIO();
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t g = t >> 1, h = t & 1;
   using Q = Fp29Of<Cv>;  // radix 2^29 on the records; R, U written as records
@@ -1307,10 +1316,10 @@ __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const
 // 2 H + sum V, 3 doublings: 16 H + 8 sum V.
 constexpr int RB_PARTS = Win<WBITS>::RB_PARTS;  // c = 16 (the most parts per set)
 
-template <class Cv, int WB = WBITS>
+template <class Cv, int WB = WBITS, bool LOWP = false>
 __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict__ R, const Xyzz<Cv>* __restrict__ U,
                                                      Xyzz<Cv>* __restrict__ parts) {
-  KZ_TAIL_PRIO();
+  if constexpr (!LOWP) KZ_TAIL_PRIO();
   using Wn = Win<WB>;
   constexpr uint32_t NSEG = Wn::NSEG, SB = Wn::SEG_BITS, RBP = Wn::RB_PARTS;
   const uint32_t set = blockIdx.x / RBP, j = blockIdx.x % RBP;
@@ -1433,10 +1442,10 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
 // One wave per set, lane-parallel arithmetic (lpfield.hpp): Horner over the bit sums (c = 16:
 // 10 XYZZ doublings + 10 additions), the 4 quarter sums, 4 doublings -- ~80 row-parallel
 // product steps instead of ~330 serial products on one lane (0.71 ms before).
-template <class Cv, int WB = WBITS>
+template <class Cv, int WB = WBITS, bool LOWP = false>
 __global__ void __launch_bounds__(64) k_reduce_bits_finish(const Xyzz<Cv>* __restrict__ parts,
                                                            Xyzz<Cv>* __restrict__ winsum) {
-  KZ_TAIL_PRIO();
+  if constexpr (!LOWP) KZ_TAIL_PRIO();
   using Wn = Win<WB>;
   constexpr int SB = Wn::SEG_BITS;
   const uint32_t set = blockIdx.x;
@@ -1465,10 +1474,10 @@ struct MsmWindows {
 // Jacobian doubling) and takes the window sum with no coordinate change: 52 product steps per
 // 16-bit window against 57 with a Jacobian running sum (+ 2 steps to XYZZ and 3 back around each
 // addition).  ~52 steps per window instead of ~134 serial products (3.9 ms for 16 windows before).
-template <class Cv, int WB = WBITS>
+template <class Cv, int WB = WBITS, bool LOWP = false>
 __global__ void __launch_bounds__(64) k_window_combine(MsmWindows mw, const Xyzz<Cv>* __restrict__ winsum,
                                                        Xyzz<Cv>* __restrict__ res) {
-  KZ_TAIL_PRIO();
+  if constexpr (!LOWP) KZ_TAIL_PRIO();
   const uint32_t m = blockIdx.x;
   const LpCtx<Cv> c = lp_ctx<Cv>();
   const Xyzz<Cv>* W = winsum + mw.set_base[m];

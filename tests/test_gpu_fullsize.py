@@ -243,3 +243,98 @@ def test_batch_path_boundaries_vs_oracle(ctx, curve, n):
     assert ok is True and A == Ao and B == Bo
     y[32 * (n // 2) + 31] ^= 1
     assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n) is False
+
+
+def _context_env(slots, **env):
+    import os
+    import kzgmi
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return kzgmi.Context(0, slots)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("curve,log_n", [("bls12_381", 17), ("bls12_381", 20), ("bn254", 17), ("bn254", 20)])
+def test_split_accumulation_vs_oracle(curve, log_n):
+    """The split accumulation (api.hip run_msm_core): MSM#1's bucket sets accumulate in one
+    launch, then MSM#0's in a second one over the sorted range before them, while MSM#1's
+    reduction and window combination run on the slot's side stream.  Forced on
+    (KZGMI_SPLIT_ACC=1) and off (=0): A, B and the verdict bit-exact vs the oracle, a corrupted
+    y flips the verdict; the split with the first launch's piece joins on the slot stream and the
+    side stream at the slot's priority (KZGMI_SPLIT_SIDEFIX=0, KZGMI_SPLIT_SIDEPRIO=0); then the
+    forced split pipelined on 4 slots with corrupted batches in flight between valid ones (each
+    verdict checked)."""
+    import torch
+    C = pc.CURVES[curve]
+    n, tau = 1 << log_n, 0x5B117 + log_n
+    gen = _context_env(1)
+    try:
+        Cm, z, y, P = _gen_batch(gen, curve, n, tau, hashlib.sha256(b"split%d" % log_n).digest())
+    finally:
+        gen.close()
+    g2 = pk.g2_to_bytes(C.g2, C)
+    tg2 = O.g2_mul(curve, g2, tau)
+    vseed = hashlib.sha256(b"split-verify%d" % log_n).digest()
+    hb = [_host(t) for t in (Cm, z, y, P)]
+    ok, Ao, Bo = O.batch_verify(curve, hb[0], hb[1], hb[2], hb[3], n, g2, tg2, vseed, want_ab=True)
+    assert ok is True
+    ybad = y.clone()
+    ybad[32 * (n // 3) + 31] ^= 1
+    for env in ({"KZGMI_SPLIT_ACC": "1"}, {"KZGMI_SPLIT_ACC": "0"}, {"KZGMI_SPLIT_ACC": "1", "KZGMI_SPLIT_SIDEFIX": "0", "KZGMI_SPLIT_SIDEPRIO": "0"}):
+        c = _context_env(1, **env)
+        try:
+            srs = c.load_srs(curve, g2, tg2)
+            assert c.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n) is True, env
+            assert c.last_combination(curve) == (Ao, Bo), env
+            assert c.batch_verify(srs, Cm, z, ybad, P, seed=vseed, n=n) is False, env
+            del srs
+        finally:
+            c.close()
+    c = _context_env(4, KZGMI_SPLIT_ACC="1")
+    try:
+        srs = c.load_srs(curve, g2, tg2)
+        want = [True, False, True, True, False, True]
+        for i, w in enumerate(want):
+            if i >= 4:
+                assert c.wait(i % 4) is want[i - 4], i - 4
+            c.batch_verify_async(srs, i % 4, Cm, z, y if w else ybad, P, n, seed=vseed)
+        for i in range(len(want) - 4, len(want)):
+            assert c.wait(i % 4) is want[i], i
+        torch.cuda.synchronize()
+        del srs
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("curve,n", [("bls12_381", 1 << 17), ("bn254", 100003), ("bls12_381", 300007)])
+def test_sort_full_bins_fallback_vs_oracle(curve, n):
+    """The sort launcher's set-table fallback (launch_msm.hip: a call with more bucket sets than
+    the SetShift table holds sorts every set in full-width coarse bins instead of aborting),
+    forced at every size with KZGMI_SORT_FULL_BINS=1: at 13-bit windows (2^17 tuples, where the
+    top windows' per-set bin widths differ) and 16-bit ones, A, B and the verdict bit-exact vs
+    the oracle, a corrupted y flips it."""
+    C = pc.CURVES[curve]
+    tau = 0xF0B1 + n
+    c = _context_env(1, KZGMI_SORT_FULL_BINS="1")
+    try:
+        Cm, z, y, P = _gen_batch(c, curve, n, tau, hashlib.sha256(b"fullbins%d" % n).digest())
+        g2 = pk.g2_to_bytes(C.g2, C)
+        tg2 = O.g2_mul(curve, g2, tau)
+        srs = c.load_srs(curve, g2, tg2)
+        vseed = hashlib.sha256(b"fullbins-verify%d" % n).digest()
+        assert c.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n) is True
+        A, B = c.last_combination(curve)
+        hb = [_host(t) for t in (Cm, z, y, P)]
+        ok, Ao, Bo = O.batch_verify(curve, hb[0], hb[1], hb[2], hb[3], n, g2, tg2, vseed, want_ab=True)
+        assert ok is True and A == Ao and B == Bo
+        y[32 * (n // 2) + 31] ^= 1
+        assert c.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n) is False
+        del srs
+    finally:
+        c.close()

@@ -561,6 +561,51 @@ def test_async_accumulation_order(torch_dev):
         c8.close()
 
 
+@pytest.mark.slow
+def test_bench_shape_pipeline_vs_oracle(torch_dev):
+    """The headline's exact shape (bench.py: 16 slots x 2^20 BLS12-381 tuples, accumulation order
+    D = 2, forced here since this process may share hardware queues): 40 submissions round the
+    slots with two corrupted batches in flight among valid ones -- every verdict as submitted --
+    and one slot's job mid-pipeline a shard partial whose A, B are bit-exact vs the oracle."""
+    torch = torch_dev
+    curve = "bls12_381"
+    C = pc.CURVES[curve]
+    n, tau = 1 << 20, 0xBE9C4
+    c16 = _context_with_env(16, KZGMI_ACC_ORDER="2", KZGMI_ACC_ORDER_SMALL="4")
+    try:
+        g2 = pk.g2_to_bytes(C.g2, C)
+        tg2 = O.g2_mul(curve, g2, tau)
+        srs = c16.load_srs(curve, g2, tg2)
+        seed = hashlib.sha256(b"bench-shape").digest()
+        Cm, z, y, P = _gen_batch(c16, torch, curve, n, tau, hashlib.sha256(b"bench-shape-tuples").digest())
+        y_bad = y.clone()
+        y_bad[32 * (n // 2) + 31] ^= 1
+        part = torch.empty(2 * c16.partial_bytes(curve), dtype=torch.uint8, device="cuda")
+        pending = {}
+        for k in range(40):
+            s = k % 16
+            if s in pending:
+                exp = pending.pop(s)
+                assert c16.wait(s) is (True if exp == "partial" else exp), (k, s)
+            if k == 20:
+                c16.batch_partial_async(srs, s, Cm, z, y, P, n, 0, seed, part)
+                pending[s] = "partial"
+                continue
+            bad = k in (7, 23)
+            c16.batch_verify_async(srs, s, Cm, z, y_bad if bad else y, P, n, seed=seed)
+            pending[s] = not bad
+        for s in sorted(pending):
+            exp = pending.pop(s)
+            assert c16.wait(s) is (True if exp == "partial" else exp), s
+        hb = [t.cpu().numpy().tobytes() for t in (Cm, z, y, P)]
+        ok, Ao, Bo = O.batch_verify(curve, hb[0], hb[1], hb[2], hb[3], n, g2, tg2, seed, want_ab=True)
+        assert ok is True
+        assert c16.partial_encode(curve, part, 2) == [Ao, Bo]
+        del srs
+    finally:
+        c16.close()
+
+
 @pytest.mark.parametrize("curve", CURVES)
 def test_async_msm_slots(ctx, curve, torch_dev):
     """Pipelined MSM: two different MSMs in flight on slots 0/1, each bit-exact vs the oracle;
