@@ -468,7 +468,7 @@ def main():
 
     # ---- single-batch latency (not pipelined), rank 0 view
     lat = None
-    phases_single = None
+    phases_single = phases_single_split = None
     lat_runs = None
     if world == 1:
         ts = []
@@ -480,11 +480,20 @@ def main():
         ts.sort()
         lat = 1e3 * ts[len(ts) // 2]
         lat_runs = [1e3 * t for t in ts]
+        # phases of the split accumulation these synchronous calls take (api.hip run_msm_core: the
+        # marks follow the critical path), then of the single-launch form the pipeline runs -- the
+        # dominant kernel the roofline prices
         ctx.set_profiling(True)
         for _ in range(6):  # phase means over 6 batches (2 read up to ~3 % apart run to run)
             assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n)
+        phases_single_split = ctx.phase_ms()
+        ctx.set_split_acc(0)
+        ctx.set_profiling(True)
+        for _ in range(6):
+            assert ctx.batch_verify(srs, Cm, z, y, P, seed=vseed, n=n)
         phases_single = ctx.phase_ms()
         ctx.set_profiling(False)
+        ctx.set_split_acc(-1)
 
     # ---- configs[0] (BASELINE.json:7): a 256-tuple batch (the CPU verifier's time is added by
     # cpu_baseline below); GPU latency of the same batch, median of 10 synchronous calls
@@ -809,12 +818,16 @@ def main():
                               ("n2e22_whole", nb, max(1, args.bn254_steps // 3))):
             vb = (Cb[: nn_ * 64], zb[: nn_ * 32], yb[: nn_ * 32], Pb[: nn_ * 64])
             rate_b = pipelined_rate(ctx, slots, st_, lambda s_: ctx.batch_verify_async(srs_b, s_, *vb, nn_, seed=vseed))
-            ctx.set_profiling(True)
             a = time.perf_counter()
             assert ctx.batch_verify(srs_b, *vb, seed=vseed, n=nn_)
             lat_b = 1e3 * (time.perf_counter() - a)
+            ctx.set_split_acc(0)  # the single-launch accumulation the pipeline runs
+            ctx.set_profiling(True)
+            for _ in range(2):
+                assert ctx.batch_verify(srs_b, *vb, seed=vseed, n=nn_)
             phb = ctx.phase_ms()
             ctx.set_profiling(False)
+            ctx.set_split_acc(-1)
             # BN254's compute floor as roofline.compute.hw_floor's: 32 nn mixed
             # additions x 10 products, 162 mads per 9-limb radix-2^29 product (9 x 9 a b + 9 x 9 m p)
             n_simd_b = 4 * torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
@@ -1141,6 +1154,9 @@ def main():
         "cfg0_n256": cfg0,
         "phase_ms_avg_in_timed_region": phases,
         "phase_ms_single_batch": phases_single,
+        "phase_ms_single_batch_note": "single-launch accumulation (the pipelined form, kzgmi_set_split_acc 0); "
+                                      "single_batch_latency_ms runs the default split form (phase_ms_single_batch_split)",
+        "phase_ms_single_batch_split": phases_single_split,
         "compressed_subgroup": comp,
         "fiat_shamir": fsm,
         "prover_commit": commit,

@@ -2530,6 +2530,16 @@ int kzgmi_set_glv(kzgmi_ctx* c, int msm, int batch) {
   return set_dev(c);
 }
 
+int kzgmi_set_split_acc(kzgmi_ctx* c, int mode) {
+  CHK(check_ctx(c));
+  if (mode < -1 || mode > 1) return fail(KZGMI_ERR_ARG, "split mode must be -1, 0 or 1");
+  for (auto& s : c->slots)
+    if (s.pending) return fail(KZGMI_ERR_ARG, "kzgmi_set_split_acc with jobs in flight");
+  c->split_acc = mode;
+  for (kzgmi_ctx* p : c->peers) CHK(kzgmi_set_split_acc(p, mode));
+  return set_dev(c);
+}
+
 int kzgmi_set_trusted_g1(kzgmi_ctx* c, int on) {
   CHK(check_ctx(c));
   for (auto& s : c->slots)

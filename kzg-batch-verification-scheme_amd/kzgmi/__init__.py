@@ -105,6 +105,7 @@ def lib():
         "kzgmi_set_glv": ([vp, c.c_int, c.c_int], c.c_int),
         "kzgmi_commit_device_async": ([vp, vp, c.c_int, vp, sz], c.c_int),
         "kzgmi_set_trusted_g1": ([vp, c.c_int], c.c_int),
+        "kzgmi_set_split_acc": ([vp, c.c_int], c.c_int),
         "kzgmi_msm_partial_device_async": ([vp, c.c_int, c.c_int, vp, vp, sz, vp], c.c_int),
         "kzgmi_msm_combine_device_async": ([vp, c.c_int, c.c_int, vp, c.c_int], c.c_int),
         "kzgmi_partial_bytes": ([c.c_int], sz),
@@ -144,7 +145,7 @@ def exported_symbols():
         "kzgmi_fs_challenge_device", "kzgmi_fs_chunk_digests_device",
         "kzgmi_fs_challenge_from_digests_device",
         "kzgmi_last_combination", "kzgmi_msm_g1", "kzgmi_msm_g1_device", "kzgmi_msm_g1_device_async",
-        "kzgmi_msm_wait", "kzgmi_set_glv", "kzgmi_commit_device_async", "kzgmi_set_trusted_g1", "kzgmi_msm_partial_device_async", "kzgmi_msm_combine_device_async", "kzgmi_partial_bytes",
+        "kzgmi_msm_wait", "kzgmi_set_glv", "kzgmi_commit_device_async", "kzgmi_set_trusted_g1", "kzgmi_set_split_acc", "kzgmi_msm_partial_device_async", "kzgmi_msm_combine_device_async", "kzgmi_partial_bytes",
         "kzgmi_batch_partial_device", "kzgmi_batch_combine_device", "kzgmi_batch_partial_device_async",
         "kzgmi_batch_combine_device_async", "kzgmi_msm_partial_device",
         "kzgmi_msm_combine_device", "kzgmi_pairing", "kzgmi_gen_g1", "kzgmi_gen_tuples",
@@ -770,6 +771,10 @@ class Context:
     def set_trusted_g1(self, on: bool = True):
         """MSM inputs on this context are known G1 members (BLS12-381 MSMs may then use GLV)."""
         _check(lib().kzgmi_set_trusted_g1(self.handle, int(bool(on))))
+
+    def set_split_acc(self, mode: int = -1):
+        """Split accumulation of a batch's two MSMs: -1 auto (large synchronous calls), 0 never, 1 always."""
+        _check(lib().kzgmi_set_split_acc(self.handle, int(mode)))
 
     def set_profiling(self, on: bool):
         _check(lib().kzgmi_set_profiling(self.handle, 1 if on else 0))

@@ -15,6 +15,9 @@ ap.add_argument("--n", type=int, default=1 << 20)
 ap.add_argument("--reps", type=int, default=4)
 ap.add_argument("--lib", default=None)
 ap.add_argument("--curve", default="bls12_381")
+ap.add_argument("--split", type=int, default=0,
+                help="kzgmi_set_split_acc mode (default 0: the single-launch accumulation the pipeline runs; "
+                     "an exported KZGMI_SPLIT_ACC takes precedence)")
 args = ap.parse_args()
 if args.lib:
     os.environ["KZGMI_LIB"] = args.lib
@@ -22,6 +25,8 @@ import torch  # noqa: E402
 import kzgmi  # noqa: E402
 
 ctx = kzgmi.Context(0, 1)
+if "KZGMI_SPLIT_ACC" not in os.environ:
+    ctx.set_split_acc(args.split)
 curve, n = args.curve, args.n
 g2 = kzgmi.G2_GENERATOR[curve]
 tau = 0x1234567

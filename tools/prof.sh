@@ -16,7 +16,8 @@
 set -o pipefail
 MODE=${1:?mode}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-case $MODE in kernel|traffic) OUT=$R/gpurun_out/prof_single ;; *) OUT=$R/gpurun_out/prof_$MODE ;; esac
+# PROF_TAG: suffix of the output directory (e.g. _bn254 for a second curve's passes)
+case $MODE in kernel|traffic) OUT=$R/gpurun_out/prof_single${PROF_TAG:-} ;; *) OUT=$R/gpurun_out/prof_$MODE${PROF_TAG:-} ;; esac
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 PT="python3 $R/tools/phase_timing.py"
