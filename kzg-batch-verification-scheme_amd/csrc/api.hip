@@ -109,8 +109,8 @@ struct Slot {
   DevBuf small_nodes, small_flags;               // small calls' summation tree (msm_small.hpp)
   DevBuf acc29b, cntb, offb;                     // second bucket store of chunked batches (run_msm_core part)
   // split accumulation (run_msm_core): the second MSM's reduction and window combination run on
-  // `side` beside the first MSM's accumulation; side_ev[0] = its sets accumulated, [1] = combined
-  hipStream_t side = nullptr;
+  // the context's side stream beside the first MSM's accumulation; side_ev[0] = its sets
+  // accumulated, [1] = combined
   hipEvent_t side_ev[2] = {};
   int* host_flags = nullptr;  // pinned: [ok, err]
   uint8_t* host_out = nullptr;  // pinned: encoded MSM result of an async MSM job
@@ -197,6 +197,11 @@ struct kzgmi_ctx {
   // batch's copy then gets the whole link and completes first-in first-out (16 concurrent
   // 256-MiB copies on the slots' own streams shared the link and all finished late)
   hipStream_t h2d_stream = nullptr;  // created with the context
+  // The split accumulation's side stream: ONE per context, created at the first split.  Splits run
+  // only on calls with no other slot in flight, so one suffices -- and every extra stream takes a
+  // hardware queue: a side stream per slot (17 + 16 queues) oversubscribed the device's queue
+  // slots and the whole 16-slot pipeline ran 180 -> 120 batch-verifies/s (gpurun call r6f)
+  hipStream_t side_stream = nullptr;
   int phase_calls = 0;
   DevBuf table[2], table_base[2];
   bool table_ready[2] = {false, false};
@@ -485,14 +490,15 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   CHK(s.scratch.ensure((size_t)nsets * rb_parts * sizeof(XY)));  // k_reduce_bits partial sums
   CHK(s.winsum.ensure((size_t)nsets * sizeof(XY)));
   CHK(s.res.ensure(2 * sizeof(XY)));
-  if (can_split && !s.side) {  // the side stream at the slot stream's priority, or the device's greatest
+  if (dry) return 0;  // kzgmi_ctx_reserve: workspace sized, nothing enqueued
+  if (split && !c->side_stream) {  // at the slot stream's priority, or the device's greatest
     int prio = 0, least = 0, greatest = 0;
     HIPCHK(hipStreamGetPriority(s.stream, &prio));
     if (c->split_side_prio && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess) prio = greatest;
-    HIPCHK(hipStreamCreateWithPriority(&s.side, hipStreamNonBlocking, prio));
-    for (auto& e : s.side_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipStreamCreateWithPriority(&c->side_stream, hipStreamNonBlocking, prio));
   }
-  if (dry) return 0;  // kzgmi_ctx_reserve: workspace sized, nothing enqueued
+  if (split && !s.side_ev[0])
+    for (auto& e : s.side_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   Roctx rx("kzgmi.msm.sort+accumulate+reduce+combine");
   hipStream_t st = s.stream;
   using L = Launch<Cv>;
@@ -531,8 +537,9 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
                   s.skey.template as<uint32_t>(), s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts, acc,
                   NB, acc_threads, acc_threads ? s.accq.template as<uint32_t>() : nullptr, crowd_a, mid,
                   c->split_side_fix ? nullptr : st);
+    hipStream_t sd = c->side_stream;
     HIPCHK(hipEventRecord(s.side_ev[0], st));
-    HIPCHK(hipStreamWaitEvent(s.side, s.side_ev[0], 0));
+    HIPCHK(hipStreamWaitEvent(sd, s.side_ev[0], 0));
     L::accumulate(st, nchunks_b, mid, s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
                   s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts, acc, nb_b, acc_threads_b,
                   acc_threads_b ? s.accq.template as<uint32_t>() : nullptr, crowd_b, nullptr, st);
@@ -541,17 +548,17 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
     // records, R / U+V records, bit sums and window sums at the offsets of its sets
     const bool lowp = c->split_low_prio;
     if (c->split_side_fix)
-      L::fixup(s.side, nchunks, s.total.template as<uint32_t>(), s.skey.template as<uint32_t>(),
+      L::fixup(sd, nchunks, s.total.template as<uint32_t>(), s.skey.template as<uint32_t>(),
                s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), acc, NB, crowd_a, mid);
     const size_t nseg = nbuckets / SEG;
     uint32_t* R29 = s.R.template as<uint32_t>();
     uint32_t* U29 = s.U.template as<uint32_t>();
-    L::reduce(s.side, hn, s.cnt.template as<uint32_t>() + (size_t)h * nbuckets, acc + (size_t)h * nbuckets * W29,
+    L::reduce(sd, hn, s.cnt.template as<uint32_t>() + (size_t)h * nbuckets, acc + (size_t)h * nbuckets * W29,
               reinterpret_cast<XY*>(R29 + h * nseg * W29), reinterpret_cast<XY*>(U29 + 2 * h * nseg * W29),
               s.scratch.template as<XY>() + (size_t)h * rb_parts, s.winsum.template as<XY>() + h, wbits, lowp);
-    L::window_combine(s.side, MsmWindows{1, {h, 0}, {mw.nwin[1], 0}}, s.winsum.template as<XY>(),
+    L::window_combine(sd, MsmWindows{1, {h, 0}, {mw.nwin[1], 0}}, s.winsum.template as<XY>(),
                       s.res.template as<XY>() + 1, wbits, lowp);
-    HIPCHK(hipEventRecord(s.side_ev[1], s.side));
+    HIPCHK(hipEventRecord(s.side_ev[1], sd));
     mark(c, s, PH_ACCUM + 1);
     L::reduce(st, h, s.cnt.template as<uint32_t>(), acc, s.R.template as<XY>(), s.U.template as<XY>(),
               s.scratch.template as<XY>(), s.winsum.template as<XY>(), wbits);
@@ -1265,6 +1272,10 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
 void kzgmi_ctx_destroy(kzgmi_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  if (c->side_stream) {  // its kernels read slot buffers: drained before any is released
+    (void)hipStreamSynchronize(c->side_stream);
+    (void)hipStreamDestroy(c->side_stream);
+  }
   for (auto& s : c->slots) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     s.for_each_buf([](DevBuf& b) { b.release(); });
@@ -1276,10 +1287,6 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
     for (int b = 0; b < 2; ++b) {
       if (s.ring_ev[b]) (void)hipEventDestroy(s.ring_ev[b]);
       if (s.ring[b]) (void)hipHostFree(s.ring[b]);
-    }
-    if (s.side) {
-      (void)hipStreamSynchronize(s.side);
-      (void)hipStreamDestroy(s.side);
     }
     for (auto& e : s.side_ev)
       if (e) (void)hipEventDestroy(e);
@@ -1294,6 +1301,7 @@ void kzgmi_ctx_destroy(kzgmi_ctx* c) {
     (void)hipStreamSynchronize(c->h2d_stream);
     (void)hipStreamDestroy(c->h2d_stream);
   }
+
   c->lines_tmp.release();
   c->tmp.release();
   for (kzgmi_ck* ck : c->ck_list) {  // detach: later kzgmi_ck_free() only deletes the struct
