@@ -383,8 +383,9 @@ int kzgmi_set_glv(kzgmi_ctx* ctx, int msm, int batch);
 int kzgmi_set_trusted_g1(kzgmi_ctx* ctx, int on);
 /* Split accumulation of a batch's two MSMs (latency): MSM#1's bucket sets accumulate first and
  * its reduction + window combination run on a side stream beside MSM#0's accumulation.
- * mode -1 (default): synchronous-sized calls of >= 2^25 window entries with no other slot in
- * flight; 0: never (the single-launch form pipelined calls always use); 1: every two-MSM call.
+ * mode -1 (default): calls of >= 2^25 window entries whose second MSM has more windows (no GLV)
+ * and no other slot in flight; 0: never (the single-launch form pipelined calls always use);
+ * 1: every two-MSM call.
  * Results are identical either way.  Not allowed while jobs are in flight. */
 int kzgmi_set_split_acc(kzgmi_ctx* ctx, int mode);
 

@@ -458,7 +458,11 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   const uint32_t split_set = mw.nmsm == 2 ? mw.set_base[1] : 0;
   const bool can_split = part == 0 && mw.set_base[0] == 0 && split_set > 0 && split_set + mw.nwin[1] == nsets &&
                          mw.nwin[0] == split_set && c->split_acc != 0;
-  const bool split = can_split && (c->split_acc > 0 || (alone && emax >= kzgmi_ctx::SPLIT_FROM));
+  // auto: only where the second MSM's tail is the longer one (BLS12-381 without GLV: 16 windows
+  // against 8).  GLV batches (BN254, trusted BLS12-381 points) have 8 windows in both MSMs: the
+  // split only adds its side-stream contention (BN254 2^22: 14.70 -> 15.18 ms)
+  const bool split = can_split && (c->split_acc > 0 || (alone && emax >= kzgmi_ctx::SPLIT_FROM &&
+                                                        mw.nwin[1] > mw.nwin[0]));
   const size_t nchunks_b = nchunks, acc_threads_b = acc_threads;  // the second launch's grid
   // pieces: [A's first | A's last | B's first | B's last] when A's joins run on the side stream
   const size_t pieces = can_split && c->split_side_fix ? nchunks + nchunks_b : std::max(nchunks, nchunks_b);
