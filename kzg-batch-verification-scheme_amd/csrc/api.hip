@@ -176,6 +176,9 @@ struct kzgmi_ctx {
   bool split_low_prio = true;    // KZGMI_SPLIT_LOWPRIO: the side stream's kernels without the tail's raised issue priority
   bool split_side_fix = true;    // KZGMI_SPLIT_SIDEFIX: the first launch's piece joins on the side stream
   bool split_side_prio = true;   // KZGMI_SPLIT_SIDEPRIO: the side stream at the device's greatest priority
+  // reduction segments on 4 threads instead of 2 while that grid stays within seg4_waves waves per
+  // SIMD (Launch::reduce; KZGMI_SEG4_WAVES, 0: always 2)
+  int seg4_waves = 1;
   // accumulation order: a slot's k_accumulate waits for the accumulation D launches before it
   // (any slot), so at most D run at once and they start in submission order.  Without it 16
   // slots in flight ran their accumulations in bursts and their tails (pairing: one CU) together,
@@ -559,13 +562,14 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
     uint32_t* U29 = s.U.template as<uint32_t>();
     L::reduce(sd, hn, s.cnt.template as<uint32_t>() + (size_t)h * nbuckets, acc + (size_t)h * nbuckets * W29,
               reinterpret_cast<XY*>(R29 + h * nseg * W29), reinterpret_cast<XY*>(U29 + 2 * h * nseg * W29),
-              s.scratch.template as<XY>() + (size_t)h * rb_parts, s.winsum.template as<XY>() + h, wbits, lowp);
+              s.scratch.template as<XY>() + (size_t)h * rb_parts, s.winsum.template as<XY>() + h, wbits, lowp,
+              c->seg4_waves, 4 * c->ncu);
     L::window_combine(sd, MsmWindows{1, {h, 0}, {mw.nwin[1], 0}}, s.winsum.template as<XY>(),
                       s.res.template as<XY>() + 1, wbits, lowp);
     HIPCHK(hipEventRecord(s.side_ev[1], sd));
     mark(c, s, PH_ACCUM + 1);
     L::reduce(st, h, s.cnt.template as<uint32_t>(), acc, s.R.template as<XY>(), s.U.template as<XY>(),
-              s.scratch.template as<XY>(), s.winsum.template as<XY>(), wbits);
+              s.scratch.template as<XY>(), s.winsum.template as<XY>(), wbits, false, c->seg4_waves, 4 * c->ncu);
     mark(c, s, PH_REDUCE + 1);
     L::window_combine(st, MsmWindows{1, {0, 0}, {mw.nwin[0], 0}}, s.winsum.template as<XY>(), s.res.template as<XY>(),
                       wbits);
@@ -588,7 +592,8 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
     return 0;  // more ranges follow
   }
   L::reduce(st, nsets, s.cnt.template as<uint32_t>(), s.acc29.template as<uint32_t>(), s.R.template as<XY>(),
-            s.U.template as<XY>(), s.scratch.template as<XY>(), s.winsum.template as<XY>(), wbits);
+            s.U.template as<XY>(), s.scratch.template as<XY>(), s.winsum.template as<XY>(), wbits, false, c->seg4_waves,
+            4 * c->ncu);
   mark(c, s, PH_REDUCE + 1);
   L::window_combine(st, mw, s.winsum.template as<XY>(), s.res.template as<XY>(), wbits);
   mark(c, s, PH_COMBINE + 1);
@@ -1221,6 +1226,7 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
   if (const char* e = getenv("KZGMI_HOST_CHUNK_MODE")) c->host_chunk_mode = atoi(e);
   if (const char* e = getenv("KZGMI_SPLIT_ACC")) c->split_acc = atoi(e) < 0 ? -1 : std::min(1, atoi(e));
   if (const char* e = getenv("KZGMI_SPLIT_LOWPRIO")) c->split_low_prio = atoi(e) != 0;
+  if (const char* e = getenv("KZGMI_SEG4_WAVES")) c->seg4_waves = std::max(0, atoi(e));
   if (const char* e = getenv("KZGMI_SPLIT_SIDEFIX")) c->split_side_fix = atoi(e) != 0;
   if (const char* e = getenv("KZGMI_SPLIT_SIDEPRIO")) c->split_side_prio = atoi(e) != 0;
   // HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 unless set before the runtime

@@ -39,8 +39,11 @@ struct Launch {
                             const uint32_t* cntb);
   // low_prio: the kernels run at normal issue priority instead of the tail's raised one (the
   // side stream of a split accumulation)
+  // seg4_waves: 4 threads per reduction segment when that grid stays within seg4_waves waves per
+  // SIMD of the device's `simds` (0: always 2 threads)
   static void reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const uint32_t* acc29, XY* R, XY* U,
-                     XY* scratch, XY* winsum, int wbits = WBITS, bool low_prio = false);
+                     XY* scratch, XY* winsum, int wbits = WBITS, bool low_prio = false, int seg4_waves = 0,
+                     int simds = 1024);
   static void window_combine(hipStream_t st, const MsmWindows& mw, const XY* winsum, XY* res, int wbits = WBITS,
                              bool low_prio = false);
   // small calls (msm_small.hpp): one wave per term + a counter tree; res (nmsm records)

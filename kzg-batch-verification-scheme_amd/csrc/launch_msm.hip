@@ -88,16 +88,21 @@ void Launch<Cv>::pts_to29(hipStream_t st, AF* pts, uint32_t n) {
 
 template <class Cv>
 void Launch<Cv>::reduce(hipStream_t st, uint32_t nsets, const uint32_t* cnt, const uint32_t* acc29, XY* R, XY* U,
-                        XY* scratch, XY* winsum, int wbits, bool low_prio) {
+                        XY* scratch, XY* winsum, int wbits, bool low_prio, int seg4_waves, int simds) {
   with_wbits(wbits, [&](auto wb) {
     constexpr int WB = decltype(wb)::value;
     const uint32_t nseg = nsets * Win<WB>::NSEG;
+    // 4 threads per segment while that grid stays within seg4_waves waves per SIMD (few sets: the
+    // segments' serial chains set the time); 2 otherwise (k_reduce_segments4 above)
+    const bool four = seg4_waves > 0 && (size_t)nseg * 4 <= (size_t)seg4_waves * simds * 64;
     auto go = [&](auto lp) {
       constexpr bool LP = decltype(lp)::value;
-      k_reduce_segments<Cv, LP><<<grid_for(2 * (size_t)nseg, 256), 256, 0, st>>>(nseg, cnt, acc29, R, U);  // 2 threads per segment
+      if (four) k_reduce_segments4<Cv, LP><<<grid_for(4 * (size_t)nseg, 256), 256, 0, st>>>(nseg, cnt, acc29, R, U);
+      else k_reduce_segments<Cv, LP><<<grid_for(2 * (size_t)nseg, 256), 256, 0, st>>>(nseg, cnt, acc29, R, U);
       // scratch: nsets * RB_PARTS partial sums
       k_reduce_bits<Cv, WB, LP><<<nsets * Win<WB>::RB_PARTS, 256, 0, st>>>(R, U, scratch);
-      k_reduce_bits_finish<Cv, WB, LP><<<nsets, 64, 0, st>>>(scratch, winsum);
+      if (four) k_reduce_bits_finish<Cv, WB, LP, 4><<<nsets, 64, 0, st>>>(scratch, winsum);
+      else k_reduce_bits_finish<Cv, WB, LP, 2><<<nsets, 64, 0, st>>>(scratch, winsum);
     };
     if (low_prio) go(std::true_type{});
     else go(std::false_type{});
@@ -137,7 +142,7 @@ template void Launch<KZ_CURVE_T>::fixup(hipStream_t, size_t, const uint32_t*, co
                                         const uint32_t*, uint32_t*, uint32_t, uint32_t*, const uint32_t*);
 template void Launch<KZ_CURVE_T>::pts_to29(hipStream_t, Affine<KZ_CURVE_T>*, uint32_t);
 template void Launch<KZ_CURVE_T>::reduce(hipStream_t, uint32_t, const uint32_t*, const uint32_t*, Xyzz<KZ_CURVE_T>*,
-                                         Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, int, bool);
+                                         Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, Xyzz<KZ_CURVE_T>*, int, bool, int, int);
 template void Launch<KZ_CURVE_T>::window_combine(hipStream_t, const MsmWindows&, const Xyzz<KZ_CURVE_T>*,
                                                  Xyzz<KZ_CURVE_T>*, int, bool);
 template void Launch<KZ_CURVE_T>::merge_buckets(hipStream_t, uint32_t, uint32_t*, uint32_t*, const uint32_t*,

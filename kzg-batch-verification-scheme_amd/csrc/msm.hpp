@@ -1305,6 +1305,113 @@ __global__ void __launch_bounds__(256, 2) k_reduce_segments(uint32_t nseg, const
   }
 }
 
+// The same records from 4 threads per segment (lanes 4g .. 4g + 3), for calls with few bucket
+// sets -- the critical path of a split accumulation reduces only MSM#0's 8 sets (api.hip
+// run_msm_core), ~0.5 waves per SIMD with 2 threads per segment, so the segment's serial chain
+// sets the time.  Quarter h runs the running sums over buckets [4h, 4h + 4): r_h = sum_{i<4} i
+// S_{4h+i}, u_h = sum_{i<4} S_{4h+i}; then, with V_3 = u_3, V_2 = u_2 + u_3, V_1 = u_1 + V_2,
+//   sum_i i S_{g SEG + i} = sum_h (r_h + 4 h u_h) = R'_g + 4 V_g,   R'_g = sum_h r_h,
+//   V_g = V_1 + V_2 + V_3,   U_g = u_0 + V_1
+// in three exchange steps of one addition per lane: 7 + 3 serial additions per segment instead
+// of 15 + 1.  The deferred scale of sum V_g is 4 (k_reduce_bits_finish<..., 4>).
+// the value of lane `src` (every lane takes part), word by word so no second whole record is
+// live (the reduction kernels sit at 256 VGPRs)
+template <class Q>
+KZ_DEV X29<Q> x29_from_lane(const X29<Q>& a, int src) {
+  X29<Q> o;
+#pragma unroll
+  for (int k = 0; k < Q::N; ++k) {
+    o.x.v[k] = (uint32_t)__shfl((int)a.x.v[k], src);
+    o.y.v[k] = (uint32_t)__shfl((int)a.y.v[k], src);
+    o.zz.v[k] = (uint32_t)__shfl((int)a.zz.v[k], src);
+    o.zzz.v[k] = (uint32_t)__shfl((int)a.zzz.v[k], src);
+  }
+  o.inf = __shfl((int)a.inf, src) != 0;
+  return o;
+}
+// lane `src`'s a1 where that lane has `c1`, else its a0 -- the select done word by word before the
+// shuffle
+template <class Q>
+KZ_DEV X29<Q> x29_from_lane_sel(bool c1, const X29<Q>& a1, const X29<Q>& a0, int src) {
+  X29<Q> o;
+#pragma unroll
+  for (int k = 0; k < Q::N; ++k) {
+    o.x.v[k] = (uint32_t)__shfl((int)(c1 ? a1.x.v[k] : a0.x.v[k]), src);
+    o.y.v[k] = (uint32_t)__shfl((int)(c1 ? a1.y.v[k] : a0.y.v[k]), src);
+    o.zz.v[k] = (uint32_t)__shfl((int)(c1 ? a1.zz.v[k] : a0.zz.v[k]), src);
+    o.zzz.v[k] = (uint32_t)__shfl((int)(c1 ? a1.zzz.v[k] : a0.zzz.v[k]), src);
+  }
+  o.inf = __shfl((int)(c1 ? a1.inf : a0.inf), src) != 0;
+  return o;
+}
+template <class Q>
+KZ_DEV void x29_swap_if(bool c, X29<Q>& a, X29<Q>& b) {
+#pragma unroll
+  for (int k = 0; k < Q::N; ++k) {
+    uint32_t t = a.x.v[k]; a.x.v[k] = c ? b.x.v[k] : t; b.x.v[k] = c ? t : b.x.v[k];
+    t = a.y.v[k]; a.y.v[k] = c ? b.y.v[k] : t; b.y.v[k] = c ? t : b.y.v[k];
+    t = a.zz.v[k]; a.zz.v[k] = c ? b.zz.v[k] : t; b.zz.v[k] = c ? t : b.zz.v[k];
+    t = a.zzz.v[k]; a.zzz.v[k] = c ? b.zzz.v[k] : t; b.zzz.v[k] = c ? t : b.zzz.v[k];
+  }
+  const bool t = a.inf;
+  a.inf = c ? b.inf : t;
+  b.inf = c ? t : b.inf;
+}
+// each step: one shuffle into b, lanes that add nothing get b = O, then acc += b on every lane
+// (swaps put each lane's addend into acc first)
+template <class Cv, bool LOWP = false>
+__global__ void __launch_bounds__(256, 2) k_reduce_segments4(uint32_t nseg, const uint32_t* __restrict__ cnt,
+                                                          const uint32_t* __restrict__ acc29,
+                                                          Xyzz<Cv>* __restrict__ R, Xyzz<Cv>* __restrict__ U) {
+  static_assert(SEG == 16, "four 4-bucket quarters per segment");
+  if constexpr (!LOWP) KZ_TAIL_PRIO();
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t g = t >> 2, h = t & 3;
+  const int lane = (int)(threadIdx.x & 63u), q0 = lane & ~3;  // the segment's first lane in the wave
+  using Q = Fp29Of<Cv>;
+  const X29<Q> O{F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), F29<Q>::zero(), true};
+  X29<Q> run = O, acc = O;  // u_h, r_h
+  if (g < nseg) {
+    const uint32_t base = g * SEG + 4 * h;
+    for (int i = 3; i >= 1; --i) {
+      if (cnt[base + i]) run = x29_add<Cv, Q>(run, load_x29<Q>(acc29, base + i));
+      acc = x29_add<Cv, Q>(acc, run);
+    }
+    if (cnt[base]) run = x29_add<Cv, Q>(run, load_x29<Q>(acc29, base));
+  }
+  // step 1 -- lane 0: r0 + r1; lane 2: V2 = u2 + u3; lane 3: r3 + r2 (lane 2 holds u2 in acc)
+  x29_swap_if<Q>(h == 2, acc, run);
+  {
+    const int src = q0 + (h == 0 ? 1 : h == 2 ? 3 : h == 3 ? 2 : 1);
+    X29<Q> b = x29_from_lane_sel<Q>(h >= 2, run, acc, src);  // lanes 2, 3 export run (r2, u3)
+    b.inf = b.inf || h == 1;
+    acc = x29_add<Cv, Q>(acc, b);
+  }
+  // step 2 -- lane 0: R' = (r0 + r1) + (r2 + r3); lane 1: V1 = u1 + V2; lane 3: V2 + V3 = u3 + V2
+  {
+    const int src = q0 + (h == 0 ? 3 : 2);
+    X29<Q> b = x29_from_lane<Q>(acc, src);
+    b.inf = b.inf || h == 2;
+    x29_swap_if<Q>((h & 1) != 0, acc, run);  // lanes 1, 3 add into u1, u3
+    acc = x29_add<Cv, Q>(acc, b);
+  }
+  // step 3 -- lane 0: U = u0 + V1; lane 1: V = V1 + (V2 + V3)
+  {
+    const int src = q0 + (h == 0 ? 1 : 3);
+    X29<Q> b = x29_from_lane<Q>(acc, src);
+    b.inf = b.inf || h >= 2;
+    x29_swap_if<Q>(h == 0, acc, run);  // lane 0: acc = u0, run = R'
+    acc = x29_add<Cv, Q>(acc, b);
+  }
+  if (g >= nseg) return;
+  if (h == 0) {
+    store_x29<Q>(reinterpret_cast<uint32_t*>(R), g, run);
+    store_x29<Q>(reinterpret_cast<uint32_t*>(U), g, acc);
+  } else if (h == 1) {
+    store_x29<Q>(reinterpret_cast<uint32_t*>(U), (size_t)nseg + g, acc);  // V_g
+  }
+}
+
 // Window sums with a short dependency chain (~40 point operations per set; the earlier one
 // workgroup per set with three serial 16-term segment levels needed ~130, 3.8 vs 1.2 ms):
 //   W = sum_g (R'_g + U_g) + 8 sum_g V_g + SEG * sum_g g U_g,   sum_g g U_g = sum_j 2^j B_j,
@@ -1442,9 +1549,12 @@ __global__ void __launch_bounds__(256) k_reduce_bits(const Xyzz<Cv>* __restrict_
 // One wave per set, lane-parallel arithmetic (lpfield.hpp): Horner over the bit sums (c = 16:
 // 10 XYZZ doublings + 10 additions), the 4 quarter sums, 4 doublings -- ~80 row-parallel
 // product steps instead of ~330 serial products on one lane (0.71 ms before).
-template <class Cv, int WB = WBITS, bool LOWP = false>
+// SEGT: threads per segment of the records (k_reduce_segments: 2, sum V scaled by 8;
+// k_reduce_segments4: 4, scaled by 4)
+template <class Cv, int WB = WBITS, bool LOWP = false, int SEGT = 2>
 __global__ void __launch_bounds__(64) k_reduce_bits_finish(const Xyzz<Cv>* __restrict__ parts,
                                                            Xyzz<Cv>* __restrict__ winsum) {
+  static_assert(SEGT == 2 || SEGT == 4, "segment threads");
   if constexpr (!LOWP) KZ_TAIL_PRIO();
   using Wn = Win<WB>;
   constexpr int SB = Wn::SEG_BITS;
@@ -1456,10 +1566,11 @@ __global__ void __launch_bounds__(64) k_reduce_bits_finish(const Xyzz<Cv>* __res
   for (int j = SB - 2; j >= 0; --j) V = lp_xyzz_add(c, lp_xyzz_dbl(c, V), lp_load_xyzz(c, &P[j]));
   LpXyzz<Cv> W = lp_xyzz_add(c, lp_xyzz_add(c, lp_load_xyzz(c, &P[SB]), lp_load_xyzz(c, &P[SB + 1])),
                              lp_xyzz_add(c, lp_load_xyzz(c, &P[SB + 2]), lp_load_xyzz(c, &P[SB + 3])));
-  // 16 H + 8 sum V = 8 (2 H + sum V)
+  // 2 threads per segment: 16 H + 8 sum V = 8 (2 H + sum V); 4: 16 H + 4 sum V = 4 (4 H + sum V)
+  if constexpr (SEGT == 4) V = lp_xyzz_dbl(c, V);
   V = lp_xyzz_add(c, lp_xyzz_dbl(c, V), lp_xyzz_add(c, lp_load_xyzz(c, &P[SB + 4]), lp_load_xyzz(c, &P[SB + 5])));
 #pragma unroll 1
-  for (int i = 0; i < 3; ++i) V = lp_xyzz_dbl(c, V);
+  for (int i = 0; i < (SEGT == 4 ? 2 : 3); ++i) V = lp_xyzz_dbl(c, V);
   lp_store_xyzz(c, &winsum[set], lp_xyzz_add(c, W, V));
 }
 
