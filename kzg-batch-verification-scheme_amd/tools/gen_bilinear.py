@@ -489,7 +489,7 @@ def selfcheck(cv, tables):
 
 # ----------------------------------------------------------------------------- pairing bytecode
 # Register file (in Fp units, LDS): [K consts 36][E lines NL*12][P 6][SCAL 4][G0..G15 x 12]
-K_ROUND, K_ROUND2, K_COPY, K_INV = 0, 1, 2, 3
+K_ROUND, K_ROUND2, K_COPY, K_INV, K_CYCRUN = 0, 1, 2, 3, 4
 OPNUM = {name: i for i, (name, _) in enumerate(OPS)}
 NONE = 0xFFFF
 LOOP = {"bls12_381": 0xD201000000010000, "bn254": 6 * 4965661367192848881 + 2}
@@ -706,6 +706,40 @@ def build_program(cv):
     return P, res
 
 
+def compress_cyc_runs(P):
+    """Runs of >= 2 chained cyclotomic squarings (cyclo_pow's zero digits: s0 -> u, u -> v, v -> u,
+    ...) become one K_CYCRUN [4, n, s0, u, v]: the interpreter runs the n rounds back to back
+    without decoding each (pairing_par.hpp)."""
+    cyc = OPNUM["CYC"]
+    out, i = [], 0
+    code = P.code
+    while i < len(code):
+        ins = code[i]
+        if ins[0] == K_ROUND and ins[1] == cyc:
+            s0, u = ins[2], ins[4]
+            j, cur, other = i + 1, u, None
+            while j < len(code) and code[j][0] == K_ROUND and code[j][1] == cyc and code[j][2] == cur:
+                o = code[j][4]
+                if other is None:
+                    if o in (cur, s0) and o != s0:
+                        break
+                    if o == cur:
+                        break
+                    other = o
+                elif o != (other if cur == u else u):
+                    break
+                cur = o
+                j += 1
+            n = j - i
+            if n >= 2 and other is not None:
+                out.append([K_CYCRUN, n, s0, u, other, 0, 0, 0, 0, 0])
+                i = j
+                continue
+        out.append(ins)
+        i += 1
+    P.code = out
+
+
 def check_program(cv, tables, P, res):
     """Run the bytecode numerically on random line values and compare with a direct
     evaluation (Miller product over the same lines, naive final exponentiation)."""
@@ -730,6 +764,12 @@ def check_program(cv, tables, P, res):
                 outs.append((o, evaluate(pr, ou, A, B, K, p)))
             for o, vals in outs:
                 R[o:o + len(vals)] = vals
+        elif kind == K_CYCRUN:
+            pr, ou = tables["CYC"]
+            src, dst = ins[2], ins[3]
+            for _ in range(ins[1]):
+                R[dst:dst + 12] = evaluate(pr, ou, R[src:src + 12], [0] * 12, K, p)
+                src, dst = dst, (ins[4] if dst == ins[3] else ins[3])
         elif kind == K_COPY:
             R[ins[4]:ins[4] + 12] = R[ins[2]:ins[2] + 12]
         elif kind == K_INV:
@@ -821,6 +861,9 @@ def emit():
             lines.append("static __constant__ uint16_t %s%s_P[%d] = {%s};" % (pfx, name, max(1, len(pidx)), ", ".join(map(str, pidx or [0]))))
             lines.append("static __constant__ uint16_t %s%s_O[%d] = {%s};" % (pfx, name, len(oidx), ", ".join(map(str, oidx))))
         prog, res = build_program(cv)
+        n_before = len(prog.code)
+        compress_cyc_runs(prog)
+        print("%s: %d instructions, %d after CYC runs" % (cv, n_before, len(prog.code)))
         check_program(cv, tables, prog, res)
         flat = [v for ins in prog.code for v in ins]
         lines.append("static __constant__ uint16_t %sPROG[%d] = {%s};" % (pfx, len(flat), ", ".join(map(str, flat))))

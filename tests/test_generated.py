@@ -69,3 +69,26 @@ def test_bilinear_program_alias_ranges():
         with pytest.raises(AssertionError):
             P.op2("SQR", P.g(0), None, P.g(1), "LL", P.e(0), P.e(0) + 6, P.g(1) + 6)  # outputs overlap
         P.op("MUL", P.g(0), P.g(1), P.g(2))             # disjoint: accepted
+
+
+def test_bilinear_cyc_runs_same_result_and_header_in_sync():
+    """compress_cyc_runs (K_CYCRUN: chained cyclotomic squarings decoded once by the interpreter)
+    leaves the program's result unchanged: check_program runs the compressed bytecode numerically
+    against a direct Miller product + naive final exponentiation, for both curves; and the shipped
+    header holds the compressed programs (NPROG)."""
+    sys.path.insert(0, os.path.join(PKG, "tools"))
+    try:
+        import gen_bilinear as g
+    finally:
+        sys.path.pop(0)
+    with open(os.path.join(PKG, "csrc", "bilinear_gen.hpp")) as f:
+        hdr = f.read()
+    for cv in ("bls12_381", "bn254"):
+        tables = {name: g.build_op(fn, cv) for name, fn in g.OPS}
+        P, res = g.build_program(cv)
+        n0 = len(P.code)
+        g.compress_cyc_runs(P)
+        assert len(P.code) < n0
+        assert any(ins[0] == g.K_CYCRUN for ins in P.code)
+        g.check_program(cv, tables, P, res)
+        assert "NPROG = %d," % len(P.code) in hdr
