@@ -68,8 +68,8 @@ HBM_PEAK = 8.0e12          # B/s, MI355X spec (MI355X_MICROARCH.md)
 TAU = 0x2A1B3C4D5E6F708192A3B4C5D6E7F8091A2B3C4D5E6F7081
 BYTES_PER_TUPLE = {"bls12_381": 256, "bn254": 192}
 BYTES_PER_MSM_POINT = {"bls12_381": 128, "bn254": 96}
-VALU_PER_ADD = 4539  # BLS12-381 k_accumulate, SQ_INSTS_VALU x 64 / 32n (profiles/r05/pmc_sq_accumulate.json)
-PROFILE_ROUND = "r05"      # profiles/<round>/rocprof_single: the committed rocprofv3 summaries
+VALU_PER_ADD = 4528  # BLS12-381 k_accumulate, SQ_INSTS_VALU x 64 / 32n (profiles/r06/pmc_sq_accumulate.json)
+PROFILE_ROUND = "r06"      # profiles/<round>/rocprof_single: the committed rocprofv3 summaries
 
 
 def log(*a):

@@ -1,9 +1,9 @@
 """Summarise tools/prof.sh kernel (rocprofv3 --kernel-trace --stats of non-pipelined single
 batches, tools/phase_timing.py) into profiles/<round>/rocprof_single/: the stats CSV, a top
-list, and kernel_single.json with the average k_accumulate + k_fixup duration that bench.py's
+list, and kernel_single.json with the average k_accumulate + k_fixup + k_fixup_crowded duration that bench.py's
 roofline.kernel_ms (single-batch HIP events around the same two kernels) must agree with.
 
-python3 tools/summarize_single.py gpurun_out/kt_single profiles/r01/rocprof_single
+python3 tools/summarize_single.py gpurun_out/prof_single profiles/r06/rocprof_single [Bn254 "n = 2^22"]
 """
 import csv
 import glob
@@ -13,13 +13,15 @@ import shutil
 import sys
 
 src, dst = sys.argv[1], sys.argv[2]
+CV = sys.argv[3] if len(sys.argv) > 3 else "Bls12_381"  # Bn254 for a BN254 trace
+LABEL = sys.argv[4] if len(sys.argv) > 4 else "n = 2^20"
 os.makedirs(dst, exist_ok=True)
 stats = sorted(glob.glob(os.path.join(src, "**", "*kernel_stats.csv"), recursive=True))[0]
 shutil.copy(stats, os.path.join(dst, "kernel_stats_single_batch.csv"))
 rows = sorted(csv.DictReader(open(stats)), key=lambda r: -float(r["TotalDurationNs"]))
 with open(os.path.join(dst, "kernel_stats_top.txt"), "w") as f:
-    f.write("# rocprofv3 --kernel-trace --stats -- python3 tools/phase_timing.py --reps 4 (n = 2^20 BLS12-381,\n"
-            "# one batch at a time: per-kernel durations without pipeline time-sharing)\n")
+    f.write("# rocprofv3 --kernel-trace --stats -- python3 tools/phase_timing.py --reps 4 (%s %s,\n" % (LABEL, CV))
+    f.write("# one batch at a time: per-kernel durations without pipeline time-sharing)\n")
     f.write("%-70s %8s %14s\n" % ("kernel", "calls", "avg_us"))
     for r in rows[:24]:
         f.write("%-70s %8s %14.1f\n" % (r["Name"][:70], r["Calls"], float(r["AverageNs"]) / 1e3))
@@ -30,13 +32,17 @@ def avg_ns(prefix):
     return float(hit[0]["AverageNs"]) if hit else 0.0
 
 
-acc = avg_ns("void kzgmi::k_accumulate<kzgmi::Bls12_381>")
-fix = avg_ns("void kzgmi::k_fixup<kzgmi::Bls12_381>")
-f29 = avg_ns("void kzgmi::k_from29<kzgmi::Bls12_381>")  # builds before the records fed the reduction directly
-out = {"command": "rocprofv3 --kernel-trace --stats -- python3 tools/phase_timing.py --reps 4 (n = 2^20)",
-       "k_accumulate_avg_ms": acc / 1e6, "k_fixup_avg_ms": fix / 1e6,
+acc = avg_ns("void kzgmi::k_accumulate<kzgmi::%s>" % CV)
+fix = avg_ns("void kzgmi::k_fixup<kzgmi::%s>" % CV)
+# the crowded-bucket joins (msm.hpp k_fixup_crowded, launched behind every k_fixup since round 5)
+crowd = avg_ns("void kzgmi::k_fixup_crowded<kzgmi::%s>" % CV)
+f29 = avg_ns("void kzgmi::k_from29<kzgmi::%s>" % CV)  # builds before the records fed the reduction directly
+out = {"command": "rocprofv3 --kernel-trace --stats -- python3 tools/phase_timing.py --reps 4 (%s, %s)" % (CV, LABEL),
+       "k_accumulate_avg_ms": acc / 1e6, "k_fixup_avg_ms": fix / 1e6, "k_fixup_crowded_avg_ms": crowd / 1e6,
        **({"k_from29_avg_ms": f29 / 1e6} if f29 else {}),
-       "accumulate_phase_avg_ms": (acc + f29 + fix) / 1e6}
+       "accumulate_phase_avg_ms": (acc + f29 + fix + crowd) / 1e6,
+       "accumulate_phase": "k_accumulate + k_fixup + k_fixup_crowded: the kernels between the accumulate "
+                           "phase's two HIP events in csrc/api.hip (bench.py roofline.kernel_ms)"}
 json.dump(out, open(os.path.join(dst, "kernel_single.json"), "w"), indent=1)
 print(json.dumps(out))
 
