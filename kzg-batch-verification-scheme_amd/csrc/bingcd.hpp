@@ -9,7 +9,8 @@
 // in a 2 x 2 matrix of signed factors (|f| + |g| <= 2^K), then applies it once to the N-limb
 // a, b and to the cofactors u, v (the cofactor update divides by 2^K modulo m with one
 // Montgomery-style correction t m).  ceil((2 len(m) - 1) / K) outer steps (26 for a 381-bit
-// modulus, 17 for 254 bits) leave b = gcd = 1 and v = y^-1 mod m.
+// modulus, 17 for 254 bits) leave b = gcd = 1 and v = y^-1 mod m; the loop leaves as soon as a
+// reaches 0.
 //
 // Variable time (the inputs of a verifier are public).  Host + device: tests/test_bingcd.py
 // runs the host build (tools/bingcd_check.cpp) against Python's pow(y, -1, m).
@@ -132,6 +133,10 @@ struct BinGcd {
     const int steps = (2 * len_m - 1 + K - 1) / K;
     for (int it = 0; it < steps; ++it) {
       const int la = bitlen(a), lb = bitlen(b);
+      // a = 0: b = gcd = 1 and every further step keeps v (f0 = 1, g0 = 0, f1 = g1 = 2^K:
+      // u <- u / 2^K, v <- v).  Random 381-bit inputs get there after 17-20 of the 26 steps
+      // (variable time: a verifier's inputs are public)
+      if (la == 0) break;
       int n = la > lb ? la : lb;
       n = n > 2 * K + 2 ? n : 2 * K + 2;
       uint64_t aa = (uint64_t)(a[0] & MASK) | ((uint64_t)bits32(a, n - (K + 2)) << K);
