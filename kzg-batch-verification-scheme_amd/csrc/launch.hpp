@@ -29,7 +29,8 @@ struct Launch {
                          uint32_t* acc29, uint32_t nb, size_t acc_threads, uint32_t* next_chunk, uint32_t* crowd,
                          const uint32_t* lo, hipStream_t fix_st);
   // the piece joins of an accumulation launch (k_fixup, k_fixup_crowded: same nchunks, nb, lo);
-  // accumulate issues them itself on fix_st (nullptr: the caller does, e.g. on another stream).
+  // accumulate issues them itself on fix_st (nullptr: the caller does, e.g. on another stream,
+  // always behind the accumulation launch with the same crowd list, which zeroes it).
   // nb: the record index of the launch's first piece (its pieces follow the nb bucket records)
   static void fixup(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* skey, const uint32_t* off,
                     const uint32_t* cnt, uint32_t* acc29, uint32_t nb, uint32_t* crowd, const uint32_t* lo);

@@ -64,9 +64,9 @@ void Launch<Cv>::accumulate(hipStream_t st, size_t nchunks, const uint32_t* tota
   if (next_chunk && acc_threads && acc_threads < nchunks) {
     (void)hipMemsetAsync(next_chunk, 0, 4, st);
     k_accumulate<Cv><<<grid_for(acc_threads, 256), 256, 0, st>>>(total, sval, skey, off, cnt, pts, acc29, nb,
-                                                                  (uint32_t)(blocks * 256u), next_chunk, lo);
+                                                                  (uint32_t)(blocks * 256u), next_chunk, lo, crowd);
   } else {
-    k_accumulate<Cv><<<blocks, 256, 0, st>>>(total, sval, skey, off, cnt, pts, acc29, nb, 0u, nullptr, lo);
+    k_accumulate<Cv><<<blocks, 256, 0, st>>>(total, sval, skey, off, cnt, pts, acc29, nb, 0u, nullptr, lo, crowd);
   }
   if (fix_st) fixup(fix_st, nchunks, total, skey, off, cnt, acc29, nb, crowd, lo);
 }
@@ -75,7 +75,7 @@ template <class Cv>
 void Launch<Cv>::fixup(hipStream_t st, size_t nchunks, const uint32_t* total, const uint32_t* skey, const uint32_t* off,
                        const uint32_t* cnt, uint32_t* acc29, uint32_t nb, uint32_t* crowd, const uint32_t* lo) {
   const unsigned blocks = grid_for(nchunks, 256);
-  (void)hipMemsetAsync(crowd, 0, 4, st);
+  // crowd: zeroed by the accumulation launch this one follows (k_accumulate)
   k_fixup<Cv><<<blocks, 256, 0, st>>>(total, skey, off, cnt, acc29, nb, crowd, lo);
   // crowded buckets: at most one per FIX_LP_FROM + 1 chunks; 1024 waves stride over the list
   k_fixup_crowded<Cv><<<256, 256, 0, st>>>(crowd, acc29, nb, blocks * 256u);

@@ -1082,7 +1082,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kAccWa
                                                     const Affine<Cv>* __restrict__ pts,
                                                     uint32_t* __restrict__ acc29, uint32_t nb,
                                                     uint32_t nchunks, uint32_t* __restrict__ next_chunk,
-                                                    const uint32_t* __restrict__ lo_p) {
+                                                    const uint32_t* __restrict__ lo_p,
+                                                    uint32_t* __restrict__ crowd) {
+  // the crowded-bucket list k_fixup appends to behind this launch starts empty (a store here
+  // instead of a fill kernel between the two launches)
+  if (crowd && blockIdx.x == 0 && threadIdx.x == 0) *crowd = 0u;
   // the entry range [lo, total) of this launch: the whole sorted list, or the sets of one MSM
   // (api.hip run_msm_core's split accumulation; no bucket crosses a set boundary, so the range
   // end is where the last bucket ends)

@@ -33,7 +33,8 @@ def test_no_stale_ab_knobs():
     allowed = {"KZ_DEV", "KZ_CURVE", "KZ_CURVE_T", "KZ_STR", "KZ_STR2", "KZ_TAIL_PRIO", "KZ_OPS_TABLE", "KZ_ROUTE",
                "KZ_STAMP", "KZ_STAMP_ARG", "KZ_STC", "KZ_PROBE_STAMPS", "KZ_PHASE_STAMPS", "KZ_CALL", "KZ_HD",
                # tuning constants with their shipped default defined in place (#ifndef X / #define X)
-               "KZ_ACC_QUEUE_FACTOR", "KZ_ACC_QUEUE_FROM", "KZ_ACC29_WAVES", "KZ_ACC29_WAVES_BN", "KZ_SGC_WAVES"}
+               "KZ_ACC_QUEUE_FACTOR", "KZ_ACC_QUEUE_FROM", "KZ_ACC29_WAVES", "KZ_ACC29_WAVES_BN", "KZ_SGC_WAVES",
+               "KZ_PAR_THREADS"}
     found = set()
     csrc = os.path.join(PKG, "csrc")
     for f in os.listdir(csrc):
