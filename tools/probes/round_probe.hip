@@ -63,30 +63,35 @@ __global__ void __launch_bounds__(512) k_round(int iters, uint64_t* out, int* si
 
 // MUL-shaped (par_round_fast<MUL>: 54 products on 32 rows, 8-term factor forms and 36-term
 // output forms read from LDS term tables each round, 12 outputs)
-template <int NP, int NO, int WF, int WO>
-__global__ void __launch_bounds__(512) k_round_lds(int iters, uint64_t* out, int* sink) {
+template <int NP, int NO, int WF, int WO, int NT = 512, int NACC = 1>
+__global__ void __launch_bounds__(NT) k_round_lds(int iters, uint64_t* out, int* sink) {
+  constexpr int ROWS = NT / 16;
   __shared__ int32_t R[NR + 64][16];
   __shared__ uint32_t fp[NP][2 * WF];
   __shared__ uint32_t fo[NO][WO];
   const LpCtx<Cv> c = lp_ctx<Cv>();
   const int tid = threadIdx.x, row = tid >> 4, lane = tid & 15;
-  for (int r = row; r < NR + 64; r += 32) R[r][lane] = lane < 13 ? (int32_t)((0x9E3779B9u * (r * 16 + lane + 1)) & LP_M29) : 0;
-  for (int i = tid; i < NP * 2 * WF; i += 512) fp[i / (2 * WF)][i % (2 * WF)] = (uint32_t)((i * 7) % NR) | (uint32_t)(((i % 3) - 1) & 0xff) << 24;
-  for (int i = tid; i < NO * WO; i += 512) fo[i / WO][i % WO] = (uint32_t)(NR + (i * 5) % NP) | (uint32_t)(((i % 3) - 1) & 0xff) << 24;
+  for (int r = row; r < NR + 64; r += ROWS) R[r][lane] = lane < 13 ? (int32_t)((0x9E3779B9u * (r * 16 + lane + 1)) & LP_M29) : 0;
+  for (int i = tid; i < NP * 2 * WF; i += NT) fp[i / (2 * WF)][i % (2 * WF)] = (uint32_t)((i * 7) % NR) | (uint32_t)(((i % 3) - 1) & 0xff) << 24;
+  for (int i = tid; i < NO * WO; i += NT) fo[i / WO][i % WO] = (uint32_t)(NR + (i * 5) % NP) | (uint32_t)(((i % 3) - 1) & 0xff) << 24;
   __syncthreads();
   auto terms = [&](const uint32_t* t, int W) {
-    int64_t a = 0;
+    int64_t a[NACC] = {};
+#pragma unroll
     for (int q = 0; q < W; q += 4) {
       const uint4 v = *reinterpret_cast<const uint4*>(t + q);
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) lp_mad_i64(a, R[w[k] & 0xffff][lane], (int32_t)w[k] >> 24);
+      for (int k = 0; k < 4; ++k) lp_mad_i64(a[(q + k) % NACC], R[w[k] & 0xffff][lane], (int32_t)w[k] >> 24);
     }
-    return a;
+    int64_t r = a[0];
+#pragma unroll
+    for (int k = 1; k < NACC; ++k) r += a[k];
+    return r;
   };
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   for (int it = 0; it < iters; ++it) {
-    for (int pp = row; pp < NP; pp += 32)
+    for (int pp = row; pp < NP; pp += ROWS)
       R[NR + pp][lane] = lp_mul(c, lp_norm64(c, terms(fp[pp], WF)), lp_norm64(c, terms(fp[pp] + WF, WF)));
     __syncthreads();
     if (row < NO) R[(row * 8) % 48][lane] = lp_reduce(c, lp_norm64(c, terms(fo[row], WO)));
@@ -97,14 +102,14 @@ __global__ void __launch_bounds__(512) k_round_lds(int iters, uint64_t* out, int
   if (R[0][lane] == 0x12345) sink[0] = 1;
 }
 
-template <int NP, int NO, int WF, int WO>
+template <int NP, int NO, int WF, int WO, int NT = 512, int NACC = 1>
 static double run_lds(int iters) {
   uint64_t* out;
   int* sink;
   (void)hipMalloc(&out, 8);
   (void)hipMalloc(&sink, 4);
-  k_round_lds<NP, NO, WF, WO><<<1, 512>>>(4, out, sink);
-  k_round_lds<NP, NO, WF, WO><<<1, 512>>>(iters, out, sink);
+  k_round_lds<NP, NO, WF, WO, NT, NACC><<<1, NT>>>(4, out, sink);
+  k_round_lds<NP, NO, WF, WO, NT, NACC><<<1, NT>>>(iters, out, sink);
   uint64_t cyc = 0;
   (void)hipMemcpy(&cyc, out, 8, hipMemcpyDeviceToHost);
   (void)hipFree(out);
@@ -136,5 +141,16 @@ int main() {
          run_lds<54, 12, 8, 36>(1000));
   printf("CYC-shaped, LDS term tables (18 products, 4-term forms, 12 outputs of 8 terms):  %.0f\n",
          run_lds<18, 12, 4, 8>(1000));
+  // round 6: 16 waves (64 rows, the shipped pairing workgroup) and independent accumulators
+  for (int pass = 0; pass < 2; ++pass) {
+    printf("MUL-shaped 1024 threads, 1 accumulator:  %.0f\n", run_lds<54, 12, 8, 36, 1024, 1>(1000));
+    printf("MUL-shaped 1024 threads, 2 accumulators: %.0f\n", run_lds<54, 12, 8, 36, 1024, 2>(1000));
+    printf("MUL-shaped 1024 threads, 4 accumulators: %.0f\n", run_lds<54, 12, 8, 36, 1024, 4>(1000));
+    printf("MUL-shaped 1024 threads, outputs of 18 terms: %.0f\n", run_lds<54, 12, 8, 18, 1024, 1>(1000));
+    printf("MUL-shaped 1024 threads, outputs of 4 terms:  %.0f\n", run_lds<54, 12, 8, 4, 1024, 1>(1000));
+    printf("MUL-shaped 1024 threads, factor forms of 4 terms: %.0f\n", run_lds<54, 12, 4, 36, 1024, 1>(1000));
+    printf("CYC-shaped LDS 1024 threads, 1 / 2 accumulators: %.0f / %.0f\n", run_lds<18, 12, 4, 8, 1024, 1>(1000),
+           run_lds<18, 12, 4, 8, 1024, 2>(1000));
+  }
   return 0;
 }
