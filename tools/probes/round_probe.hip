@@ -102,6 +102,69 @@ __global__ void __launch_bounds__(NT) k_round_lds(int iters, uint64_t* out, int*
   if (R[0][lane] == 0x12345) sink[0] = 1;
 }
 
+// A CYC chain with the output phase of squaring k run beside the products of squaring k + 1 (rows
+// 32.. vs rows 0..NP-1): the factor forms of k + 1 composed through k's output forms (WF terms over
+// k's products and inputs, reduced before the product), one barrier per squaring
+template <int NP, int NO, int WF, int WO, int NT = 1024>
+__global__ void __launch_bounds__(NT) k_round_comp(int iters, uint64_t* out, int* sink) {
+  constexpr int ROWS = NT / 16;
+  __shared__ int32_t R[NR + 128][16];
+  __shared__ uint32_t fp[NP][2 * WF];
+  __shared__ uint32_t fo[NO][WO];
+  const LpCtx<Cv> c = lp_ctx<Cv>();
+  const int tid = threadIdx.x, row = tid >> 4, lane = tid & 15;
+  for (int r = row; r < NR + 128; r += ROWS) R[r][lane] = lane < 13 ? (int32_t)((0x9E3779B9u * (r * 16 + lane + 1)) & LP_M29) : 0;
+  // factor terms: half products of the previous squaring (rows NR + buf * 64 + u), half inputs
+  for (int i = tid; i < NP * 2 * WF; i += NT)
+    fp[i / (2 * WF)][i % (2 * WF)] = (i & 1 ? (uint32_t)(NR + (i * 5) % NP) | 1u << 16 : (uint32_t)((i * 7) % 48)) |
+                                     (uint32_t)(((i % 3) - 1) & 0xff) << 24;
+  for (int i = tid; i < NO * WO; i += NT)
+    fo[i / WO][i % WO] = (uint32_t)(NR + (i * 5) % NP) | 1u << 16 | (uint32_t)(((i % 3) - 1) & 0xff) << 24;
+  __syncthreads();
+  auto terms = [&](const uint32_t* t, int W, int pb) {
+    int64_t a = 0;
+#pragma unroll
+    for (int q = 0; q < W; q += 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(t + q);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) lp_mad_i64(a, R[(w[k] & 0xffff) + (w[k] >> 16 & 1) * pb][lane], (int32_t)w[k] >> 24);
+    }
+    return a;
+  };
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+    const int pb = (it & 1) * 64, nb = 64 - pb;  // previous products at +pb, this squaring's at +nb
+    if (row < NP) {
+      const int32_t L = lp_reduce(c, lp_norm64(c, terms(fp[row], WF, pb)));
+      const int32_t Rr = lp_reduce(c, lp_norm64(c, terms(fp[row] + WF, WF, pb)));
+      R[NR + nb + row][lane] = lp_mul(c, L, Rr);
+    } else if (row >= 32 && row < 32 + NO) {
+      const int o = row - 32;
+      R[48 + (o * 8 + (it & 1) * 4) % 48][lane] = lp_reduce(c, lp_norm64(c, terms(fo[o], WO, pb)));
+    }
+    __syncthreads();
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (tid == 0) out[0] = t1 - t0;
+  if (R[0][lane] == 0x12345) sink[0] = 1;
+}
+
+template <int NP, int NO, int WF, int WO>
+static double run_comp(int iters) {
+  uint64_t* out;
+  int* sink;
+  (void)hipMalloc(&out, 8);
+  (void)hipMalloc(&sink, 4);
+  k_round_comp<NP, NO, WF, WO><<<1, 1024>>>(4, out, sink);
+  k_round_comp<NP, NO, WF, WO><<<1, 1024>>>(iters, out, sink);
+  uint64_t cyc = 0;
+  (void)hipMemcpy(&cyc, out, 8, hipMemcpyDeviceToHost);
+  (void)hipFree(out);
+  (void)hipFree(sink);
+  return (double)cyc / iters;
+}
+
 template <int NP, int NO, int WF, int WO, int NT = 512, int NACC = 1>
 static double run_lds(int iters) {
   uint64_t* out;
@@ -151,6 +214,8 @@ int main() {
     printf("MUL-shaped 1024 threads, factor forms of 4 terms: %.0f\n", run_lds<54, 12, 4, 36, 1024, 1>(1000));
     printf("CYC-shaped LDS 1024 threads, 1 / 2 accumulators: %.0f / %.0f\n", run_lds<18, 12, 4, 8, 1024, 1>(1000),
            run_lds<18, 12, 4, 8, 1024, 2>(1000));
+    printf("CYC chain, composed factor forms (16 / 24 / 32 terms), outputs beside the next products, one barrier: %.0f / %.0f / %.0f\n",
+           run_comp<18, 12, 16, 8>(1000), run_comp<18, 12, 24, 8>(1000), run_comp<18, 12, 32, 8>(1000));
   }
   return 0;
 }
