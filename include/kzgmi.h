@@ -381,8 +381,9 @@ int kzgmi_probe_fpmul(kzgmi_ctx* ctx, kzgmi_curve curve, double* muls_per_s);
 int kzgmi_set_glv(kzgmi_ctx* ctx, int msm, int batch);
 /* Declare that every point passed to kzgmi_msm_g1* on this context is in G1 (default 0). */
 int kzgmi_set_trusted_g1(kzgmi_ctx* ctx, int on);
-/* Split accumulation of a batch's two MSMs (latency): MSM#1's bucket sets accumulate first and
- * its reduction + window combination run on a side stream beside MSM#0's accumulation.
+/* Split accumulation of a batch's two MSMs (latency): MSM#0's bucket sets accumulate in a first
+ * launch and its reduction + window combination run on a side stream beside MSM#1's launch
+ * (KZGMI_SPLIT_REV=0 in the environment at context creation: MSM#1's sets first instead).
  * mode -1 (default): calls of >= 2^25 window entries whose second MSM has more windows (no GLV)
  * and no other slot in flight; 0: never (the single-launch form pipelined calls always use);
  * 1: every two-MSM call.

@@ -176,6 +176,11 @@ struct kzgmi_ctx {
   bool split_low_prio = true;    // KZGMI_SPLIT_LOWPRIO: the side stream's kernels without the tail's raised issue priority
   bool split_side_fix = true;    // KZGMI_SPLIT_SIDEFIX: the first launch's piece joins on the side stream
   bool split_side_prio = true;   // KZGMI_SPLIT_SIDEPRIO: the side stream at the device's greatest priority
+  // KZGMI_SPLIT_REV: MSM#0's sets (8 windows) in the first launch, its short tail on the side
+  // stream, hidden behind MSM#1's 3x longer launch; MSM#1's tail after it on an idle chip.  0:
+  // MSM#1's first, whose side tail outlasts the short second launch.  2^20: 7.95 vs 7.98 ms
+  // (one launch 8.02; profiles/r06/ab_split_rev.txt)
+  bool split_rev = true;
   // reduction segments on 4 threads instead of 2 while that grid stays within seg4_waves waves per
   // SIMD (Launch::reduce; KZGMI_SEG4_WAVES, 0: always 2)
   int seg4_waves = 1;
@@ -454,10 +459,9 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
     if (nchunks <= cap) acc_threads = 0;
   }
   nchunks = (nchunks + 255) / 256 * 256;  // = the launched thread count (part arrays indexed by thread)
-  // Split accumulation (latency): the second MSM's sets (a suffix of the sets: MSM#1 of a batch)
-  // accumulate first, then the first MSM's; the second MSM's reduction and window combination run
-  // on the slot's side stream beside the first MSM's accumulation, so only the first MSM's
-  // (fewer windows: 8 of a 127-bit randomiser against 16) stay on the critical path.
+  // Split accumulation (latency): the two MSMs' sets (MSM#1's a suffix of the sets) accumulate
+  // in two launches; the first launch's MSM reduces and combines on the slot's side stream beside
+  // the second launch (split_rev: which MSM goes first).
   const uint32_t split_set = mw.nmsm == 2 ? mw.set_base[1] : 0;
   const bool can_split = part == 0 && mw.set_base[0] == 0 && split_set > 0 && split_set + mw.nwin[1] == nsets &&
                          mw.nwin[0] == split_set && c->split_acc != 0;
@@ -538,41 +542,48 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
     uint32_t* crowd_a = s.crowd.template as<uint32_t>();
     uint32_t* crowd_b = crowd_a + crowd_words;
     // launch A's pieces follow the buckets, launch B's follow A's: A's joins may run on the side
-    // stream while B accumulates
+    // stream while B accumulates.  Order: MSM#1's sets [mid, total) first (split_rev 0), or
+    // MSM#0's [0, mid) first (1); the first launch's MSM finishes on the side stream.
+    const bool rev = c->split_rev;
+    const uint32_t* total_a = rev ? mid : s.total.template as<uint32_t>();
+    const uint32_t* lo_a = rev ? nullptr : mid;
+    const uint32_t* total_b = rev ? s.total.template as<uint32_t>() : mid;
+    const uint32_t* lo_b = rev ? mid : nullptr;
     const uint32_t nb_b = c->split_side_fix ? (uint32_t)(NB + 2 * nchunks) : NB;
-    L::accumulate(st, nchunks, s.total.template as<uint32_t>(), s.sval.template as<uint32_t>(),
-                  s.skey.template as<uint32_t>(), s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts, acc,
-                  NB, acc_threads, acc_threads ? s.accq.template as<uint32_t>() : nullptr, crowd_a, mid,
+    L::accumulate(st, nchunks, total_a, s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
+                  s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts, acc, NB, acc_threads,
+                  acc_threads ? s.accq.template as<uint32_t>() : nullptr, crowd_a, lo_a,
                   c->split_side_fix ? nullptr : st);
     hipStream_t sd = c->side_stream;
     HIPCHK(hipEventRecord(s.side_ev[0], st));
     HIPCHK(hipStreamWaitEvent(sd, s.side_ev[0], 0));
-    L::accumulate(st, nchunks_b, mid, s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
+    L::accumulate(st, nchunks_b, total_b, s.sval.template as<uint32_t>(), s.skey.template as<uint32_t>(),
                   s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), pts, acc, nb_b, acc_threads_b,
-                  acc_threads_b ? s.accq.template as<uint32_t>() : nullptr, crowd_b, nullptr, st);
+                  acc_threads_b ? s.accq.template as<uint32_t>() : nullptr, crowd_b, lo_b, st);
     if (order_ev) HIPCHK(hipEventRecord(*order_ev, st));
-    // side: (A's piece joins,) the second MSM's reduction and window combination -- bucket
-    // records, R / U+V records, bit sums and window sums at the offsets of its sets
-    const bool lowp = c->split_low_prio;
-    if (c->split_side_fix)
-      L::fixup(sd, nchunks, s.total.template as<uint32_t>(), s.skey.template as<uint32_t>(),
-               s.off.template as<uint32_t>(), s.cnt.template as<uint32_t>(), acc, NB, crowd_a, mid);
+    // MSM m's reduction and window combination on stream q: bucket records, R / U+V records, bit
+    // sums and window sums at the offsets of its sets
     const size_t nseg = nbuckets / SEG;
     uint32_t* R29 = s.R.template as<uint32_t>();
     uint32_t* U29 = s.U.template as<uint32_t>();
-    L::reduce(sd, hn, s.cnt.template as<uint32_t>() + (size_t)h * nbuckets, acc + (size_t)h * nbuckets * W29,
-              reinterpret_cast<XY*>(R29 + h * nseg * W29), reinterpret_cast<XY*>(U29 + 2 * h * nseg * W29),
-              s.scratch.template as<XY>() + (size_t)h * rb_parts, s.winsum.template as<XY>() + h, wbits, lowp,
-              c->seg4_waves, 4 * c->ncu);
-    L::window_combine(sd, MsmWindows{1, {h, 0}, {mw.nwin[1], 0}}, s.winsum.template as<XY>(),
-                      s.res.template as<XY>() + 1, wbits, lowp);
+    auto tail = [&](hipStream_t q, int m, bool lowp) {
+      const uint32_t s0 = m ? h : 0, ns = m ? hn : h;
+      L::reduce(q, ns, s.cnt.template as<uint32_t>() + (size_t)s0 * nbuckets, acc + (size_t)s0 * nbuckets * W29,
+                reinterpret_cast<XY*>(R29 + s0 * nseg * W29), reinterpret_cast<XY*>(U29 + 2 * s0 * nseg * W29),
+                s.scratch.template as<XY>() + (size_t)s0 * rb_parts, s.winsum.template as<XY>() + s0, wbits, lowp,
+                c->seg4_waves, 4 * c->ncu);
+      if (q == st) mark(c, s, PH_REDUCE + 1);
+      L::window_combine(q, MsmWindows{1, {s0, 0}, {mw.nwin[m], 0}}, s.winsum.template as<XY>(),
+                        s.res.template as<XY>() + m, wbits, lowp);
+    };
+    // side: (A's piece joins,) the first launch's MSM
+    if (c->split_side_fix)
+      L::fixup(sd, nchunks, total_a, s.skey.template as<uint32_t>(), s.off.template as<uint32_t>(),
+               s.cnt.template as<uint32_t>(), acc, NB, crowd_a, lo_a);
+    tail(sd, rev ? 0 : 1, c->split_low_prio);
     HIPCHK(hipEventRecord(s.side_ev[1], sd));
     mark(c, s, PH_ACCUM + 1);
-    L::reduce(st, h, s.cnt.template as<uint32_t>(), acc, s.R.template as<XY>(), s.U.template as<XY>(),
-              s.scratch.template as<XY>(), s.winsum.template as<XY>(), wbits, false, c->seg4_waves, 4 * c->ncu);
-    mark(c, s, PH_REDUCE + 1);
-    L::window_combine(st, MsmWindows{1, {0, 0}, {mw.nwin[0], 0}}, s.winsum.template as<XY>(), s.res.template as<XY>(),
-                      wbits);
+    tail(st, rev ? 1 : 0, false);
     HIPCHK(hipStreamWaitEvent(st, s.side_ev[1], 0));
     mark(c, s, PH_COMBINE + 1);
     HIPCHK(hipGetLastError());
@@ -1229,6 +1240,7 @@ int kzgmi_ctx_create_device(kzgmi_ctx** out, int device_id, int pipeline_slots) 
   if (const char* e = getenv("KZGMI_SEG4_WAVES")) c->seg4_waves = std::max(0, atoi(e));
   if (const char* e = getenv("KZGMI_SPLIT_SIDEFIX")) c->split_side_fix = atoi(e) != 0;
   if (const char* e = getenv("KZGMI_SPLIT_SIDEPRIO")) c->split_side_prio = atoi(e) != 0;
+  if (const char* e = getenv("KZGMI_SPLIT_REV")) c->split_rev = atoi(e) != 0;
   // HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 unless set before the runtime
   // starts) and serialises the streams of one queue, so every slot in flight needs a queue of its
   // own (16 slots on 24 queues pipeline; 24 on 24 ran 3.6x slower).  The runtime keeps that many

@@ -262,12 +262,13 @@ def _context_env(slots, **env):
 
 @pytest.mark.parametrize("curve,log_n", [("bls12_381", 17), ("bls12_381", 20), ("bn254", 17), ("bn254", 20)])
 def test_split_accumulation_vs_oracle(curve, log_n):
-    """The split accumulation (api.hip run_msm_core): MSM#1's bucket sets accumulate in one
-    launch, then MSM#0's in a second one over the sorted range before them, while MSM#1's
+    """The split accumulation (api.hip run_msm_core): MSM#0's bucket sets accumulate in one
+    launch, then MSM#1's in a second one over the sorted range after them, while MSM#0's
     reduction and window combination run on the slot's side stream.  Forced on
     (KZGMI_SPLIT_ACC=1) and off (=0): A, B and the verdict bit-exact vs the oracle, a corrupted
     y flips the verdict; the split with the first launch's piece joins on the slot stream and the
-    side stream at the slot's priority (KZGMI_SPLIT_SIDEFIX=0, KZGMI_SPLIT_SIDEPRIO=0); then the
+    side stream at the slot's priority (KZGMI_SPLIT_SIDEFIX=0, KZGMI_SPLIT_SIDEPRIO=0); the
+    other order (MSM#1's sets first, its tail on the side stream: KZGMI_SPLIT_REV=0); then the
     forced split pipelined on 4 slots with corrupted batches in flight between valid ones (each
     verdict checked)."""
     import torch
@@ -286,7 +287,8 @@ def test_split_accumulation_vs_oracle(curve, log_n):
     assert ok is True
     ybad = y.clone()
     ybad[32 * (n // 3) + 31] ^= 1
-    for env in ({"KZGMI_SPLIT_ACC": "1"}, {"KZGMI_SPLIT_ACC": "0"}, {"KZGMI_SPLIT_ACC": "1", "KZGMI_SPLIT_SIDEFIX": "0", "KZGMI_SPLIT_SIDEPRIO": "0"}):
+    for env in ({"KZGMI_SPLIT_ACC": "1"}, {"KZGMI_SPLIT_ACC": "0"}, {"KZGMI_SPLIT_ACC": "1", "KZGMI_SPLIT_SIDEFIX": "0", "KZGMI_SPLIT_SIDEPRIO": "0"},
+                {"KZGMI_SPLIT_ACC": "1", "KZGMI_SPLIT_REV": "0"}, {"KZGMI_SPLIT_ACC": "1", "KZGMI_SPLIT_REV": "0", "KZGMI_SPLIT_SIDEFIX": "0"}):
         c = _context_env(1, **env)
         try:
             srs = c.load_srs(curve, g2, tg2)
