@@ -384,8 +384,9 @@ int kzgmi_set_trusted_g1(kzgmi_ctx* ctx, int on);
 /* Split accumulation of a batch's two MSMs (latency): MSM#0's bucket sets accumulate in a first
  * launch and its reduction + window combination run on a side stream beside MSM#1's launch
  * (KZGMI_SPLIT_REV=0 in the environment at context creation: MSM#1's sets first instead).
- * mode -1 (default): calls of >= 2^25 window entries whose second MSM has more windows (no GLV)
- * and no other slot in flight; 0: never (the single-launch form pipelined calls always use);
+ * mode -1 (default): synchronous kzgmi_batch_verify_device calls of >= 2^25 window entries whose
+ * second MSM has more windows (no GLV) with no other slot in flight (async calls never split:
+ * the first batch of a pipeline is alone too); 0: never;
  * 1: every two-MSM call.
  * Results are identical either way.  Not allowed while jobs are in flight. */
 int kzgmi_set_split_acc(kzgmi_ctx* ctx, int mode);

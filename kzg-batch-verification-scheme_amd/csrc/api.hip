@@ -181,6 +181,10 @@ struct kzgmi_ctx {
   // MSM#1's first, whose side tail outlasts the short second launch.  2^20: 7.95 vs 7.98 ms
   // (one launch 8.02; profiles/r06/ab_split_rev.txt)
   bool split_rev = true;
+  // set by the synchronous device-buffer call while it enqueues: only such calls split (the first
+  // batch of a pipeline is alone when it is enqueued too, and split it cost the 20-step bench
+  // ~1 ms: its two launches, then a gap while the next batch's front end ran)
+  bool sync_call = false;
   // reduction segments on 4 threads instead of 2 while that grid stays within seg4_waves waves per
   // SIMD (Launch::reduce; KZGMI_SEG4_WAVES, 0: always 2)
   int seg4_waves = 1;
@@ -468,7 +472,7 @@ int run_msm_core(kzgmi_ctx* c, Slot& s, const TermList& tl_in, uint32_t nsets, s
   // auto: only where the second MSM's tail is the longer one (BLS12-381 without GLV: 16 windows
   // against 8).  GLV batches (BN254, trusted BLS12-381 points) have 8 windows in both MSMs: the
   // split only adds its side-stream contention (BN254 2^22: 14.70 -> 15.18 ms)
-  const bool split = can_split && (c->split_acc > 0 || (alone && emax >= kzgmi_ctx::SPLIT_FROM &&
+  const bool split = can_split && (c->split_acc > 0 || (alone && c->sync_call && emax >= kzgmi_ctx::SPLIT_FROM &&
                                                         mw.nwin[1] > mw.nwin[0]));
   const size_t nchunks_b = nchunks, acc_threads_b = acc_threads;  // the second launch's grid
   // pieces: [A's first | A's last | B's first | B's last] when A's joins run on the side stream
@@ -1517,7 +1521,10 @@ int kzgmi_slot_wait(kzgmi_ctx* c, int slot, int* ok_out) {
 int kzgmi_batch_verify_device(kzgmi_ctx* c, const kzgmi_srs* srs, const void* dC, const void* dz, const void* dy,
                               const void* dpi, size_t n, const uint8_t* seed32, int* ok_out) {
   if (!ok_out) return fail(KZGMI_ERR_ARG, "null ok_out");
-  CHK(kzgmi_batch_verify_device_async(c, srs, 0, dC, dz, dy, dpi, n, seed32));
+  c->sync_call = true;
+  const int rc = kzgmi_batch_verify_device_async(c, srs, 0, dC, dz, dy, dpi, n, seed32);
+  c->sync_call = false;
+  CHK(rc);
   return kzgmi_slot_wait(c, 0, ok_out);
 }
 
