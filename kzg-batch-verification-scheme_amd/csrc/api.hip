@@ -166,11 +166,11 @@ struct kzgmi_ctx {
   uint32_t small_terms = 4096;  // calls of at most this many terms: msm_small.hpp (KZGMI_SMALL_TERMS; 0: never)
   int host_chunks_env = 0;       // KZGMI_HOST_CHUNKS: ranges of a synchronous host-buffer batch (batch_host_chunked)
   int host_chunk_mode = 0;       // KZGMI_HOST_CHUNK_MODE=1: shard partials even where one bucket store applies
-  // Split accumulation of two-MSM calls (run_msm_core): -1 calls of at least SPLIT_FROM entries
-  // with no other slot in flight (latency-bound), 0 never, 1 always (KZGMI_SPLIT_ACC).  Single
-  // 2^20 BLS12-381 batches 8.47 -> 8.37 ms; 2^17 ones lose (3.46 -> 3.69 ms: the side work
-  // outlasts the short second launch), so smaller calls keep one launch
-  // (profiles/r06/split_accumulation.txt)
+  // Split accumulation of two-MSM calls (run_msm_core): -1 synchronous device calls of at least
+  // SPLIT_FROM entries with no other slot in flight (latency-bound), 0 never, 1 always
+  // (KZGMI_SPLIT_ACC).  Single 2^20 BLS12-381 batches 8.02 -> 7.95 ms; 2^17 ones lose (2.95 ->
+  // 3.01 ms: the side work outlasts the short second launch), so smaller calls keep one launch
+  // (profiles/r06/split_accumulation.txt, ab_split_rev.txt)
   static constexpr size_t SPLIT_FROM = size_t(1) << 25;
   int split_acc = -1;
   bool split_low_prio = true;    // KZGMI_SPLIT_LOWPRIO: the side stream's kernels without the tail's raised issue priority
